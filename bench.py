@@ -1,0 +1,189 @@
+"""Headline benchmark: SASRec-neg training sequences/sec at B=1024/GPU, L=200, |I|=10M, d=128 (BASELINE.json).
+
+One step = forward + backward + FusedAdam over every parameter (the dense Adam over all 10,000,003 item
+rows included, reference semantics SURVEY Q7) on one synthetic batch that is already resident in HBM.
+    python bench.py                      # N=1, defaults finish in a few minutes
+    torchrun --nproc-per-node N bench.py --gpus N
+Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import __graft_entry__  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="sequences per GPU")
+    ap.add_argument("--seq-len", type=int, default=200)
+    ap.add_argument("--items", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--heads", type=int, default=2)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--dropout", type=float, default=0.2)
+    ap.add_argument("--table-grad", choices=["sparse", "dense"], default="sparse")
+    ap.add_argument("--ids", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
+    ap.add_argument("--cpu-batch", type=int, default=32, help="sequences per CPU-baseline step")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def synthetic_batch(B, L, V, seed, dev, kind="uniform"):
+    """Full-length sequences (no padding): ids ~ U[3, V) (or Zipf(1.07) over item rank), pos = next id,
+    neg ~ U[3, V)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    if kind == "uniform":
+        full = torch.randint(3, V, (B, L + 1), device=dev, generator=g)
+    else:
+        # Zipf(1.07) by inverse-CDF on a truncated harmonic approximation
+        u = torch.rand(B, L + 1, device=dev, generator=g, dtype=torch.float64)
+        a = 1.07
+        n = V - 3
+        hmax = (n ** (1 - a) - 1) / (1 - a)
+        r = ((u * hmax) * (1 - a) + 1) ** (1 / (1 - a))
+        full = (r.long().clamp(1, n) - 1 + 3)
+    g2 = torch.Generator(device=dev).manual_seed(seed + 1)
+    neg = torch.randint(3, V, (B, L), device=dev, generator=g2)
+    return {"item": full[:, :L].contiguous(), "positive_samples": full[:, 1:].contiguous(), "negative_samples": neg}
+
+
+def cpu_baseline(args, V):
+    """CPU oracle (oracle/asme_oracle.py) on the host cores: the same step (fwd+bwd+dense Adam over the
+    full 10M-row table) on a bounded batch sample."""
+    from oracle import asme_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    d, L, N, h = args.dim, args.seq_len, args.layers, args.heads
+    sd = O.init_sasrec_state(V, L, d, N, seed=0)
+    params = [p.requires_grad_(True) for p in sd.values()]
+    opt = torch.optim.Adam(params, lr=1e-3, betas=(0.99, 0.998), weight_decay=1e-3, foreach=False)
+    B = args.cpu_batch
+    batch = synthetic_batch(B, L, V, 1234, torch.device("cpu"))
+    times = []
+    for i in range(1 + args.cpu_steps):
+        t0 = time.perf_counter()
+        O.sasrec_neg_train_step(sd, opt, batch["item"], batch["positive_samples"], batch["negative_samples"], h,
+                                dropout=args.dropout)
+        times.append(time.perf_counter() - t0)
+    per_step = sum(times[1:]) / len(times[1:])
+    cpu_name = platform.processor() or "cpu"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(B / per_step, 3), "unit": "sequences/s", "cores": threads, "kind": "port",
+            "sample": f"SASRec-neg fwd+bwd+dense Adam, B={B} L={L} d={d} |V|={V} (full table), "
+                      f"{args.cpu_steps} timed steps after 1 warm-up, {per_step:.2f} s/step, torch CPU fp32, "
+                      f"{cpu_name}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    asme = __graft_entry__.load_package()
+    V = args.items + 3
+    B, L, d = args.batch, args.seq_len, args.dim
+
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = asme.SASRecModel(transformer_hidden_size=d, num_transformer_heads=args.heads,
+                                 num_transformer_layers=args.layers, item_vocab_size=V, max_seq_length=L,
+                                 transformer_dropout=args.dropout)
+    tok = asme.tokenization.Tokenizer(args.items)
+    module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
+                                                           table_grad=args.table_grad)
+    module.train()
+    opt = module.configure_optimizers()
+    batches = [synthetic_batch(B, L, V, 1234 + 7 * (rank * 2 + i), dev, args.ids) for i in range(2)]
+
+    for i in range(args.warmup):
+        asme.modules.train_step(module, opt, None, batches[i % 2], i)
+    torch.cuda.synchronize()
+
+    # per-kernel device time of the dominant kernel (HIP events on the launching stream)
+    timer = asme._lib.KernelTimer(["asme_adam_rows_step", "asme_attention_fwd", "asme_attention_bwd",
+                                   "asme_embedding_fwd", "asme_embedding_bwd"])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with timer:
+        for i in range(args.steps):
+            asme.modules.train_step(module, opt, None, batches[i % 2], i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = 1000.0 * elapsed / args.steps
+    value = B * world * args.steps / elapsed
+
+    kstats = timer.summary()
+    adam = kstats.get("asme_adam_rows_step")
+    roof = None
+    if adam and adam["count"]:
+        # algorithmic bytes per launch: read+write p, m, v over all V rows (6*V*d*4) + row_slot (V*4)
+        # + the compact gradient rows of the step's unique ids (U*d*4; U <= 3*B*L)
+        U = min(3 * B * L, V)
+        bytes_per = 6 * V * d * 4 + V * 4 + U * d * 4
+        achieved = bytes_per / (adam["avg_ms"] / 1e3) / 1e9
+        roof = {"kernel": "asme_adam_rows_step", "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                "avg_ms": round(adam["avg_ms"], 4), "algorithmic_bytes_per_launch": bytes_per}
+
+    result = {
+        "metric": "training sequences/sec at B=1024 L=200 |I|=10M (SASRec-neg, fwd+bwd+Adam)",
+        "value": round(value, 2), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (uniform ids, random-init weights)",
+        "config": {"workload": "sasrec-neg train step", "model": "SASRec", "global_batch": B * world,
+                   "batch_per_gpu": B, "seq_len": L, "items": args.items, "dim": d, "heads": args.heads,
+                   "layers": args.layers, "dropout": args.dropout, "table_grad": args.table_grad,
+                   "ids": args.ids, "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "roofline": roof,
+        "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kstats.items() if v["count"]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        del model, module, opt, batches
+        torch.cuda.empty_cache()
+        result["cpu_baseline"] = cpu_baseline(args, V)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+/*
+ * asme_mi.h — C ABI of libasme_mi.so: hand-written gfx950 (MI355X / CDNA4) HIP kernels for the
+ * ASME sequential-recommender training/eval hot path.
+ *
+ * The reference (LSX-UniWue/recsys-22-user-attributes-recommender, "ASME") is pure Python on
+ * PyTorch; it has no native FFI.  Each entry point below replaces the stock PyTorch op chain that
+ * the cited reference function executes (paths relative to /root/reference/src/asme).  The Python
+ * host package (recsys-22-user-attributes-recommender_amd/) binds them with ctypes and mirrors the
+ * reference's model/module classes, so ASME's `imports:` plugin mechanism can swap them in
+ * (see INTEGRATION.md).
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers (caller-owned; kernels never allocate or free), except the
+ *     pointer ARRAYS of asme_adam_step, which are host arrays of device pointers.
+ *   - fp32 storage and fp32 arithmetic; ids are int64; masks are uint8 (0 / 1).
+ *   - `stream` is a hipStream_t (NULL = default stream).  Every call is asynchronous and
+ *     stream-ordered; no call synchronises the device.
+ *   - Return value: 0 = OK, -1 = invalid argument, -2 = HIP launch error.  The message of the last
+ *     failure on the calling thread is returned by asme_mi_last_error().
+ *   - Dropout uses a counter-based Philox4x32-10 keyed by (seed, element index), so forward and
+ *     backward regenerate identical masks; p = 0 disables it.
+ */
+#ifndef ASME_MI_H
+#define ASME_MI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------------------------ */
+const char* asme_mi_last_error(void);
+int asme_mi_abi_version(void);
+
+/* ---- embedding (core/models/common/layers/transformer_layers.py:55-80 TransformerEmbedding.forward,
+ *      core/models/kebert4rec/components.py:54-63 PreFusion...forward) ------------------------------
+ * out[t] = drop2( LN2( drop1( LN1( table[ids[t]] + pos_table[t % seq_len] ) ) + extra[t] ) )
+ * Any of pos_table / LN1 (ln1_w,ln1_b) / extra / LN2 may be NULL (identity).  stats: (n_tokens, 4)
+ * = mean1, rstd1, mean2, rstd2 for the backward.  err_flag (nullable) gets bit 0 set on an
+ * out-of-range id (nn.Embedding would raise IndexError). */
+int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
+                       int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float ln1_eps,
+                       float p1, uint64_t seed1, const float* extra, const float* ln2_w, const float* ln2_b,
+                       float ln2_eps, float p2, uint64_t seed2, float* out, float* stats, int* err_flag,
+                       void* stream);
+/* Backward of asme_embedding_fwd: d_rows (n_tokens, dim) = grad wrt (table row + pos row);
+ * d_extra (nullable) = grad wrt extra; partials (n_partials, 4*dim) = per-block sums of
+ * dLN1.w, dLN1.b, dLN2.w, dLN2.b (reduce with asme_reduce_rows). */
+int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
+                       int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float p1,
+                       uint64_t seed1, const float* extra, const float* ln2_w, float p2, uint64_t seed2,
+                       const float* dout, const float* stats, float* d_rows, float* d_extra, float* partials,
+                       int64_t n_partials, void* stream);
+int asme_embedding_bwd_partials_count(void);
+/* nn.Embedding dense backward (autograd embedding_dense_backward): grad[ids[r]] += scale * rows[r]
+ * (hardware fp32 atomics; ids outside [0, vocab) are skipped). */
+int asme_scatter_add_rows(const float* rows, const int64_t* ids, int64_t n_rows, int64_t dim, float* grad,
+                          int64_t vocab, float scale, void* stream);
+/* position-embedding gradient: grad_pos[p] (+)= sum_b rows[b*seq_len + p]; workspace n_chunks*seq_len*dim */
+int asme_position_grad(const float* rows, int64_t batch, int64_t seq_len, int64_t dim, float* workspace,
+                       int64_t n_chunks, float* grad_pos, int accumulate, void* stream);
+/* column sums of a (n_rows, width) matrix: out (+)= sum_r part[r] */
+int asme_reduce_rows(const float* part, int64_t n_rows, int64_t width, float* out, int accumulate, void* stream);
+/* attribute embeddings (core/models/kebert4rec/components.py:15-24; layers.py:15-27 LinearUpscaler):
+ * out[t] (+)= bias + sum_k table[ids[t,k]] (ids == 0 skipped when skip_zero: the pad category) */
+int asme_gather_sum_fwd(const int64_t* ids, int64_t n, int64_t k, int skip_zero, const float* table, int64_t vocab,
+                        int64_t dim, const float* bias, float* out, int accumulate, void* stream);
+int asme_gather_sum_bwd(const float* dout, const int64_t* ids, int64_t n, int64_t k, int skip_zero, float* grad,
+                        int64_t vocab, int64_t dim, void* stream);
+
+/* ---- transformer block pointwise (transformer_layers.py:120-130 SublayerConnection, :251-258
+ *      TransformerBlock, :217-220 PositionwiseFeedForward; ffn_modifier.py:24-26) ---------------- */
+int asme_layernorm_fwd(const float* x, int64_t n_rows, int64_t dim, const float* w, const float* b, float eps,
+                       float* y, float* stats, void* stream);
+int asme_layernorm_bwd(const float* x, int64_t n_rows, int64_t dim, const float* w, const float* stats,
+                       const float* dy, float* dx, int accumulate, float* partials, int64_t n_partials, void* stream);
+/* s = drop_b(res + drop_a(y)); ln_out = LN(s) (LN optional: w == NULL) */
+int asme_residual_ln_fwd(const float* res, const float* y, int64_t n_rows, int64_t dim, float p_a, uint64_t seed_a,
+                         float p_b, uint64_t seed_b, const float* w, const float* b, float eps, float* s_out,
+                         float* ln_out, float* stats, void* stream);
+/* d_res = drop_b'(d_s + LN'(d_ln)); d_y = drop_a'(d_res); partials (n_partials, 2*dim): dLN.w, dLN.b */
+int asme_residual_ln_bwd(const float* s, int64_t n_rows, int64_t dim, float p_a, uint64_t seed_a, float p_b,
+                         uint64_t seed_b, const float* w, const float* stats, const float* d_s, const float* d_ln,
+                         float* d_res, float* d_y, float* partials, int64_t n_partials, void* stream);
+/* y = drop(GELU_erf(x)) elementwise (16-B aligned buffers) */
+int asme_gelu_dropout_fwd(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream);
+int asme_gelu_dropout_bwd(const float* x, const float* dy, int64_t n, float p, uint64_t seed, float* dx,
+                          void* stream);
+
+/* ---- attention (transformer_layers.py:138-155 Attention.forward, :181-199 MultiHeadedAttention;
+ *      core/models/transformer/sequence_representation.py:34-48 mask) -------------------------------
+ * Q/K/V: token-major rows with row strides ld_*; head h = columns [h*head_dim, (h+1)*head_dim).
+ * key_valid (batch, seq_len) uint8 (NULL = all valid); causal = tril mask (SASRec).
+ * Masked scores are exactly -1e9 (reference masked_fill); out (n_tokens, heads*head_dim) with
+ * stride ld_out; lse (batch*heads, seq_len, 2) = (row max, 1/row sum of exp) of the scaled, masked
+ * scores (kept separate so a row with no admissible key keeps its exact 1/L weights).
+ * head_dim in {16, 32, 64, 128}; seq_len <= 1024. */
+int asme_attention_fwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k, int64_t ld_v,
+                       const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
+                       int causal, float scale, float p_drop, uint64_t seed, float* out, int64_t ld_out, float* lse,
+                       void* stream);
+/* dsum_ws: (batch*heads*seq_len) floats of workspace. dq/dk/dv may be column blocks of one buffer. */
+int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k, int64_t ld_v,
+                       const float* out, int64_t ld_out, const float* dout, int64_t ld_dout, const float* lse,
+                       const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
+                       int causal, float scale, float p_drop, uint64_t seed, float* dsum_ws, float* dq, int64_t ld_dq,
+                       float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream);
+
+/* ---- heads & losses -----------------------------------------------------------------------
+ * sampled head (core/models/sasrec/components.py:34-44): pos_out[t] = <hidden[t], table[pos_ids[t]]> */
+int asme_sampled_logits_fwd(const float* hidden, const float* table, const int64_t* pos_ids, const int64_t* neg_ids,
+                            int64_t n_tokens, int64_t dim, int64_t vocab, float* pos_out, float* neg_out,
+                            void* stream);
+/* d_hidden[t] = g_pos[t] table[pos] + g_neg[t] table[neg]; d_table[pos] += g_pos[t] hidden[t] (atomics) */
+int asme_sampled_logits_bwd(const float* hidden, const float* table, const int64_t* pos_ids, const int64_t* neg_ids,
+                            int64_t n_tokens, int64_t dim, int64_t vocab, const float* g_pos, const float* g_neg,
+                            float* d_hidden, float* d_table, void* stream);
+/* SASRec BCE (core/losses/sasrec/sas_rec_losses.py:47-75); out[0] = loss, out[1] = sum(mask);
+ * workspace: 2*n_parts floats */
+int asme_sasrec_bce_fwd(const float* pos_logits, const float* neg_logits, const uint8_t* mask, int64_t n_tokens,
+                        float* workspace, int64_t n_parts, float* out, void* stream);
+int asme_sasrec_bce_bwd(const float* pos_logits, const float* neg_logits, const uint8_t* mask, int64_t n_tokens,
+                        const float* dloss, const float* stats, float* g_pos, float* g_neg, void* stream);
+/* nn.CrossEntropyLoss(ignore_index) mean reduction (masked_training_module.py:93-111,
+ * sas_rec_losses.py:15-32, losses.py:77-115): lse/row_loss (n_rows); out[0] = loss, out[1] = count */
+int asme_cross_entropy_fwd(const float* logits, int64_t ld, const int64_t* targets, int64_t ignore_index,
+                           int64_t n_rows, int64_t n_classes, float* lse, float* row_loss, float* out, void* stream);
+/* dlogits may alias logits (in-place) */
+int asme_cross_entropy_bwd(const float* logits, int64_t ld, const float* lse, const int64_t* targets,
+                           int64_t ignore_index, int64_t n_rows, int64_t n_classes, const float* dloss,
+                           const float* stats, float* dlogits, int64_t ld_dlogits, void* stream);
+/* ranking (core/metrics/common.py:4-27 get_true_positives): 1-based rank of targets[r] in row r of
+ * scores, descending, ties broken by lower item id */
+int asme_target_rank(const float* scores, int64_t ld, const int64_t* targets, int64_t n_rows, int64_t n_items,
+                     int64_t* ranks, void* stream);
+
+/* ---- optimizer (torch.optim.Adam as configured in core/modules/*_training_module.py) ---------- */
+int asme_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numels, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int64_t step, void* stream);
+/* dense Adam over a (rows, dim) table whose gradient is row-sparse: row r's gradient is
+ * grad_rows[row_slot[r]] when row_slot[r] >= 0, else 0 (still decayed / L2-coupled like torch) */
+int asme_adam_rows_step(float* param, float* exp_avg, float* exp_avg_sq, int64_t rows, int64_t dim,
+                        const int32_t* row_slot, const float* grad_rows, float lr, float beta1, float beta2,
+                        float eps, float weight_decay, int64_t step, void* stream);
+
+/* ---- id dedup & shard bucketing (row-sharded item table) ------------------------ */
+int64_t asme_dedup_workspace_bytes(int64_t n);
+int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_t* map, void* workspace,
+                   int64_t workspace_bytes, int64_t* unique, int64_t* inverse, int32_t* count, void* stream);
+int asme_dedup_reset(const int64_t* unique, const int32_t* count, int64_t cap, int32_t* map, void* stream);
+int asme_owner_histogram(const int64_t* unique, const int32_t* count, int64_t cap, int world, int32_t* owner,
+                         int32_t* counts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASME_MI_H */

@@ -1,0 +1,144 @@
+"""ctypes binding of libasme_mi.so (include/asme_mi.h).
+
+The product path has exactly one implementation: these HIP kernels.  There is no CPU or
+PyTorch fallback; if the shared library is missing or a tensor is not on a ROCm device the
+call raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ASME_MI_LIB", os.path.join(_HERE, "libasme_mi.so"))
+
+p, i64, i32, f32, u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
+
+# name -> argument types (every function returns int status unless listed in _RESTYPES)
+SIGNATURES = {
+    "asme_mi_last_error": [],
+    "asme_mi_abi_version": [],
+    "asme_embedding_fwd": [p, i64, i64, p, i64, i64, p, p, p, f32, f32, u64, p, p, p, f32, f32, u64, p, p, p, p],
+    "asme_embedding_bwd": [p, i64, i64, p, i64, i64, p, p, p, f32, u64, p, p, f32, u64, p, p, p, p, p, i64, p],
+    "asme_embedding_bwd_partials_count": [],
+    "asme_scatter_add_rows": [p, p, i64, i64, p, i64, f32, p],
+    "asme_position_grad": [p, i64, i64, i64, p, i64, p, i32, p],
+    "asme_reduce_rows": [p, i64, i64, p, i32, p],
+    "asme_gather_sum_fwd": [p, i64, i64, i32, p, i64, i64, p, p, i32, p],
+    "asme_gather_sum_bwd": [p, p, i64, i64, i32, p, i64, i64, p],
+    "asme_layernorm_fwd": [p, i64, i64, p, p, f32, p, p, p],
+    "asme_layernorm_bwd": [p, i64, i64, p, p, p, p, i32, p, i64, p],
+    "asme_residual_ln_fwd": [p, p, i64, i64, f32, u64, f32, u64, p, p, f32, p, p, p, p],
+    "asme_residual_ln_bwd": [p, i64, i64, f32, u64, f32, u64, p, p, p, p, p, p, p, i64, p],
+    "asme_gelu_dropout_fwd": [p, i64, f32, u64, p, p],
+    "asme_gelu_dropout_bwd": [p, p, i64, f32, u64, p, p],
+    "asme_attention_fwd": [p, p, p, i64, i64, i64, p, i64, i64, i64, i64, i32, f32, f32, u64, p, i64, p, p],
+    "asme_attention_bwd": [p, p, p, i64, i64, i64, p, i64, p, i64, p, p, i64, i64, i64, i64, i32, f32, f32, u64, p,
+                           p, i64, p, i64, p, i64, p],
+    "asme_sampled_logits_fwd": [p, p, p, p, i64, i64, i64, p, p, p],
+    "asme_sampled_logits_bwd": [p, p, p, p, i64, i64, i64, p, p, p, p, p],
+    "asme_sasrec_bce_fwd": [p, p, p, i64, p, i64, p, p],
+    "asme_sasrec_bce_bwd": [p, p, p, i64, p, p, p, p, p],
+    "asme_cross_entropy_fwd": [p, i64, p, i64, i64, i64, p, p, p, p],
+    "asme_cross_entropy_bwd": [p, i64, p, p, i64, i64, i64, p, p, p, i64, p],
+    "asme_target_rank": [p, i64, p, i64, i64, p, p],
+    "asme_adam_step": [i32, p, p, p, p, p, f32, f32, f32, f32, f32, i64, p],
+    "asme_adam_rows_step": [p, p, p, i64, i64, p, p, f32, f32, f32, f32, f32, i64, p],
+    "asme_dedup_workspace_bytes": [i64],
+    "asme_dedup_ids": [p, i64, i64, p, p, i64, p, p, p, p],
+    "asme_dedup_reset": [p, p, i64, p, p],
+    "asme_owner_histogram": [p, p, i64, i32, p, p, p],
+}
+_RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class ASMEKernelError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP kernel library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ASMEKernelError(
+            f"libasme_mi.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C recsys-22-user-attributes-recommender_amd/csrc`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    lib = load()
+    return {n for n in SIGNATURES if hasattr(lib, n)}
+
+
+class KernelTimer:
+    """Device time of selected C-ABI calls, measured with HIP events recorded on the launching stream
+    (torch's current stream, which every call uses).  Use as a context manager around a timed region."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.events = {n: [] for n in self.names}
+
+    def __enter__(self):
+        global _TIMER
+        _TIMER = self
+        return self
+
+    def __exit__(self, *exc):
+        global _TIMER
+        _TIMER = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for n, evs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            out[n] = {"count": len(ms), "avg_ms": (sum(ms) / len(ms)) if ms else 0.0, "total_ms": sum(ms)}
+        return out
+
+
+_TIMER: Optional[KernelTimer] = None
+
+
+def call(name: str, *args) -> int:
+    lib = load()
+    timer = _TIMER
+    if timer is not None and name in timer.names:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib, name)(*args)
+        e1.record()
+        timer.events[name].append((e0, e1))
+    else:
+        rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.asme_mi_last_error().decode(errors="replace")
+        raise ASMEKernelError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def ptr(t: Optional[torch.Tensor]):
+    """Device pointer of a tensor (None -> NULL).  Rejects host tensors loudly."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ASMEKernelError(
+            "ASME MI355X kernels need ROCm device tensors; got a CPU tensor (there is no CPU fallback)")
+    return t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream

@@ -1,0 +1,175 @@
+// Fused dense Adam (L2 weight decay coupled into the gradient) over many tensors in one launch.
+//
+// Reference semantics: torch.optim.Adam as configured by
+//   SequenceNextItemPredictionTrainingModule.configure_optimizers
+//       core/modules/sequence_next_item_prediction_training_module.py:181-185   (wd 1e-3)
+//   BaseNextItemPredictionTrainingModule.configure_optimizers
+//       core/modules/next_item_prediction_training_module.py:134-138            (wd 0)
+//   MaskedTrainingModule.configure_optimizers + LambdaLR warmup
+//       core/modules/masked_training_module.py:165-189                          (no wd)
+// Per element (fp32, same operation order as torch's single-tensor Adam):
+//   g  = grad + wd * p
+//   m  = m + (1 - b1) * (g - m)                (lerp)
+//   v  = v * b2 + (1 - b2) * g * g
+//   p  = p + (-step_size) * (m / (sqrt(v) / sqrt(bc2) + eps)),  step_size = lr / bc1
+// Every row of the item table is updated every step: this is the largest HBM stream of the
+// training step (7 x |V| x d x 4 B), so the kernel is a pure float4 streaming pass.
+//
+// The "sparse-gradient" variant takes the table gradient as a compact list of (row, grad-row) pairs
+// (row_slot[r] = index into grad_rows or -1) and applies the exact same dense update (g = 0 + wd*p for
+// rows without a gradient), saving the dense-gradient write/zero/read traffic.
+#include "common.h"
+#include <algorithm>
+#include <cmath>
+
+using namespace asme;
+
+namespace {
+
+constexpr int kMaxTensors = 40;
+constexpr int kChunk = 8192;  // elements per block
+
+struct AdamList {
+    float* p[kMaxTensors];
+    const float* g[kMaxTensors];
+    float* m[kMaxTensors];
+    float* v[kMaxTensors];
+    int64_t n[kMaxTensors];
+    int64_t chunk_start[kMaxTensors + 1];
+    int count;
+};
+
+struct AdamHyper {
+    float b1, b2, one_minus_b1, one_minus_b2, eps, wd, neg_step_size, bc2_sqrt;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamHyper& hp) {
+    if (hp.wd != 0.f) g = g + hp.wd * p;
+    m = m + hp.one_minus_b1 * (g - m);
+    v = v * hp.b2 + hp.one_minus_b2 * g * g;
+    const float denom = sqrtf(v) / hp.bc2_sqrt + hp.eps;
+    p = p + hp.neg_step_size * (m / denom);
+}
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamList L, AdamHyper hp) {
+    const int64_t blk = blockIdx.x;
+    int ti = 0;
+    while (ti + 1 < L.count && L.chunk_start[ti + 1] <= blk) ++ti;
+    const int64_t n = L.n[ti];
+    const int64_t base = (blk - L.chunk_start[ti]) * kChunk;
+    float* __restrict__ p = L.p[ti];
+    const float* __restrict__ g = L.g[ti];
+    float* __restrict__ m = L.m[ti];
+    float* __restrict__ v = L.v[ti];
+    const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+    const int64_t end = min(n, base + kChunk);
+    if (vec) {
+        for (int64_t i = base + 4 * threadIdx.x; i + 3 < end; i += 4 * blockDim.x) {
+            float4 P = *reinterpret_cast<const float4*>(p + i);
+            const float4 G = g ? *reinterpret_cast<const float4*>(g + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 M = *reinterpret_cast<const float4*>(m + i);
+            float4 Vv = *reinterpret_cast<const float4*>(v + i);
+            adam_elem(P.x, G.x, M.x, Vv.x, hp);
+            adam_elem(P.y, G.y, M.y, Vv.y, hp);
+            adam_elem(P.z, G.z, M.z, Vv.z, hp);
+            adam_elem(P.w, G.w, M.w, Vv.w, hp);
+            *reinterpret_cast<float4*>(p + i) = P;
+            *reinterpret_cast<float4*>(m + i) = M;
+            *reinterpret_cast<float4*>(v + i) = Vv;
+        }
+        const int64_t tail = base + ((end - base) / 4) * 4;
+        for (int64_t i = tail + threadIdx.x; i < end; i += blockDim.x) adam_elem(p[i], g ? g[i] : 0.f, m[i], v[i], hp);
+    } else {
+        for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) adam_elem(p[i], g ? g[i] : 0.f, m[i], v[i], hp);
+    }
+}
+
+// dense update of a (rows x D) table whose gradient is given sparsely: row r has gradient
+// grad_rows[row_slot[r]] if row_slot[r] >= 0, else zero.  One thread = 4 consecutive floats.
+__global__ __launch_bounds__(256) void adam_rows_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                        float* __restrict__ v, int64_t rows, int D,
+                                                        const int32_t* __restrict__ row_slot,
+                                                        const float* __restrict__ grad_rows, AdamHyper hp) {
+    const int64_t nvec = rows * D / 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = i * 4;
+        const int64_t r = e / D;
+        const int c = (int)(e - r * D);
+        const int32_t slot = row_slot[r];
+        float4 G = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (slot >= 0) G = *reinterpret_cast<const float4*>(grad_rows + (int64_t)slot * D + c);
+        float4 P = *reinterpret_cast<const float4*>(p + e);
+        float4 M = *reinterpret_cast<const float4*>(m + e);
+        float4 Vv = *reinterpret_cast<const float4*>(v + e);
+        adam_elem(P.x, G.x, M.x, Vv.x, hp);
+        adam_elem(P.y, G.y, M.y, Vv.y, hp);
+        adam_elem(P.z, G.z, M.z, Vv.z, hp);
+        adam_elem(P.w, G.w, M.w, Vv.w, hp);
+        *reinterpret_cast<float4*>(p + e) = P;
+        *reinterpret_cast<float4*>(m + e) = M;
+        *reinterpret_cast<float4*>(v + e) = Vv;
+    }
+}
+
+AdamHyper make_hyper(float lr, float b1, float b2, float eps, float wd, int64_t step) {
+    AdamHyper h;
+    h.b1 = b1;
+    h.b2 = b2;
+    h.one_minus_b1 = 1.f - b1;
+    h.one_minus_b2 = 1.f - b2;
+    h.eps = eps;
+    h.wd = wd;
+    const double bc1 = 1.0 - std::pow((double)b1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)b2, (double)step);
+    h.neg_step_size = (float)(-(double)lr / bc1);
+    h.bc2_sqrt = (float)std::sqrt(bc2);
+    return h;
+}
+
+}  // namespace
+
+ASME_API int asme_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                            float* const* exp_avg_sq, const int64_t* numels, float lr, float beta1, float beta2,
+                            float eps, float weight_decay, int64_t step, void* stream) {
+    ASME_CHECK_ARG(n_tensors >= 0 && params && exp_avg && exp_avg_sq && numels, "asme_adam_step: bad argument");
+    ASME_CHECK_ARG(step >= 1, "asme_adam_step: step must be >= 1");
+    const AdamHyper hp = make_hyper(lr, beta1, beta2, eps, weight_decay, step);
+    int i = 0;
+    while (i < n_tensors) {
+        AdamList L{};
+        int64_t blocks = 0;
+        int c = 0;
+        for (; i < n_tensors && c < kMaxTensors; ++i) {
+            if (numels[i] == 0) continue;
+            L.p[c] = params[i];
+            L.g[c] = grads ? grads[i] : nullptr;
+            L.m[c] = exp_avg[i];
+            L.v[c] = exp_avg_sq[i];
+            L.n[c] = numels[i];
+            L.chunk_start[c] = blocks;
+            blocks += (numels[i] + kChunk - 1) / kChunk;
+            ++c;
+        }
+        L.chunk_start[c] = blocks;
+        L.count = c;
+        if (c == 0) break;
+        hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, L, hp);
+        const int rc = hip_status(hipGetLastError(), "asme_adam_step");
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+ASME_API int asme_adam_rows_step(float* param, float* exp_avg, float* exp_avg_sq, int64_t rows, int64_t dim,
+                                 const int32_t* row_slot, const float* grad_rows, float lr, float beta1, float beta2,
+                                 float eps, float weight_decay, int64_t step, void* stream) {
+    ASME_CHECK_ARG(param && exp_avg && exp_avg_sq && row_slot && grad_rows, "asme_adam_rows_step: null pointer");
+    ASME_CHECK_ARG(dim % 4 == 0 && step >= 1, "asme_adam_rows_step: dim must be a multiple of 4");
+    const AdamHyper hp = make_hyper(lr, beta1, beta2, eps, weight_decay, step);
+    const int64_t nvec = rows * dim / 4;
+    const int64_t blocks = std::min<int64_t>((nvec + 255) / 256, 256 * 32);
+    if (nvec == 0) return 0;
+    hipLaunchKernelGGL(adam_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param, exp_avg,
+                       exp_avg_sq, rows, (int)dim, row_slot, grad_rows, hp);
+    ASME_LAUNCH_CHECK("asme_adam_rows_step");
+}

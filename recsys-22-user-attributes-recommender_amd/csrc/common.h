@@ -1,0 +1,97 @@
+// Shared device helpers for the ASME MI355X (gfx950) kernels.
+// Wave = 64 lanes. All reductions below are full-wave (64-lane) butterflies.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#define ASME_API extern "C" __attribute__((visibility("default")))
+
+namespace asme {
+
+// ------------------------------------------------------------------ status
+void set_error(const std::string& msg);
+int hip_status(hipError_t e, const char* where);
+
+#define ASME_CHECK_ARG(cond, msg)            \
+    do {                                     \
+        if (!(cond)) {                       \
+            ::asme::set_error(msg);          \
+            return -1;                       \
+        }                                    \
+    } while (0)
+
+#define ASME_LAUNCH_CHECK(where) return ::asme::hip_status(hipGetLastError(), where)
+
+// ------------------------------------------------------------------ wave ops
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// reduce over the 4 lane-groups {l, l^16, l^32, l^48} (the MFMA 16x16 "row group" dimension)
+__device__ __forceinline__ float group4_sum(float v) {
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+}
+__device__ __forceinline__ float group4_max(float v) {
+    v = fmaxf(v, __shfl_xor(v, 16, 64));
+    v = fmaxf(v, __shfl_xor(v, 32, 64));
+    return v;
+}
+// reduce over the 16 lanes that share (l >> 4)
+__device__ __forceinline__ float lane16_sum(float v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+        uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+// 4 uniforms in [0,1) for the 4 consecutive elements starting at (idx & ~3) of stream `salt`.
+__device__ __forceinline__ void philox_uniform4(uint64_t seed, uint32_t salt, uint64_t idx4, float u[4]) {
+    u32x4 c{(uint32_t)idx4, (uint32_t)(idx4 >> 32), salt, 0x5851F42Du};
+    u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float s = 5.9604644775390625e-08f;  // 2^-24
+    u[0] = (float)(r.x >> 8) * s;
+    u[1] = (float)(r.y >> 8) * s;
+    u[2] = (float)(r.z >> 8) * s;
+    u[3] = (float)(r.w >> 8) * s;
+}
+// dropout keep-factor for element `idx`: 0 (dropped) or 1/(1-p)
+__device__ __forceinline__ float dropout_factor(uint64_t seed, uint32_t salt, uint64_t idx, float p) {
+    float u[4];
+    philox_uniform4(seed, salt, idx >> 2, u);
+    const uint32_t k = (uint32_t)idx & 3u;
+    const float v = k == 0 ? u[0] : (k == 1 ? u[1] : (k == 2 ? u[2] : u[3]));
+    return v >= p ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    const float pdf = 0.3989422804014327f * expf(-0.5f * x * x);
+    return cdf + x * pdf;
+}
+
+}  // namespace asme

@@ -1,0 +1,411 @@
+// Embedding hot path for ASME on gfx950: fused item-row gather + position add + LayerNorm +
+// dropout (+ side-attribute add + second LayerNorm + dropout), its backward, and the
+// row scatter-add / position / LayerNorm-parameter reductions.
+//
+// Reference semantics (paths relative to /root/reference/src/asme):
+//   TransformerEmbedding.forward      core/models/common/layers/transformer_layers.py:55-80
+//   PreFusionContext...forward        core/models/kebert4rec/components.py:54-63  (second LN)
+//   nn.Embedding backward (dense)     autograd embedding_dense_backward           
+//   LinearUpscaler.forward            core/models/kebert4rec/layers.py:15-27      (gather-sum, A7)
+//
+// Layout: table (V, D) fp32 row-major; tokens t = b*L + s; activations (T, D) fp32.
+// One 64-lane wave owns one token row; lane l holds elements l + 64*j (coalesced 256-B segments).
+#include "common.h"
+
+using namespace asme;
+
+namespace {
+
+constexpr int kWavesPerBlock = 4;
+
+template <int VPL>
+__device__ __forceinline__ void ln_stats(const float (&x)[VPL], int lane, int D, float eps, float& mean,
+                                         float& rstd) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) s += (lane + 64 * j < D) ? x[j] : 0.f;
+    mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const float c = (lane + 64 * j < D) ? x[j] - mean : 0.f;
+        q += c * c;
+    }
+    rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void emb_fwd_kernel(
+    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
+    const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float eps1, float p1,
+    uint64_t s1, const float* __restrict__ extra, const float* __restrict__ w2, const float* __restrict__ b2,
+    float eps2, float p2, uint64_t s2, float* __restrict__ out, float* __restrict__ stats, int* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (t >= T) return;
+    int64_t id = ids[t];
+    if (id < 0 || id >= V) {
+        if (lane == 0 && err) atomicOr(err, 1);
+        id = 0;
+    }
+    const float* row = table + id * D;
+    const float* prow = pos ? pos + (t % L) * D : nullptr;
+    float x[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        x[j] = e < D ? row[e] + (prow ? prow[e] : 0.f) : 0.f;
+    }
+    float m1 = 0.f, r1 = 1.f, m2 = 0.f, r2 = 1.f;
+    if (w1) {
+        ln_stats<VPL>(x, lane, D, eps1, m1, r1);
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            if (e < D) x[j] = (x[j] - m1) * r1 * w1[e] + b1[e];
+        }
+    }
+    if (p1 > 0.f) {
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) x[j] *= dropout_factor(s1, 1u, (uint64_t)t * D + lane + 64 * j, p1);
+    }
+    if (extra) {
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            if (e < D) x[j] += extra[t * D + e];
+        }
+    }
+    if (w2) {
+        ln_stats<VPL>(x, lane, D, eps2, m2, r2);
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            if (e < D) x[j] = (x[j] - m2) * r2 * w2[e] + b2[e];
+        }
+    }
+    if (p2 > 0.f) {
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) x[j] *= dropout_factor(s2, 2u, (uint64_t)t * D + lane + 64 * j, p2);
+    }
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        if (e < D) out[t * D + e] = x[j];
+    }
+    if (lane == 0 && stats) {
+        stats[t * 4 + 0] = m1;
+        stats[t * 4 + 1] = r1;
+        stats[t * 4 + 2] = m2;
+        stats[t * 4 + 3] = r2;
+    }
+}
+
+// LayerNorm input-gradient for one row held by a wave: gx = rstd * (gy*w - mean(gy*w) - xhat*mean(gy*w*xhat))
+template <int VPL>
+__device__ __forceinline__ void ln_bwd_row(const float (&gy)[VPL], const float (&xhat)[VPL], const float* w, float rstd,
+                                           int lane, int D, float (&gx)[VPL]) {
+    float a = 0.f, b = 0.f;
+    float dxh[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        dxh[j] = e < D ? gy[j] * w[e] : 0.f;
+        a += dxh[j];
+        b += dxh[j] * xhat[j];
+    }
+    a = wave_sum(a) / (float)D;
+    b = wave_sum(b) / (float)D;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) gx[j] = rstd * (dxh[j] - a - xhat[j] * b);
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void emb_bwd_kernel(
+    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
+    const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1, uint64_t s1,
+    const float* __restrict__ extra, const float* __restrict__ w2, float p2, uint64_t s2,
+    const float* __restrict__ dout, const float* __restrict__ stats, float* __restrict__ d_rows,
+    float* __restrict__ d_extra, float* __restrict__ partials) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    float acc[4][VPL];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) acc[k][j] = 0.f;
+
+    for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave; t < T; t += (int64_t)gridDim.x * kWavesPerBlock) {
+        int64_t id = ids[t];
+        if (id < 0 || id >= V) id = 0;
+        const float* row = table + id * D;
+        const float* prow = pos ? pos + (t % L) * D : nullptr;
+        const float m1 = stats[t * 4 + 0], r1 = stats[t * 4 + 1], m2 = stats[t * 4 + 2], r2 = stats[t * 4 + 3];
+        float xh1[VPL], f1[VPL], xh2[VPL], g[VPL];
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            const bool ok = e < D;
+            const float x0 = ok ? row[e] + (prow ? prow[e] : 0.f) : 0.f;
+            xh1[j] = ok ? (w1 ? (x0 - m1) * r1 : x0) : 0.f;
+            const float y1 = ok ? (w1 ? xh1[j] * w1[e] + b1[e] : x0) : 0.f;
+            f1[j] = p1 > 0.f ? dropout_factor(s1, 1u, (uint64_t)t * D + e, p1) : 1.f;
+            const float z = y1 * f1[j] + ((extra && ok) ? extra[t * D + e] : 0.f);
+            xh2[j] = ok ? (w2 ? (z - m2) * r2 : z) : 0.f;
+            const float f2 = p2 > 0.f ? dropout_factor(s2, 2u, (uint64_t)t * D + e, p2) : 1.f;
+            g[j] = ok ? dout[t * D + e] * f2 : 0.f;
+        }
+        float gz[VPL];
+        if (w2) {
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) {
+                acc[2][j] += g[j] * xh2[j];
+                acc[3][j] += g[j];
+            }
+            ln_bwd_row<VPL>(g, xh2, w2, r2, lane, D, gz);
+        } else {
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) gz[j] = g[j];
+        }
+        if (d_extra) {
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) {
+                const int e = lane + 64 * j;
+                if (e < D) d_extra[t * D + e] = gz[j];
+            }
+        }
+        float gy1[VPL], gx0[VPL];
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) gy1[j] = gz[j] * f1[j];
+        if (w1) {
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) {
+                acc[0][j] += gy1[j] * xh1[j];
+                acc[1][j] += gy1[j];
+            }
+            ln_bwd_row<VPL>(gy1, xh1, w1, r1, lane, D, gx0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) gx0[j] = gy1[j];
+        }
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            if (e < D) d_rows[t * D + e] = gx0[j];
+        }
+    }
+    if (!partials) return;
+    // block-level reduction of the 4 LayerNorm parameter-gradient accumulators (deterministic order)
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][4][D]
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            if (e < D) red[(wave * 4 + k) * D + e] = acc[k][j];
+        }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 4 * D; c += blockDim.x) {
+        float s = 0.f;
+        for (int w = 0; w < kWavesPerBlock; ++w) s += red[w * 4 * D + c];
+        partials[(int64_t)blockIdx.x * 4 * D + c] = s;
+    }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float* __restrict__ rows,
+                                                               const int64_t* __restrict__ ids, int64_t n, int D,
+                                                               float* __restrict__ grad, int64_t V, float scale) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const int64_t id = ids[r];
+    if (id < 0 || id >= V) return;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        if (e < D) unsafeAtomicAdd(&grad[id * D + e], rows[r * D + e] * scale);
+    }
+}
+
+// sum over the batch of per-token rows -> per-position grad; grid (L, nchunk), partial per chunk
+__global__ __launch_bounds__(256) void pos_partial_kernel(const float* __restrict__ rows, int64_t B, int64_t L, int D,
+                                                          int64_t chunk, float* __restrict__ part) {
+    const int64_t p = blockIdx.x;
+    const int64_t c = blockIdx.y;
+    const int64_t b0 = c * chunk, b1 = min(B, b0 + chunk);
+    for (int e = threadIdx.x; e < D; e += blockDim.x) {
+        float s = 0.f;
+        for (int64_t b = b0; b < b1; ++b) s += rows[(b * L + p) * D + e];
+        part[(c * L + p) * D + e] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int64_t nrows,
+                                                          int64_t width, float* __restrict__ out, int accumulate) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= width) return;
+    float s = 0.f;
+    for (int64_t r = 0; r < nrows; ++r) s += part[r * width + c];
+    out[c] = accumulate ? out[c] + s : s;
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void gather_sum_fwd_kernel(const int64_t* __restrict__ ids, int64_t n, int K,
+                                                             int skip_zero, const float* __restrict__ table,
+                                                             int64_t V, int D, const float* __restrict__ bias,
+                                                             float* __restrict__ out, int accumulate) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (t >= n) return;
+    float x[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        x[j] = (bias && e < D) ? bias[e] : 0.f;
+    }
+    for (int k = 0; k < K; ++k) {
+        const int64_t id = ids[t * K + k];
+        if ((skip_zero && id == 0) || id < 0 || id >= V) continue;
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            if (e < D) x[j] += table[id * D + e];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        if (e < D) out[t * D + e] = accumulate ? out[t * D + e] + x[j] : x[j];
+    }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void gather_sum_bwd_kernel(const float* __restrict__ dout,
+                                                             const int64_t* __restrict__ ids, int64_t n, int K,
+                                                             int skip_zero, float* __restrict__ grad, int64_t V,
+                                                             int D) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (t >= n) return;
+    for (int k = 0; k < K; ++k) {
+        const int64_t id = ids[t * K + k];
+        if ((skip_zero && id == 0) || id < 0 || id >= V) continue;
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const int e = lane + 64 * j;
+            if (e < D) unsafeAtomicAdd(&grad[id * D + e], dout[t * D + e]);
+        }
+    }
+}
+
+inline int vpl_of(int64_t D) { return (int)((D + 63) / 64); }
+
+#define ASME_VPL_DISPATCH(VPLV, ...)                              \
+    switch (VPLV) {                                               \
+        case 1: { constexpr int VPL = 1; __VA_ARGS__; } break;    \
+        case 2: { constexpr int VPL = 2; __VA_ARGS__; } break;    \
+        case 3: { constexpr int VPL = 3; __VA_ARGS__; } break;    \
+        case 4: { constexpr int VPL = 4; __VA_ARGS__; } break;    \
+        case 5: { constexpr int VPL = 5; __VA_ARGS__; } break;    \
+        case 6: { constexpr int VPL = 6; __VA_ARGS__; } break;    \
+        case 7: { constexpr int VPL = 7; __VA_ARGS__; } break;    \
+        case 8: { constexpr int VPL = 8; __VA_ARGS__; } break;    \
+        default: set_error("hidden size must be in [1, 512]"); return -1; \
+    }
+
+}  // namespace
+
+ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
+                                int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
+                                const float* ln1_b, float ln1_eps, float p1, uint64_t seed1, const float* extra,
+                                const float* ln2_w, const float* ln2_b, float ln2_eps, float p2, uint64_t seed2,
+                                float* out, float* stats, int* err_flag, void* stream) {
+    ASME_CHECK_ARG(ids && table && out && stats, "asme_embedding_fwd: null pointer");
+    ASME_CHECK_ARG(dim >= 1 && dim <= 512 && seq_len >= 1 && n_tokens >= 0, "asme_embedding_fwd: bad shape");
+    ASME_CHECK_ARG(p1 >= 0.f && p1 < 1.f && p2 >= 0.f && p2 < 1.f, "asme_embedding_fwd: dropout p must be in [0,1)");
+    if (n_tokens == 0) return 0;
+    const dim3 grid((unsigned)((n_tokens + kWavesPerBlock - 1) / kWavesPerBlock));
+    ASME_VPL_DISPATCH(vpl_of(dim),
+                      hipLaunchKernelGGL(emb_fwd_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, ids, n_tokens,
+                                         seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, ln1_eps, p1, seed1,
+                                         extra, ln2_w, ln2_b, ln2_eps, p2, seed2, out, stats, err_flag));
+    ASME_LAUNCH_CHECK("asme_embedding_fwd");
+}
+
+ASME_API int asme_embedding_bwd_partials_count(void) { return 1024; }
+
+ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
+                                int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
+                                const float* ln1_b, float p1, uint64_t seed1, const float* extra, const float* ln2_w,
+                                float p2, uint64_t seed2, const float* dout, const float* stats, float* d_rows,
+                                float* d_extra, float* partials, int64_t n_partials, void* stream) {
+    ASME_CHECK_ARG(ids && table && dout && stats && d_rows, "asme_embedding_bwd: null pointer");
+    ASME_CHECK_ARG(dim >= 1 && dim <= 512, "asme_embedding_bwd: bad shape");
+    ASME_CHECK_ARG(!partials || n_partials >= 1, "asme_embedding_bwd: n_partials must be >= 1");
+    if (n_tokens == 0) return 0;
+    int64_t nb = (n_tokens + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (partials) nb = n_partials;  // grid-stride; one partial row per block
+    const size_t lds = partials ? (size_t)kWavesPerBlock * 4 * dim * sizeof(float) : 0;
+    ASME_VPL_DISPATCH(vpl_of(dim),
+                      hipLaunchKernelGGL(emb_bwd_kernel<VPL>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream,
+                                         ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1,
+                                         seed1, extra, ln2_w, p2, seed2, dout, stats, d_rows, d_extra, partials));
+    ASME_LAUNCH_CHECK("asme_embedding_bwd");
+}
+
+ASME_API int asme_scatter_add_rows(const float* rows, const int64_t* ids, int64_t n_rows, int64_t dim, float* grad,
+                                   int64_t vocab, float scale, void* stream) {
+    ASME_CHECK_ARG(rows && ids && grad, "asme_scatter_add_rows: null pointer");
+    ASME_CHECK_ARG(dim >= 1 && dim <= 512, "asme_scatter_add_rows: bad shape");
+    if (n_rows == 0) return 0;
+    const dim3 grid((unsigned)((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+    ASME_VPL_DISPATCH(vpl_of(dim), hipLaunchKernelGGL(scatter_add_rows_kernel<VPL>, grid, dim3(256), 0,
+                                                      (hipStream_t)stream, rows, ids, n_rows, (int)dim, grad, vocab,
+                                                      scale));
+    ASME_LAUNCH_CHECK("asme_scatter_add_rows");
+}
+
+ASME_API int asme_position_grad(const float* rows, int64_t batch, int64_t seq_len, int64_t dim, float* workspace,
+                                int64_t n_chunks, float* grad_pos, int accumulate, void* stream) {
+    ASME_CHECK_ARG(rows && workspace && grad_pos && n_chunks >= 1, "asme_position_grad: bad argument");
+    const int64_t chunk = (batch + n_chunks - 1) / n_chunks;
+    hipLaunchKernelGGL(pos_partial_kernel, dim3((unsigned)seq_len, (unsigned)n_chunks), dim3(128), 0,
+                       (hipStream_t)stream, rows, batch, seq_len, (int)dim, chunk, workspace);
+    const int64_t width = seq_len * dim;
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       workspace, n_chunks, width, grad_pos, accumulate);
+    ASME_LAUNCH_CHECK("asme_position_grad");
+}
+
+ASME_API int asme_reduce_rows(const float* part, int64_t n_rows, int64_t width, float* out, int accumulate,
+                              void* stream) {
+    ASME_CHECK_ARG(part && out, "asme_reduce_rows: null pointer");
+    if (width == 0) return 0;
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       part, n_rows, width, out, accumulate);
+    ASME_LAUNCH_CHECK("asme_reduce_rows");
+}
+
+ASME_API int asme_gather_sum_fwd(const int64_t* ids, int64_t n, int64_t k, int skip_zero, const float* table,
+                                 int64_t vocab, int64_t dim, const float* bias, float* out, int accumulate,
+                                 void* stream) {
+    ASME_CHECK_ARG(ids && table && out && k >= 1, "asme_gather_sum_fwd: bad argument");
+    if (n == 0) return 0;
+    const dim3 grid((unsigned)((n + kWavesPerBlock - 1) / kWavesPerBlock));
+    ASME_VPL_DISPATCH(vpl_of(dim), hipLaunchKernelGGL(gather_sum_fwd_kernel<VPL>, grid, dim3(256), 0,
+                                                      (hipStream_t)stream, ids, n, (int)k, skip_zero, table, vocab,
+                                                      (int)dim, bias, out, accumulate));
+    ASME_LAUNCH_CHECK("asme_gather_sum_fwd");
+}
+
+ASME_API int asme_gather_sum_bwd(const float* dout, const int64_t* ids, int64_t n, int64_t k, int skip_zero,
+                                 float* grad, int64_t vocab, int64_t dim, void* stream) {
+    ASME_CHECK_ARG(ids && grad && dout && k >= 1, "asme_gather_sum_bwd: bad argument");
+    if (n == 0) return 0;
+    const dim3 grid((unsigned)((n + kWavesPerBlock - 1) / kWavesPerBlock));
+    ASME_VPL_DISPATCH(vpl_of(dim), hipLaunchKernelGGL(gather_sum_bwd_kernel<VPL>, grid, dim3(256), 0,
+                                                      (hipStream_t)stream, dout, ids, n, (int)k, skip_zero, grad,
+                                                      vocab, (int)dim));
+    ASME_LAUNCH_CHECK("asme_gather_sum_bwd");
+}

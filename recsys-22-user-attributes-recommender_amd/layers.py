@@ -1,0 +1,399 @@
+"""Transformer-recommender building blocks with the reference's module hierarchy and fused forwards.
+
+Attribute names mirror the reference so `state_dict` keys (and therefore checkpoints and the golden
+fixtures) are interchangeable, e.g.
+  _sequence_embedding_layer.item_embedding_layer.item_embedding.embedding.weight
+  _sequence_representation_layer.transformer_layer.transformer_blocks.0.attention.linear_layers.0.weight
+The forward passes do not call the sub-modules one by one: they hand the parameters to the fused
+gfx950 kernels in `ops` (embedding+LN+dropout, attention, residual+dropout+LN, GELU+dropout) and
+use PyTorch (hipBLASLt) only for the plain Linear GEMMs.
+
+Reference classes (paths relative to /root/reference/src/asme):
+  SequenceElementsEmbeddingLayer    core/models/common/layers/sequence_embedding.py:47-93
+  TransformerEmbedding              core/models/common/layers/transformer_layers.py:15-80
+  TransformerLayer / Block / ...    transformer_layers.py:83-258
+  TransformerSequenceRepresentationComponent  core/models/transformer/sequence_representation.py:10-51
+  LinearProjectionLayer / ItemEmbeddingProjectionLayer / build_projection_layer
+                                    core/models/common/layers/layers.py:92-157
+  FFNSequenceRepresentationModifierComponent  core/models/common/components/representation_modifier/ffn_modifier.py
+  PreFusion / PostFusion components, LinearUpscaler  core/models/kebert4rec/{components,layers}.py
+  PostFusionIdentitySequenceRepresentationModifierLayer  core/models/sasrec/components.py:63-106
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import ops
+from .sequence import get_attribute
+
+
+def _p(module: nn.Module, training: bool) -> float:
+    """dropout probability of an nn.Dropout (0 in eval mode / for Identity)."""
+    if not training or not isinstance(module, (nn.Dropout, nn.Dropout2d)):
+        return 0.0
+    return float(module.p)
+
+
+def key_valid_mask(padding_mask: Optional[torch.Tensor], shape) -> Optional[torch.Tensor]:
+    if padding_mask is None:
+        return None
+    return padding_mask.reshape(shape[0], shape[1]).to(torch.uint8).contiguous()
+
+
+# ------------------------------------------------------------------------------------ embeddings
+class SequenceElementsEmbeddingLayer(nn.Module):
+    def __init__(self, item_voc_size: int, embedding_size: int, embedding_pooling_type: Optional[str] = None,
+                 dropout: Optional[float] = None):
+        super().__init__()
+        if embedding_pooling_type:
+            raise NotImplementedError("basket pooling (embedding_pooling_type) is outside the MI355X hot path")
+        self.item_voc_size = item_voc_size
+        self.embedding_size = embedding_size
+        self.embedding_mode = embedding_pooling_type
+        self.dropout = dropout
+        self.pooling = nn.Identity()
+        # NARM's Dropout2d on (N, S, E) drops whole (n, s) positions
+        self.dropout_layer = nn.Dropout2d(p=dropout) if dropout and dropout > 0.0 else nn.Identity()
+        self.embedding = nn.Embedding(num_embeddings=item_voc_size, embedding_dim=embedding_size)
+        self.embedding.weight._asme_table_grad = ops.TableGrad()
+
+    def get_weight(self) -> torch.Tensor:
+        return self.embedding.weight
+
+    def forward(self, items: torch.Tensor, flatten: bool = True) -> torch.Tensor:
+        spec = ops.EmbeddingSpec(seq_len=items.shape[-1] if items.dim() > 1 else max(1, items.numel()),
+                                 table_grad=self.embedding.weight._asme_table_grad)
+        emb = ops.embedding(items, self.embedding.weight, spec=spec)
+        if isinstance(self.dropout_layer, nn.Dropout2d) and self.training:
+            emb = self.dropout_layer(emb)
+        return emb
+
+
+class TransformerEmbedding(nn.Module):
+    def __init__(self, item_voc_size: int, max_seq_len: int, embedding_size: int, dropout: float,
+                 positional_embedding: bool = True, embedding_pooling_type: str = None, norm_embedding: bool = True):
+        super().__init__()
+        self.embedding_size = embedding_size
+        self.positional_embedding_active = positional_embedding
+        self.item_embedding = SequenceElementsEmbeddingLayer(item_voc_size=item_voc_size,
+                                                             embedding_size=embedding_size,
+                                                             embedding_pooling_type=embedding_pooling_type)
+        if self.positional_embedding_active:
+            self.position_embedding = nn.Embedding(max_seq_len, self.embedding_size)
+        self.embedding_norm = nn.LayerNorm(self.embedding_size) if norm_embedding else nn.Identity()
+        self.dropout = nn.Dropout(p=dropout)
+
+    def get_item_embedding_weight(self) -> torch.Tensor:
+        return self.item_embedding.embedding.weight
+
+    def fused_args(self):
+        pos = self.position_embedding.weight if self.positional_embedding_active else None
+        ln1 = (self.embedding_norm.weight, self.embedding_norm.bias) if isinstance(self.embedding_norm,
+                                                                                   nn.LayerNorm) else None
+        eps1 = self.embedding_norm.eps if ln1 is not None else 1e-5
+        return pos, ln1, eps1
+
+    def embed(self, ids: torch.Tensor, extra=None, ln2: Optional[nn.LayerNorm] = None, p2: float = 0.0):
+        """Fused: drop2(LN2(drop1(LN1(E[ids] + P)) + extra)) — transformer_layers.py:55-80
+        (+ kebert4rec/components.py:54-63 when ln2/extra are given)."""
+        pos, ln1, eps1 = self.fused_args()
+        if pos is not None and ids.shape[1] > pos.shape[0]:
+            raise IndexError(f"sequence length {ids.shape[1]} exceeds max_seq_len {pos.shape[0]}")
+        w = self.get_item_embedding_weight()
+        spec = ops.EmbeddingSpec(seq_len=ids.shape[1], ln1_eps=eps1, p1=_p(self.dropout, self.training),
+                                 ln2_eps=ln2.eps if ln2 is not None else 1e-5, p2=p2,
+                                 table_grad=w._asme_table_grad)
+        ln2_t = (ln2.weight, ln2.bias) if ln2 is not None else None
+        return ops.embedding(ids, w, pos, ln1, extra, ln2_t, spec)
+
+    def forward(self, sequence) -> torch.Tensor:
+        return self.embed(sequence.sequence)
+
+
+class LinearUpscaler(nn.Module):
+    """multi-hot(ids) -> Linear(vocab -> d); pad category 0 ignored (kebert4rec/layers.py:15-27)."""
+
+    def __init__(self, vocab_size: int, embed_size: int):
+        super().__init__()
+        self.linear = nn.Linear(vocab_size, embed_size)
+        self.vocab_size = vocab_size
+
+    def forward(self, content_input: torch.Tensor) -> torch.Tensor:
+        table = self.linear.weight.t().contiguous()  # (vocab, d): column gather == row gather
+        return ops.gather_sum(content_input, table, self.linear.bias, skip_zero=True)
+
+
+class _ContentEmbedding(nn.Embedding):
+    """nn.Embedding whose lookup runs on the gather kernel (kebert4rec/components.py:15-24)."""
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        return ops.gather_sum(ids, self.weight, None, skip_zero=False)
+
+
+def build_embedding_type(embedding_type: str, vocab_size: int, hidden_size: int) -> nn.Module:
+    if embedding_type == "content_embedding":
+        return _ContentEmbedding(num_embeddings=vocab_size, embedding_dim=hidden_size)
+    if embedding_type == "linear_upscale":
+        return LinearUpscaler(vocab_size=vocab_size, embed_size=hidden_size)
+    raise KeyError(embedding_type)
+
+
+def _attribute_sum(modules: nn.ModuleDict, sequence) -> Optional[torch.Tensor]:
+    total = None
+    for key, module in modules.items():
+        meta = get_attribute(sequence, key)
+        if meta is None:
+            raise Exception(f"The batch does not contain the following additional metadata: {key}.")
+        e = module(meta)
+        total = e if total is None else total + e
+    return total
+
+
+class PreFusionContextSequenceElementsRepresentationComponent(nn.Module):
+    def __init__(self, item_embedding_layer: TransformerEmbedding, embedding_size: int,
+                 prefusion_attributes: Optional[Dict[str, Dict[str, Any]]],
+                 additional_attributes_tokenizer: Optional[Dict[str, Any]], dropout: float = 0.0):
+        super().__init__()
+        self.item_embedding_layer = item_embedding_layer
+        pre = {}
+        for name, info in (prefusion_attributes or {}).items():
+            vocab = len(additional_attributes_tokenizer["tokenizers." + name])
+            pre[name] = build_embedding_type(info["embedding_type"], vocab, embedding_size)
+        self.prefusion_attribute_embeddings = nn.ModuleDict(pre)
+        self.dropout_embedding = nn.Dropout(dropout)
+        self.norm_embedding = nn.LayerNorm(embedding_size)
+
+    def forward(self, sequence) -> torch.Tensor:
+        extra = _attribute_sum(self.prefusion_attribute_embeddings, sequence)
+        return self.item_embedding_layer.embed(sequence.sequence, extra=extra, ln2=self.norm_embedding,
+                                               p2=_p(self.dropout_embedding, self.training))
+
+
+# ------------------------------------------------------------------------------------ transformer
+class SublayerConnection(nn.Module):
+    def __init__(self, size, dropout):
+        super().__init__()
+        self.norm = nn.LayerNorm(size)
+        self.dropout = nn.Dropout(dropout)
+
+
+class Attention(nn.Module):
+    """parameter-free marker (the computation is ops.attention)"""
+
+
+class MultiHeadedAttention(nn.Module):
+    def __init__(self, heads: int, d_model: int, dropout: float = 0.1):
+        super().__init__()
+        assert d_model % heads == 0
+        self.d_k = d_model // heads
+        self.heads = heads
+        self.linear_layers = nn.ModuleList([nn.Linear(d_model, d_model) for _ in range(3)])
+        self.output_linear = nn.Linear(d_model, d_model)
+        self.attention = Attention()
+        self.dropout = nn.Dropout(p=dropout)
+
+    def qkv_weights(self):
+        w = torch.cat([l.weight for l in self.linear_layers], 0)
+        b = torch.cat([l.bias for l in self.linear_layers], 0)
+        return w, b
+
+
+class PositionwiseFeedForward(nn.Module):
+    def __init__(self, d_model: int, d_ff: int, dropout: float = 0.1):
+        super().__init__()
+        self.w_1 = nn.Linear(d_model, d_ff)
+        self.w_2 = nn.Linear(d_ff, d_model)
+        self.dropout = nn.Dropout(dropout)
+        self.activation = nn.GELU()
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, hidden: int, attn_heads: int, feed_forward_hidden: int, dropout: float,
+                 attention_dropout: float = None):
+        super().__init__()
+        if attention_dropout is None:
+            attention_dropout = dropout
+        self.attention = MultiHeadedAttention(heads=attn_heads, d_model=hidden, dropout=attention_dropout)
+        self.feed_forward = PositionwiseFeedForward(d_model=hidden, d_ff=feed_forward_hidden, dropout=dropout)
+        self.input_sublayer = SublayerConnection(size=hidden, dropout=dropout)
+        self.output_sublayer = SublayerConnection(size=hidden, dropout=dropout)
+        self.dropout = nn.Dropout(p=dropout)
+
+
+class TransformerLayer(nn.Module):
+    def __init__(self, hidden_size: int, num_heads: int, num_layers: int, dim_feedforward: int, dropout: float,
+                 attention_dropout: float = None):
+        super().__init__()
+        self.transformer_blocks = nn.ModuleList(
+            [TransformerBlock(hidden_size, num_heads, dim_feedforward, dropout, attention_dropout=attention_dropout)
+             for _ in range(num_layers)])
+
+    def forward(self, x: torch.Tensor, key_valid: Optional[torch.Tensor], causal: bool) -> torch.Tensor:
+        """N pre-LN blocks (transformer_layers.py:100-106, 120-130, 251-258) on the fused kernels:
+           h1 = x + drop(O(attn(LN_in(x))));  x' = drop(h1 + drop(W2 drop(GELU(W1 LN_out(h1)))))
+        No final LayerNorm after the last block."""
+        blocks = self.transformer_blocks
+        if len(blocks) == 0:
+            return x
+        tr = self.training
+        ln = ops.layer_norm(x, blocks[0].input_sublayer.norm)
+        for i, blk in enumerate(blocks):
+            att, ff = blk.attention, blk.feed_forward
+            w_qkv, b_qkv = att.qkv_weights()
+            qkv = F.linear(ln, w_qkv, b_qkv)
+            o = ops.attention(qkv, key_valid, att.heads, causal, _p(att.dropout, tr))
+            a = F.linear(o, att.output_linear.weight, att.output_linear.bias)
+            h1, ln2 = ops.residual_ln(x, a, blk.output_sublayer.norm, _p(blk.input_sublayer.dropout, tr), 0.0)
+            f = F.linear(ln2, ff.w_1.weight, ff.w_1.bias)
+            g = ops.gelu_dropout(f, _p(ff.dropout, tr))
+            f2 = F.linear(g, ff.w_2.weight, ff.w_2.bias)
+            nxt = blocks[i + 1].input_sublayer.norm if i + 1 < len(blocks) else None
+            x, ln = ops.residual_ln(h1, f2, nxt, _p(blk.output_sublayer.dropout, tr), _p(blk.dropout, tr))
+        return x
+
+
+class TransformerSequenceRepresentationComponent(nn.Module):
+    def __init__(self, transformer_layer: TransformerLayer, bidirectional: bool):
+        super().__init__()
+        self.transformer_layer = transformer_layer
+        self.bidirectional = bidirectional
+
+    def forward(self, embedded: torch.Tensor, padding_mask: Optional[torch.Tensor]) -> torch.Tensor:
+        kv = key_valid_mask(padding_mask, embedded.shape)
+        return self.transformer_layer(embedded, kv, causal=not self.bidirectional)
+
+
+# ------------------------------------------------------------------------------------ modifiers
+class IdentitySequenceRepresentationModifierLayer(nn.Module):
+    def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
+        return encoded
+
+
+class FFNSequenceRepresentationModifierComponent(nn.Module):
+    """LN(GELU(Linear(x))) (ffn_modifier.py:24-26)"""
+
+    def __init__(self, feature_size: int):
+        super().__init__()
+        self.transform = nn.Sequential(nn.Linear(feature_size, feature_size), nn.GELU(), nn.LayerNorm(feature_size))
+
+    def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
+        lin, _, norm = self.transform
+        return ops.layer_norm(ops.gelu_dropout(F.linear(encoded, lin.weight, lin.bias), 0.0), norm)
+
+
+def _merge(x: torch.Tensor, ctx: torch.Tensor, fn: str) -> torch.Tensor:
+    if fn == "add":
+        return x + ctx
+    if fn == "multiply":
+        return x * ctx
+    return x
+
+
+class PostFusionContextSequenceRepresentationModifierComponent(nn.Module):
+    """x (+|*)= sum attr-emb, then Linear -> GELU -> LN (kebert4rec/components.py:65-115)"""
+
+    def __init__(self, feature_size: int, postfusion_attributes, additional_attributes_tokenizer,
+                 merge_function: str = "add"):
+        super().__init__()
+        self.merge_function = merge_function
+        post = {}
+        for name, info in postfusion_attributes.items():
+            vocab = len(additional_attributes_tokenizer["tokenizers." + name])
+            post[name] = build_embedding_type(info["embedding_type"], vocab, feature_size)
+        self.postfusion_attribute_embeddings = nn.ModuleDict(post)
+        self.transform = nn.Sequential(nn.Linear(feature_size, feature_size), nn.GELU(), nn.LayerNorm(feature_size))
+
+    def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
+        x = _merge(encoded, _attribute_sum(self.postfusion_attribute_embeddings, sequence), self.merge_function)
+        lin, _, norm = self.transform
+        return ops.layer_norm(ops.gelu_dropout(F.linear(x, lin.weight, lin.bias), 0.0), norm)
+
+
+class PostFusionIdentitySequenceRepresentationModifierLayer(nn.Module):
+    """x (+|*)= sum attr-emb, no transform (sasrec/components.py:63-106)"""
+
+    def __init__(self, feature_size: int, postfusion_attributes, additional_attributes_tokenizer,
+                 merge_function: str = "add"):
+        super().__init__()
+        self.merge_function = merge_function
+        post = {}
+        for name, info in postfusion_attributes.items():
+            vocab = len(additional_attributes_tokenizer["tokenizers." + name])
+            post[name] = build_embedding_type(info["embedding_type"], vocab, feature_size)
+        self.postfusion_attribute_embeddings = nn.ModuleDict(post)
+
+    def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
+        return _merge(encoded, _attribute_sum(self.postfusion_attribute_embeddings, sequence), self.merge_function)
+
+
+# ------------------------------------------------------------------------------------ projections
+PROJECT_TYPE_LINEAR = "linear"
+
+
+class LinearProjectionLayer(nn.Module):
+    def __init__(self, hidden_size: int, item_vocab_size: int):
+        super().__init__()
+        self.linear = nn.Linear(hidden_size, item_vocab_size)
+
+    def weight_bias(self):
+        return self.linear.weight, self.linear.bias
+
+    def forward(self, representation: torch.Tensor, sequence=None) -> torch.Tensor:
+        return F.linear(representation, self.linear.weight, self.linear.bias)
+
+
+class ItemEmbeddingProjectionLayer(nn.Module):
+    """tied head h E^T + b (layers.py:112-143)"""
+
+    def __init__(self, item_vocab_size: int, embedding: nn.Embedding):
+        super().__init__()
+        self.item_vocab_size = item_vocab_size
+        self.embedding = embedding
+        self.output_bias = nn.Parameter(torch.empty(item_vocab_size))
+        bound = 1 / math.sqrt(item_vocab_size)
+        nn.init.uniform_(self.output_bias, -bound, bound)
+
+    def weight_bias(self):
+        return self.embedding.weight, self.output_bias
+
+    def forward(self, representation: torch.Tensor, sequence=None) -> torch.Tensor:
+        return F.linear(representation, self.embedding.weight, self.output_bias)
+
+
+def build_projection_layer(project_type: str, transformer_hidden_size: int, item_voc_size: int,
+                           embedding: nn.Embedding) -> nn.Module:
+    if project_type == PROJECT_TYPE_LINEAR:
+        return LinearProjectionLayer(transformer_hidden_size, item_voc_size)
+    if project_type == "transpose_embedding":
+        return ItemEmbeddingProjectionLayer(item_voc_size, embedding)
+    raise KeyError(f"{project_type} invalid projection layer")
+
+
+class SASRecProjectionComponent(nn.Module):
+    """sasrec/components.py:14-61: sampled pos/neg dot products (train) or full-catalogue scores of
+    the last valid position (inference)."""
+
+    def __init__(self, embedding: TransformerEmbedding):
+        super().__init__()
+        self.embedding = embedding
+
+    def forward(self, representation: torch.Tensor, sequence) -> Any:
+        pos = get_attribute(sequence, "positive_samples")
+        neg = get_attribute(sequence, "negative_samples")
+        table = self.embedding.get_item_embedding_weight()
+        if neg is not None:
+            return ops.sampled_logits(representation, table, pos, neg, table._asme_table_grad)
+        # inference: H[b, len_b - 1] . E[items]^T
+        mask = sequence.padding_mask
+        idx = mask.sum(-1) - 1
+        last = representation[torch.arange(representation.shape[0], device=representation.device), idx]
+        if pos.dim() == 2 and pos.shape[1] == table.shape[0] and bool(
+                (pos[0] == torch.arange(table.shape[0], device=pos.device)).all()) and bool((pos == pos[0]).all()):
+            return last @ table.t()  # all items, in id order (predict_step's items_to_rank)
+        rows = F.embedding(pos, table)  # (N, I, d)
+        return torch.bmm(rows, last.unsqueeze(-1)).squeeze(-1)

@@ -1,0 +1,302 @@
+"""SASRec / BERT4Rec / KeBERT4Rec / NARM with the reference constructors and forward contract.
+
+Constructor parameter names and defaults equal the reference's, because ASME's GenericModelFactory
+builds models by introspecting `__init__` (core/init/factories/modules/modules.py:116-127):
+  SASRecModel      core/models/sasrec/sasrec_model.py:29-116
+  BERT4RecModel    core/models/bert4rec/bert4rec_model.py:24-68
+  KeBERT4RecModel  core/models/kebert4rec/kebert4rec_model.py:24-89
+  NarmModel        core/models/narm/narm_model.py:25-68 (+ components.py, layers.py)
+`forward(InputSequence) -> Tensor | (Tensor, Tensor)` follows SequenceRecommenderModel.forward
+(core/models/sequence_recommendation_model.py:35-53): embed -> represent -> modify -> project.
+"""
+from __future__ import annotations
+
+import functools
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import layers as Ly
+from . import ops
+from .sequence import get_attribute
+
+
+class SequenceRecommenderModel(nn.Module):
+    def __init__(self, sequence_embedding_layer, sequence_representation_layer,
+                 sequence_representation_modifier_layer, projection_layer):
+        super().__init__()
+        self._sequence_embedding_layer = sequence_embedding_layer
+        self._sequence_representation_layer = sequence_representation_layer
+        self._sequence_representation_modifier_layer = sequence_representation_modifier_layer
+        self._projection_layer = projection_layer
+
+    def encode(self, sequence) -> torch.Tensor:
+        """embed -> represent -> modify; returns the representation fed to the projection."""
+        emb = self._sequence_embedding_layer(sequence)
+        rep = self._sequence_representation_layer(emb, sequence.padding_mask)
+        return self._sequence_representation_modifier_layer(rep, sequence)
+
+    def forward(self, sequence):
+        return self._projection_layer(self.encode(sequence), sequence)
+
+    def required_metadata_keys(self) -> List[str]:
+        return []
+
+    def optional_metadata_keys(self) -> List[str]:
+        return []
+
+    def item_table(self) -> Optional[nn.Parameter]:
+        return None
+
+
+class TransformerEncoderModel(SequenceRecommenderModel):
+    """core/models/transformer/transformer_encoder_model.py:12-73"""
+
+    def __init__(self, transformer_hidden_size: int, num_transformer_heads: int, num_transformer_layers: int,
+                 transformer_dropout: float, embedding_layer, sequence_representation_modifier_layer,
+                 projection_layer, bidirectional: bool = False, transformer_intermediate_size: int = None,
+                 transformer_attention_dropout: float = None):
+        if transformer_intermediate_size is None:
+            transformer_intermediate_size = 4 * transformer_hidden_size
+        transformer_layer = Ly.TransformerLayer(transformer_hidden_size, num_transformer_heads,
+                                                num_transformer_layers, transformer_intermediate_size,
+                                                transformer_dropout, attention_dropout=transformer_attention_dropout)
+        rep = Ly.TransformerSequenceRepresentationComponent(transformer_layer, bidirectional=bidirectional)
+        super().__init__(embedding_layer, rep, sequence_representation_modifier_layer, projection_layer)
+        self.apply(self._init_weights)
+
+    @staticmethod
+    def _init_weights(module):
+        is_linear, is_emb = isinstance(module, nn.Linear), isinstance(module, nn.Embedding)
+        if is_linear or is_emb:
+            nn.init.xavier_normal_(module.weight.data)
+        elif isinstance(module, nn.LayerNorm):
+            module.bias.data.zero_()
+            module.weight.data.fill_(1.0)
+        if is_linear and module.bias is not None:
+            module.bias.data.zero_()
+
+    def forward_rows(self, sequence, rows: torch.Tensor) -> torch.Tensor:
+        """Full-catalogue logits for the flattened positions `rows` only, (M, |V|).  Identical to
+        forward(sequence).view(-1, |V|)[rows] without the (B, L, |V|) tensor."""
+        rep = self.encode(sequence)
+        h = rep.reshape(-1, rep.shape[-1]).index_select(0, rows)
+        return self._projection_layer(h, sequence)
+
+
+def normal_initialize_weights(module: nn.Module, initializer_range: float = 0.2) -> None:
+    """core/models/bert4rec/bert4rec_model.py:59-68"""
+    is_linear, is_emb = isinstance(module, nn.Linear), isinstance(module, nn.Embedding)
+    if is_linear or is_emb:
+        module.weight.data.normal_(mean=0.0, std=initializer_range)
+    elif isinstance(module, nn.LayerNorm):
+        module.bias.data.zero_()
+        module.weight.data.fill_(1.0)
+    if is_linear and module.bias is not None:
+        module.bias.data.zero_()
+
+
+class SASRecModel(TransformerEncoderModel):
+    def __init__(self, transformer_hidden_size: int, num_transformer_heads: int, num_transformer_layers: int,
+                 item_vocab_size: int, max_seq_length: int, transformer_dropout: float,
+                 prefusion_attributes: Dict[str, Dict[str, Any]] = None,
+                 postfusion_attributes: Dict[str, Dict[str, Any]] = None,
+                 additional_attributes_tokenizer: Dict[str, Any] = None, postfusion_merge_function: str = "add",
+                 embedding_pooling_type: str = None, transformer_intermediate_size: int = None,
+                 transformer_attention_dropout: float = None, mode: str = "neg_sampling"):
+        self.additional_metadata_keys = list(prefusion_attributes or {}) + list(postfusion_attributes or {})
+        emb = Ly.TransformerEmbedding(item_voc_size=item_vocab_size, max_seq_len=max_seq_length,
+                                      embedding_size=transformer_hidden_size, dropout=transformer_dropout,
+                                      embedding_pooling_type=embedding_pooling_type, positional_embedding=True)
+        element_rep = Ly.PreFusionContextSequenceElementsRepresentationComponent(
+            emb, transformer_hidden_size, prefusion_attributes, additional_attributes_tokenizer,
+            dropout=transformer_dropout)
+        self.mode = mode
+        if mode == "neg_sampling":
+            projection = Ly.SASRecProjectionComponent(emb)
+        elif mode == "full":
+            projection = Ly.LinearProjectionLayer(transformer_hidden_size, item_vocab_size)
+        else:
+            raise Exception(f"{mode} is an unknown projection mode. Choose either <full> or <neg_sampling>.")
+        if postfusion_attributes is not None:
+            modifier = Ly.PostFusionIdentitySequenceRepresentationModifierLayer(
+                transformer_hidden_size, postfusion_attributes, additional_attributes_tokenizer,
+                postfusion_merge_function)
+        else:
+            modifier = Ly.IdentitySequenceRepresentationModifierLayer()
+        super().__init__(transformer_hidden_size=transformer_hidden_size, num_transformer_heads=num_transformer_heads,
+                         num_transformer_layers=num_transformer_layers, transformer_dropout=transformer_dropout,
+                         bidirectional=False, embedding_layer=element_rep,
+                         sequence_representation_modifier_layer=modifier, projection_layer=projection,
+                         transformer_intermediate_size=transformer_intermediate_size,
+                         transformer_attention_dropout=transformer_attention_dropout)
+        self.apply(self._init_weights)  # the reference initialises twice
+
+    def required_metadata_keys(self):
+        return self.additional_metadata_keys
+
+    def item_table(self):
+        return self._sequence_embedding_layer.item_embedding_layer.get_item_embedding_weight()
+
+
+class BERT4RecModel(TransformerEncoderModel):
+    def __init__(self, transformer_hidden_size: int, num_transformer_heads: int, num_transformer_layers: int,
+                 item_vocab_size: int, max_seq_length: int, transformer_dropout: float,
+                 project_layer_type: str = "transpose_embedding", embedding_pooling_type: str = None,
+                 initializer_range: float = 0.02, transformer_intermediate_size: int = None,
+                 transformer_attention_dropout: float = None):
+        modifier = Ly.FFNSequenceRepresentationModifierComponent(transformer_hidden_size)
+        # The reference passes embedding_pooling_type POSITIONALLY into TransformerEmbedding's 5th
+        # parameter, `positional_embedding` (bert4rec_model.py:40-41 vs transformer_layers.py:21-28): with
+        # the default None, BERT4Rec runs WITHOUT a position embedding.  Reproduced on purpose.
+        emb = Ly.TransformerEmbedding(item_vocab_size, max_seq_length, transformer_hidden_size, transformer_dropout,
+                                      embedding_pooling_type)
+        projection = Ly.build_projection_layer(project_layer_type, transformer_hidden_size, item_vocab_size,
+                                               emb.item_embedding.embedding)
+        super().__init__(transformer_hidden_size=transformer_hidden_size, num_transformer_heads=num_transformer_heads,
+                         num_transformer_layers=num_transformer_layers, transformer_dropout=transformer_dropout,
+                         bidirectional=True, embedding_layer=emb,
+                         projection_layer=projection, sequence_representation_modifier_layer=modifier,
+                         transformer_intermediate_size=transformer_intermediate_size,
+                         transformer_attention_dropout=transformer_attention_dropout)
+        self.apply(functools.partial(normal_initialize_weights, initializer_range=initializer_range))
+
+    def item_table(self):
+        return self._sequence_embedding_layer.get_item_embedding_weight()
+
+
+class KeBERT4RecModel(TransformerEncoderModel):
+    def __init__(self, transformer_hidden_size: int, num_transformer_heads: int, num_transformer_layers: int,
+                 item_vocab_size: int, max_seq_length: int, transformer_dropout: float,
+                 prefusion_attributes: Dict[str, Dict[str, Any]] = None,
+                 postfusion_attributes: Dict[str, Dict[str, Any]] = None,
+                 additional_attributes_tokenizer: Dict[str, Any] = None, postfusion_merge_function: str = "add",
+                 positional_embedding: bool = True, embedding_pooling_type: str = None,
+                 initializer_range: float = 0.02, transformer_intermediate_size: Optional[int] = None,
+                 transformer_attention_dropout: Optional[float] = None):
+        self.additional_metadata_keys = list(prefusion_attributes or {}) + list(postfusion_attributes or {})
+        emb = Ly.TransformerEmbedding(item_vocab_size, max_seq_length, transformer_hidden_size, 0.0,
+                                      positional_embedding=positional_embedding,
+                                      embedding_pooling_type=embedding_pooling_type, norm_embedding=False)
+        element_rep = Ly.PreFusionContextSequenceElementsRepresentationComponent(
+            emb, transformer_hidden_size, prefusion_attributes, additional_attributes_tokenizer,
+            dropout=transformer_dropout)
+        if postfusion_attributes is not None:
+            modifier = Ly.PostFusionContextSequenceRepresentationModifierComponent(
+                transformer_hidden_size, postfusion_attributes, additional_attributes_tokenizer,
+                postfusion_merge_function)
+        else:
+            modifier = Ly.FFNSequenceRepresentationModifierComponent(transformer_hidden_size)
+        projection = Ly.build_projection_layer(Ly.PROJECT_TYPE_LINEAR, transformer_hidden_size, item_vocab_size,
+                                               emb.item_embedding.embedding)
+        super().__init__(transformer_hidden_size=transformer_hidden_size, num_transformer_heads=num_transformer_heads,
+                         num_transformer_layers=num_transformer_layers, transformer_dropout=transformer_dropout,
+                         embedding_layer=element_rep, sequence_representation_modifier_layer=modifier,
+                         projection_layer=projection, bidirectional=True,
+                         transformer_intermediate_size=transformer_intermediate_size,
+                         transformer_attention_dropout=transformer_attention_dropout)
+        self.apply(functools.partial(normal_initialize_weights, initializer_range=initializer_range))
+
+    def required_metadata_keys(self):
+        return self.additional_metadata_keys
+
+    def item_table(self):
+        return self._sequence_embedding_layer.item_embedding_layer.get_item_embedding_weight()
+
+
+# ------------------------------------------------------------------------------------ NARM
+class SequenceElementsEmbeddingComponent(nn.Module):
+    """core/models/common/components/representations/sequence_embedding.py:12-35"""
+
+    def __init__(self, vocabulary_size: int, embedding_size: int, pooling_type: Optional[str] = None,
+                 dropout: Optional[float] = None):
+        super().__init__()
+        self.elements_embedding = Ly.SequenceElementsEmbeddingLayer(vocabulary_size, embedding_size, pooling_type,
+                                                                    dropout)
+
+    def forward(self, sequence) -> torch.Tensor:
+        return self.elements_embedding(sequence.sequence)
+
+
+class LocalEncoderLayer(nn.Module):
+    """v . sigmoid(A1 c_g + A2 h_i), masked weighted sum (core/models/narm/layers.py:8-66)"""
+
+    def __init__(self, hidden_size: int, latent_size: int):
+        super().__init__()
+        self.A1 = nn.Linear(hidden_size, latent_size, bias=False)
+        self.A2 = nn.Linear(hidden_size, latent_size, bias=False)
+        self.v = nn.Parameter(torch.empty(latent_size))
+        self.projection_activation = nn.Sigmoid()
+        torch.nn.init.uniform_(self.v, -1.0, 1.0)
+
+    def forward(self, s1, s2, mask):
+        proj = torch.sigmoid(self.A1(s1).unsqueeze(1) + self.A2(s2))      # (N, S, H)
+        alphas = torch.matmul(proj, self.v).unsqueeze(2)                   # (N, S, 1)
+        weighted = mask.unsqueeze(-1).to(s2.dtype) * (alphas * s2)
+        return weighted.sum(dim=1)
+
+
+class NARMSequenceRepresentationComponent(nn.Module):
+    """GRU global encoder + attentive local encoder (core/models/narm/components.py:14-56).
+    The reference packs the padded batch (lengths.cpu(): a host sync); the GRU is causal,
+    so running it on the padded batch and reading the output at len-1 gives the same c_g and the same
+    masked local context without leaving the device."""
+
+    def __init__(self, item_embedding_size: int, global_encoder_size: int, global_encoder_num_layers: int,
+                 context_dropout: float, batch_first: bool = True):
+        super().__init__()
+        self.batch_first = batch_first
+        self.global_encoder = nn.GRU(item_embedding_size, global_encoder_size, num_layers=global_encoder_num_layers,
+                                     batch_first=batch_first)
+        self.local_encoder = LocalEncoderLayer(global_encoder_size, global_encoder_size)
+        self.context_dropout = nn.Dropout(context_dropout)
+
+    def forward(self, embedded: torch.Tensor, padding_mask: torch.Tensor) -> torch.Tensor:
+        h_i, _ = self.global_encoder(embedded)
+        last = padding_mask.sum(-1) - 1
+        c_g = h_i[torch.arange(h_i.shape[0], device=h_i.device), last]
+        c_l = self.local_encoder(c_g, h_i, padding_mask)
+        return self.context_dropout(torch.cat([c_g, c_l], dim=1))
+
+
+class BilinearDecoderLayer(nn.Module):
+    """scores = context . (B E_items)^T over all items (core/models/narm/layers.py:69-120)"""
+
+    def __init__(self, embedding_layer: Ly.SequenceElementsEmbeddingLayer, encoded_representation_size: int,
+                 apply_softmax: bool = False):
+        super().__init__()
+        self.embedding_layer = embedding_layer
+        self.B = nn.Linear(embedding_layer.embedding.weight.size()[1], encoded_representation_size, bias=False)
+        self.activation = nn.Softmax() if apply_softmax else nn.Identity()
+
+    def forward(self, context: torch.Tensor, items: torch.Tensor = None):
+        table = self.embedding_layer.embedding.weight
+        emb = table if items is None else F.embedding(items, table)
+        return self.activation(context @ self.B(emb).t())
+
+
+class BilinearProjectionComponent(nn.Module):
+    def __init__(self, embedding_layer, encoded_representation_size: int, apply_softmax: bool = False):
+        super().__init__()
+        self.decoder = BilinearDecoderLayer(embedding_layer, encoded_representation_size, apply_softmax)
+
+    def forward(self, representation: torch.Tensor, sequence=None):
+        return self.decoder(representation)
+
+
+class NarmModel(SequenceRecommenderModel):
+    def __init__(self, item_vocab_size: int, item_embedding_size: int, global_encoder_size: int,
+                 global_encoder_num_layers: int, embedding_dropout: float, context_dropout: float,
+                 batch_first: bool = True, embedding_pooling_type: str = None):
+        emb = SequenceElementsEmbeddingComponent(item_vocab_size, item_embedding_size, embedding_pooling_type,
+                                                 embedding_dropout)
+        rep = NARMSequenceRepresentationComponent(item_embedding_size, global_encoder_size,
+                                                  global_encoder_num_layers, context_dropout, batch_first)
+        modifier = Ly.IdentitySequenceRepresentationModifierLayer()
+        projection = BilinearProjectionComponent(emb.elements_embedding, 2 * global_encoder_size)
+        super().__init__(emb, rep, modifier, projection)
+
+    def item_table(self):
+        return self._sequence_embedding_layer.elements_embedding.embedding.weight

@@ -1,0 +1,317 @@
+"""Training modules: the boundary the ASME trainer calls (training_step / validation_step /
+predict_step / configure_optimizers), re-provided with the reference's constructor signatures.
+
+  SequenceNextItemPredictionTrainingModule  core/modules/sequence_next_item_prediction_training_module.py:22-185
+  NextItemPredictionTrainingModule          core/modules/next_item_prediction_training_module.py:24-256
+  MaskedTrainingModule                      core/modules/masked_training_module.py:20-189
+  get_padding_mask / build_model_input      core/modules/util/module_util.py:13-30,106-151
+
+Differences that do not change results:
+  * full-catalogue losses are computed on the non-ignored rows only (identical loss, the
+    (B, L, |V|) logits tensor is never built);
+  * validation of sasrec-neg uses predict_step (the reference calls an undefined self.predict, Q13);
+  * `table_grad="sparse"` keeps the item-table gradient row-sparse and lets FusedAdam apply the exact
+    dense Adam update (Q7) without a dense (|V|, d) gradient.
+Batch keys: item, item.target, positive_samples, negative_samples (data/datasets/__init__.py:5-14).
+"""
+from __future__ import annotations
+
+import inspect
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+from torch.optim.lr_scheduler import LambdaLR
+
+from . import ops
+from .losses import SASRecBinaryCrossEntropyLoss, SASRecFullSequenceCrossEntropyLoss, SingleTargetCrossEntropyLoss
+from .optim import FusedAdam
+from .sequence import InputSequence
+
+ITEM_SEQ_ENTRY_NAME = "item"
+TARGET_ENTRY_NAME = "item.target"
+POSITIVE_SAMPLES_ENTRY_NAME = "positive_samples"
+NEGATIVE_SAMPLES_ENTRY_NAME = "negative_samples"
+LOG_KEY_TRAINING_LOSS = "train_loss"
+LOG_KEY_VALIDATION_LOSS = "val_loss"
+LOG_KEY_TEST_LOSS = "test_loss"
+
+try:  # use Lightning when it is installed (the reference's trainer); otherwise a plain nn.Module
+    import pytorch_lightning as _pl  # type: ignore
+
+    _Base = _pl.LightningModule
+except Exception:  # pragma: no cover - Lightning is not part of this image
+    class _Base(nn.Module):
+        def log(self, *args, **kwargs):
+            pass
+
+        def save_hyperparameters(self, *args, **kwargs):
+            pass
+
+
+def get_padding_mask(sequence: torch.Tensor, tokenizer) -> torch.Tensor:
+    if sequence.dim() > 2:
+        sequence = sequence.max(dim=2).values
+    return sequence.ne(tokenizer.pad_token_id)
+
+
+def get_additional_meta_data(model, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    metadata = {}
+    for key in model.required_metadata_keys():
+        if key not in batch:
+            raise Exception(f"The batch does not contain the following additional metadata: {key}. "
+                            f"Found the following batch entries: {', '.join(batch.keys())}")
+        metadata[key] = batch[key]
+    for key in model.optional_metadata_keys():
+        if key in batch:
+            metadata[key] = batch[key]
+    return metadata
+
+
+def build_model_input(model, item_tokenizer, batch) -> InputSequence:
+    seq = batch[ITEM_SEQ_ENTRY_NAME]
+    return InputSequence(seq, get_padding_mask(seq, item_tokenizer), get_additional_meta_data(model, batch))
+
+
+def build_eval_step_return_dict(input_sequence, predictions, targets, mask=None) -> Dict[str, torch.Tensor]:
+    d = {"sequence": input_sequence, "predictions": predictions, "targets": targets}
+    if mask is not None:
+        d["mask"] = mask
+    return d
+
+
+class _TableGradMixin:
+    """Row-sparse item-table gradients (see ops.SparseTablePlan / optim.FusedAdam)."""
+
+    def _init_table_grad(self, mode: str):
+        if mode not in ("dense", "sparse"):
+            raise ValueError("table_grad must be 'dense' or 'sparse'")
+        self.table_grad = mode
+        self._slot_map = None
+
+    def _plan_table(self, id_sets):
+        if self.table_grad != "sparse" or not self.training:
+            return
+        table = self.model.item_table()
+        if table is None or not table.requires_grad:
+            return
+        if self._slot_map is None or self._slot_map.device != table.device:
+            self._slot_map = torch.full((table.shape[0],), -1, dtype=torch.int32, device=table.device)
+        tg = table._asme_table_grad
+        if tg.plan is not None and not tg.plan.consumed:
+            tg.plan.release()
+        tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map)
+
+    def _update_metrics(self, targets: torch.Tensor, predictions: torch.Tensor):
+        if self.metrics is not None and targets.dim() == 1:
+            self.metrics.update(None, targets, predictions)
+
+
+class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
+    def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
+                 beta_2: float = 0.998, weight_decay: float = 1e-3,
+                 loss_function=None, table_grad: str = "dense"):
+        super().__init__()
+        self.model = model
+        self.learning_rate, self.beta_1, self.beta_2, self.weight_decay = learning_rate, beta_1, beta_2, weight_decay
+        self.item_tokenizer = item_tokenizer
+        self.metrics = metrics
+        self.loss_function = loss_function if loss_function is not None else SASRecBinaryCrossEntropyLoss()
+        self._init_table_grad(table_grad)
+
+    def training_step(self, batch, batch_idx):
+        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
+        padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
+        pos, neg = batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]
+        meta = get_additional_meta_data(self.model, batch)
+        meta["positive_samples"], meta["negative_samples"] = pos, neg
+        self._plan_table([input_seq, pos, neg])
+        pos_logits, neg_logits = self.model(InputSequence(input_seq, padding_mask, meta))
+        item_mask = input_seq.ne(self.item_tokenizer.pad_token_id)
+        loss = self.loss_function(pos_logits, neg_logits, mask=item_mask)
+        self.log(LOG_KEY_TRAINING_LOSS, loss)
+        return {"loss": loss}
+
+    def predict_step(self, batch, batch_idx, dataloader_idx: Optional[int] = None) -> torch.Tensor:
+        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
+        meta = get_additional_meta_data(self.model, batch)
+        padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
+        n = len(self.item_tokenizer.get_vocabulary())
+        items = torch.arange(n, dtype=torch.long, device=input_seq.device).repeat([input_seq.shape[0], 1])
+        meta["positive_samples"] = items
+        return self.model(InputSequence(input_seq, padding_mask, meta))
+
+    def validation_step(self, batch, batch_idx):
+        input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
+        prediction = self.predict_step(batch, batch_idx)
+        self._update_metrics(targets, prediction)
+        mask = None if targets.dim() == 1 else ~targets.eq(self.item_tokenizer.pad_token_id)
+        return build_eval_step_return_dict(input_seq, prediction, targets, mask=mask)
+
+    def test_step(self, batch, batch_idx):
+        return self.validation_step(batch, batch_idx)
+
+    def configure_optimizers(self):
+        return FusedAdam(self.parameters(), lr=self.learning_rate, betas=(self.beta_1, self.beta_2),
+                         weight_decay=self.weight_decay)
+
+
+def _instantiate_loss(loss_function, item_tokenizer):
+    if loss_function is None:
+        return SingleTargetCrossEntropyLoss(item_tokenizer)
+    if inspect.isclass(loss_function):
+        if "item_tokenizer" in inspect.signature(loss_function).parameters:
+            return loss_function(item_tokenizer=item_tokenizer)
+        return loss_function()
+    return loss_function
+
+
+class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
+    def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
+                 beta_2: float = 0.998, weight_decay: float = 0, loss_function=None, table_grad: str = "dense"):
+        super().__init__()
+        self.model = model
+        self.learning_rate, self.beta_1, self.beta_2, self.weight_decay = learning_rate, beta_1, beta_2, weight_decay
+        self.item_tokenizer = item_tokenizer
+        self.metrics = metrics
+        self.loss_function = _instantiate_loss(loss_function, item_tokenizer)
+        self._init_table_grad(table_grad)
+
+    def forward(self, batch, batch_idx: Optional[int] = None) -> torch.Tensor:
+        return self.model(build_model_input(self.model, self.item_tokenizer, batch))
+
+    def training_step(self, batch, batch_idx):
+        target = batch[TARGET_ENTRY_NAME]
+        pad = self.item_tokenizer.pad_token_id
+        ce_loss = isinstance(self.loss_function, (SASRecFullSequenceCrossEntropyLoss, SingleTargetCrossEntropyLoss))
+        self._plan_table([batch[ITEM_SEQ_ENTRY_NAME]])
+        if ce_loss and target.dim() == 2 and hasattr(self.model, "forward_rows"):
+            # per-step targets: only the non-pad positions contribute to the CE
+            rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)
+            logits = self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
+            loss = ops.cross_entropy(logits, target.reshape(-1).index_select(0, rows), pad)
+        else:
+            loss = self.loss_function(target, self(batch, batch_idx))
+        self.log(LOG_KEY_TRAINING_LOSS, loss)
+        return {"loss": loss}
+
+    def _extract_target_logits(self, input_seq, logits):
+        seq_length = get_padding_mask(input_seq, self.item_tokenizer).sum(dim=-1) - 1
+        return logits[torch.arange(input_seq.shape[0], device=logits.device), seq_length]
+
+    def _last_position_logits(self, batch):
+        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
+        if hasattr(self.model, "forward_rows"):
+            L = input_seq.shape[1]
+            last = get_padding_mask(input_seq, self.item_tokenizer).sum(dim=-1) - 1
+            rows = torch.arange(input_seq.shape[0], device=input_seq.device) * L + last
+            return self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
+        logits = self(batch)
+        return self._extract_target_logits(input_seq, logits) if logits.dim() == 3 else logits
+
+    def validation_step(self, batch, batch_idx):
+        input_seq, target = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
+        target_logits = self._last_position_logits(batch)
+        loss = self.loss_function(target, target_logits)
+        self.log(LOG_KEY_VALIDATION_LOSS, loss, prog_bar=True)
+        self._update_metrics(target, target_logits)
+        mask = None if target.dim() == 1 else ~target.eq(self.item_tokenizer.pad_token_id)
+        return build_eval_step_return_dict(input_seq, target_logits, target, mask=mask)
+
+    def test_step(self, batch, batch_idx):
+        return self.validation_step(batch, batch_idx)
+
+    def predict_step(self, batch, batch_idx, dataloader_idx: Optional[int] = None):
+        return self._last_position_logits(batch)
+
+    def configure_optimizers(self):
+        return FusedAdam(self.parameters(), lr=self.learning_rate, betas=(self.beta_1, self.beta_2),
+                         weight_decay=self.weight_decay)
+
+
+class MaskedTrainingModule(_TableGradMixin, _Base):
+    def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
+                 beta_2: float = 0.998, weight_decay: float = 0.001, num_warmup_steps: int = 10000,
+                 table_grad: str = "dense"):
+        super().__init__()
+        self.model = model
+        self.learning_rate, self.beta_1, self.beta_2 = learning_rate, beta_1, beta_2
+        self.weight_decay = weight_decay  # accepted but unused by the optimizer, as in the reference (Q7)
+        self.num_warmup_steps = num_warmup_steps
+        self.item_tokenizer = item_tokenizer
+        self.metrics = metrics
+        self._init_table_grad(table_grad)
+
+    def forward(self, batch, batch_idx: Optional[int] = None) -> torch.Tensor:
+        return self.model(build_model_input(self.model, self.item_tokenizer, batch))
+
+    def training_step(self, batch, batch_idx):
+        target = batch[TARGET_ENTRY_NAME]
+        if target.dim() > 2:
+            raise NotImplementedError("basket (multi-target) masked training is outside the MI355X hot path")
+        pad = self.item_tokenizer.pad_token_id
+        self._plan_table([batch[ITEM_SEQ_ENTRY_NAME]])
+        rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)
+        logits = self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
+        loss = ops.cross_entropy(logits, target.reshape(-1).index_select(0, rows), pad)
+        self.log(LOG_KEY_TRAINING_LOSS, loss, prog_bar=False)
+        return {"loss": loss}
+
+    def _get_prediction_for_masked_item(self, batch, batch_idx=None) -> torch.Tensor:
+        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
+        target_mask = input_seq.eq(self.item_tokenizer.mask_token_id)
+        if target_mask.dim() == 3:
+            target_mask = target_mask.max(dim=-1).values
+        rows = torch.nonzero(target_mask.reshape(-1)).squeeze(1)
+        return self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
+
+    def _eval_step(self, batch, batch_idx, is_test: bool = False):
+        input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
+        prediction = self._get_prediction_for_masked_item(batch, batch_idx)
+        loss = ops.cross_entropy(prediction, targets, self.item_tokenizer.pad_token_id)
+        self.log(LOG_KEY_TEST_LOSS if is_test else LOG_KEY_VALIDATION_LOSS, loss, prog_bar=True)
+        self._update_metrics(targets, prediction)
+        mask = None if targets.dim() == 1 else ~targets.eq(self.item_tokenizer.pad_token_id)
+        return build_eval_step_return_dict(input_seq, prediction, targets, mask=mask)
+
+    def validation_step(self, batch, batch_idx):
+        return self._eval_step(batch, batch_idx)
+
+    def test_step(self, batch, batch_idx):
+        return self._eval_step(batch, batch_idx, is_test=True)
+
+    def predict_step(self, batch, batch_idx, dataloader_idx: Optional[int] = None):
+        return self._get_prediction_for_masked_item(batch, batch_idx)
+
+    def configure_optimizers(self):
+        optimizer = FusedAdam(self.parameters(), lr=self.learning_rate, betas=(self.beta_1, self.beta_2))
+        if self.num_warmup_steps > 0:
+            warm = self.num_warmup_steps
+            scheduler = LambdaLR(optimizer, lambda step: min(1.0, step / warm))
+            return [optimizer], [{"scheduler": scheduler, "interval": "step", "strict": True}]
+        return [optimizer]
+
+
+def split_optimizers(configured):
+    """Normalise configure_optimizers() output -> (optimizer, scheduler or None)."""
+    if isinstance(configured, torch.optim.Optimizer):
+        return configured, None
+    if isinstance(configured, (list, tuple)) and len(configured) == 2 and isinstance(configured[0], list):
+        opts, scheds = configured
+        s = scheds[0]["scheduler"] if scheds and isinstance(scheds[0], dict) else (scheds[0] if scheds else None)
+        return opts[0], s
+    if isinstance(configured, (list, tuple)):
+        return configured[0], None
+    raise TypeError(f"unsupported optimizer configuration {type(configured)}")
+
+
+def train_step(module, optimizer, scheduler, batch, batch_idx: int = 0) -> torch.Tensor:
+    """One optimisation step as Lightning's automatic optimisation runs it."""
+    out = module.training_step(batch, batch_idx)
+    loss = out["loss"]
+    loss.backward()
+    optimizer.step()
+    if scheduler is not None:
+        scheduler.step()
+    optimizer.zero_grad(set_to_none=True)
+    return loss

@@ -1,0 +1,503 @@
+"""Autograd wrappers over the gfx950 HIP kernels (libasme_mi.so).
+
+Each Function here replaces a chain of stock PyTorch ops of the reference (cited per Function) with
+one or two hand-written kernels.  Plain library GEMMs (the Linear projections) stay on PyTorch's
+hipBLASLt path; everything around them is fused here.
+
+Dropout: every call with p > 0 draws a fresh 64-bit seed from torch's default CPU generator; the
+kernels derive the mask from (seed, element index) with Philox, so the backward regenerates it.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+
+_N_PARTIALS = 1024  # blocks (and partial rows) used by the grid-stride backward reductions
+
+
+def new_seed(p: float) -> int:
+    if p <= 0.0:
+        return 0
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"expected float32 tensor, got {t.dtype}")
+    return t.contiguous()
+
+
+def _i64(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.int64).contiguous()
+
+
+def _reduce_partials(part: torch.Tensor, width: int) -> torch.Tensor:
+    out = torch.empty(width, device=part.device, dtype=torch.float32)
+    call("asme_reduce_rows", ptr(part), part.shape[0], width, ptr(out), 0, stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------ table gradients
+class TableGrad:
+    """How the item-table gradient leaves the backward pass.
+
+    dense  -> a dense (V, d) gradient tensor returned to autograd (nn.Embedding semantics)
+    sparse -> contributions are scatter-added into a compact (U, d) buffer of the step's unique rows
+              (`SparseTablePlan`); the table parameter gets no .grad and FusedAdam applies the exact
+              dense update from the compact rows (rows without gradient still decay)."""
+
+    def __init__(self):
+        self.plan: Optional["SparseTablePlan"] = None
+
+
+class SparseTablePlan:
+    """Per-step dedup of every id that touches the table: slot map, unique rows, compact grad."""
+
+    def __init__(self, table: torch.Tensor, id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor):
+        dev = table.device
+        flat = torch.cat([_i64(x).reshape(-1) for x in id_sets])
+        n = flat.numel()
+        self.vocab, self.dim = table.shape
+        self.slot_map = slot_map
+        ws_bytes = int(_lib.load().asme_dedup_workspace_bytes(n))
+        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+        self.unique = torch.empty(n, device=dev, dtype=torch.int64)
+        inverse = torch.empty(n, device=dev, dtype=torch.int64)
+        self.count = torch.empty(1, device=dev, dtype=torch.int32)
+        call("asme_dedup_ids", ptr(flat), n, self.vocab, ptr(slot_map), ptr(ws), ws_bytes, ptr(self.unique),
+             ptr(inverse), ptr(self.count), stream())
+        self.capacity = n
+        self.grad_rows = torch.zeros(n, self.dim, device=dev, dtype=torch.float32)
+        self._inverse = {}
+        off = 0
+        for x in id_sets:
+            k = x.numel()
+            self._inverse[x.data_ptr(), tuple(x.shape)] = inverse[off:off + k].view(x.shape)
+            off += k
+        self.consumed = False
+
+    def inverse_of(self, ids: torch.Tensor) -> torch.Tensor:
+        key = (ids.data_ptr(), tuple(ids.shape))
+        if key not in self._inverse:
+            raise KeyError("ids were not registered with the sparse table plan of this step")
+        return self._inverse[key]
+
+    def release(self):
+        call("asme_dedup_reset", ptr(self.unique), ptr(self.count), self.capacity, ptr(self.slot_map), stream())
+        self.consumed = True
+
+
+# ------------------------------------------------------------------------------------ embedding
+@dataclass
+class EmbeddingSpec:
+    """TransformerEmbedding (+ PreFusion) configuration for one forward call."""
+    seq_len: int
+    ln1_eps: float = 1e-5
+    p1: float = 0.0
+    ln2_eps: float = 1e-5
+    p2: float = 0.0
+    table_grad: Optional[TableGrad] = None
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    """transformer_layers.py:55-80 (+ kebert4rec/components.py:54-63):
+    drop2(LN2(drop1(LN1(E[ids] + P[pos])) + extra))"""
+
+    @staticmethod
+    def forward(ctx, ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, spec: EmbeddingSpec):
+        ids = _i64(ids)
+        T = ids.numel()
+        V, D = table.shape
+        out = torch.empty(T, D, device=table.device, dtype=torch.float32)
+        stats = torch.empty(T, 4, device=table.device, dtype=torch.float32)
+        s1, s2 = new_seed(spec.p1), new_seed(spec.p2)
+        extra_c = None if extra is None else _f32(extra).reshape(T, D)
+        call("asme_embedding_fwd", ptr(ids), T, spec.seq_len, ptr(table), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
+             spec.ln1_eps, spec.p1, s1, ptr(extra_c), ptr(ln2_w), ptr(ln2_b), spec.ln2_eps, spec.p2, s2, ptr(out),
+             ptr(stats), None, stream())
+        ctx.save_for_backward(ids, table, pos, ln1_w, ln1_b, extra_c, ln2_w, stats)
+        ctx.spec, ctx.seeds = spec, (s1, s2)
+        ctx.has = (pos is not None, ln1_w is not None, extra is not None, ln2_w is not None)
+        return out.view(*ids.shape, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        ids, table, pos, ln1_w, ln1_b, extra, ln2_w, stats = ctx.saved_tensors
+        spec = ctx.spec
+        s1, s2 = ctx.seeds
+        T = ids.numel()
+        V, D = table.shape
+        dout = _f32(dout).reshape(T, D)
+        d_rows = torch.empty(T, D, device=table.device, dtype=torch.float32)
+        d_extra = torch.empty(T, D, device=table.device, dtype=torch.float32) if ctx.has[2] else None
+        has_ln = ctx.has[1] or ctx.has[3]
+        part = torch.empty(_N_PARTIALS, 4 * D, device=table.device, dtype=torch.float32) if has_ln else None
+        call("asme_embedding_bwd", ptr(ids), T, spec.seq_len, ptr(table), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
+             spec.p1, s1, ptr(extra), ptr(ln2_w), spec.p2, s2, ptr(dout), ptr(stats), ptr(d_rows), ptr(d_extra),
+             ptr(part), _N_PARTIALS, stream())
+        g_table = None
+        if ctx.needs_input_grad[1]:
+            plan = spec.table_grad.plan if spec.table_grad is not None else None
+            if plan is not None:
+                inv = plan.inverse_of(ids)
+                call("asme_scatter_add_rows", ptr(d_rows), ptr(inv), T, D, ptr(plan.grad_rows), plan.capacity, 1.0,
+                     stream())
+            else:
+                g_table = torch.zeros_like(table)
+                call("asme_scatter_add_rows", ptr(d_rows), ptr(ids), T, D, ptr(g_table), V, 1.0, stream())
+        g_pos = None
+        if ctx.has[0] and ctx.needs_input_grad[2]:
+            L = spec.seq_len
+            B = T // L
+            g_pos = torch.zeros_like(pos)
+            nch = max(1, min(32, B))
+            ws = torch.empty(nch, L, D, device=table.device, dtype=torch.float32)
+            call("asme_position_grad", ptr(d_rows), B, L, D, ptr(ws), nch, ptr(g_pos), 0, stream())
+        g = [None] * 4
+        if has_ln:
+            red = _reduce_partials(part, 4 * D)
+            g = [red[0:D], red[D:2 * D], red[2 * D:3 * D], red[3 * D:4 * D]]
+        g_extra = d_extra.view(*ids.shape, D) if d_extra is not None else None
+        return (None, g_table, g_pos, g[0] if ctx.has[1] else None, g[1] if ctx.has[1] else None, g_extra,
+                g[2] if ctx.has[3] else None, g[3] if ctx.has[3] else None, None)
+
+
+def embedding(ids, table, pos=None, ln1=None, extra=None, ln2=None, spec: EmbeddingSpec = None):
+    ln1_w, ln1_b = (None, None) if ln1 is None else ln1
+    ln2_w, ln2_b = (None, None) if ln2 is None else ln2
+    return _EmbeddingFn.apply(ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, spec)
+
+
+class _GatherSumFn(torch.autograd.Function):
+    """kebert4rec/components.py:15-24 content_embedding (k=1) / layers.py:15-27 LinearUpscaler
+    (multi-hot -> Linear == sum of weight columns of the non-pad ids, + bias)."""
+
+    @staticmethod
+    def forward(ctx, ids, table, bias, skip_zero: bool):
+        ids = _i64(ids)
+        shape = ids.shape
+        if skip_zero:  # (N, S, K) multi-hot ids
+            n, k = ids.numel() // shape[-1], shape[-1]
+            out_shape = shape[:-1]
+        else:
+            n, k = ids.numel(), 1
+            out_shape = shape
+        V, D = table.shape
+        out = torch.empty(n, D, device=table.device, dtype=torch.float32)
+        call("asme_gather_sum_fwd", ptr(ids), n, k, int(skip_zero), ptr(table), V, D, ptr(bias), ptr(out), 0,
+             stream())
+        ctx.save_for_backward(ids)
+        ctx.meta = (n, k, skip_zero, V, D, bias is not None)
+        return out.view(*out_shape, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids,) = ctx.saved_tensors
+        n, k, skip_zero, V, D, has_bias = ctx.meta
+        dout = _f32(dout).reshape(n, D)
+        g_table = torch.zeros(V, D, device=dout.device, dtype=torch.float32)
+        call("asme_gather_sum_bwd", ptr(dout), ptr(ids), n, k, int(skip_zero), ptr(g_table), V, D, stream())
+        g_bias = None
+        if has_bias:
+            g_bias = _reduce_rows(dout)
+        return None, g_table, g_bias, None
+
+
+def _reduce_rows(x: torch.Tensor) -> torch.Tensor:
+    x = _f32(x)
+    out = torch.empty(x.shape[-1], device=x.device, dtype=torch.float32)
+    call("asme_reduce_rows", ptr(x), x.numel() // x.shape[-1], x.shape[-1], ptr(out), 0, stream())
+    return out
+
+
+def gather_sum(ids, table, bias=None, skip_zero=False):
+    return _GatherSumFn.apply(ids, table, bias, skip_zero)
+
+
+# ------------------------------------------------------------------------------------ layer norm
+class _LayerNormFn(torch.autograd.Function):
+    """nn.LayerNorm over the last dim (fp32, biased variance)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps: float):
+        shape = x.shape
+        D = shape[-1]
+        x2 = _f32(x).reshape(-1, D)
+        n = x2.shape[0]
+        y = torch.empty_like(x2)
+        stats = torch.empty(n, 2, device=x.device, dtype=torch.float32)
+        call("asme_layernorm_fwd", ptr(x2), n, D, ptr(w), ptr(b), eps, ptr(y), ptr(stats), stream())
+        ctx.save_for_backward(x2, w, stats)
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, stats = ctx.saved_tensors
+        n, D = x2.shape
+        dy2 = _f32(dy).reshape(n, D)
+        dx = torch.empty_like(x2)
+        part = torch.empty(_N_PARTIALS, 2 * D, device=x2.device, dtype=torch.float32)
+        call("asme_layernorm_bwd", ptr(x2), n, D, ptr(w), ptr(stats), ptr(dy2), ptr(dx), 0, ptr(part), _N_PARTIALS,
+             stream())
+        red = _reduce_partials(part, 2 * D)
+        return dx.view(dy.shape), red[:D], red[D:], None
+
+
+def layer_norm(x, norm: torch.nn.LayerNorm):
+    return _LayerNormFn.apply(x, norm.weight, norm.bias, norm.eps)
+
+
+class _ResidualLNFn(torch.autograd.Function):
+    """SublayerConnection epilogue + block dropout + next pre-LN (transformer_layers.py:120-130, 251-258):
+    s = drop_b(res + drop_a(y));  ln = LN(s)"""
+
+    @staticmethod
+    def forward(ctx, res, y, w, b, eps: float, p_a: float, p_b: float):
+        shape = res.shape
+        D = shape[-1]
+        r2 = _f32(res).reshape(-1, D)
+        y2 = _f32(y).reshape(-1, D)
+        n = r2.shape[0]
+        s = torch.empty_like(r2)
+        has_ln = w is not None
+        ln = torch.empty_like(r2) if has_ln else None
+        stats = torch.empty(n, 2, device=res.device, dtype=torch.float32) if has_ln else None
+        sa, sb = new_seed(p_a), new_seed(p_b)
+        call("asme_residual_ln_fwd", ptr(r2), ptr(y2), n, D, p_a, sa, p_b, sb, ptr(w), ptr(b), eps, ptr(s), ptr(ln),
+             ptr(stats), stream())
+        ctx.save_for_backward(s, w, stats)
+        ctx.meta = (p_a, sa, p_b, sb, has_ln, shape)
+        if has_ln:
+            return s.view(shape), ln.view(shape)
+        return s.view(shape), s.new_empty(0)
+
+    @staticmethod
+    def backward(ctx, d_s, d_ln):
+        s, w, stats = ctx.saved_tensors
+        p_a, sa, p_b, sb, has_ln, shape = ctx.meta
+        n, D = s.shape
+        ds2 = None if d_s is None else _f32(d_s).reshape(n, D)
+        dl2 = None if (d_ln is None or not has_ln) else _f32(d_ln).reshape(n, D)
+        d_res = torch.empty_like(s)
+        d_y = torch.empty_like(s) if p_a > 0 else None
+        part = torch.empty(_N_PARTIALS, 2 * D, device=s.device, dtype=torch.float32) if dl2 is not None else None
+        call("asme_residual_ln_bwd", ptr(s), n, D, p_a, sa, p_b, sb, ptr(w), ptr(stats), ptr(ds2), ptr(dl2),
+             ptr(d_res), ptr(d_y), ptr(part), _N_PARTIALS, stream())
+        gw = gb = None
+        if has_ln:
+            if part is not None:
+                red = _reduce_partials(part, 2 * D)
+                gw, gb = red[:D], red[D:]
+            else:
+                gw, gb = torch.zeros_like(w), torch.zeros_like(w)
+        dy = d_y if d_y is not None else d_res
+        return d_res.view(shape), dy.view(shape), gw, gb, None, None, None
+
+
+def residual_ln(res, y, norm: Optional[torch.nn.LayerNorm], p_a: float, p_b: float):
+    if norm is None:
+        s, _ = _ResidualLNFn.apply(res, y, None, None, 1e-5, p_a, p_b)
+        return s, None
+    return _ResidualLNFn.apply(res, y, norm.weight, norm.bias, norm.eps, p_a, p_b)
+
+
+class _GeluDropoutFn(torch.autograd.Function):
+    """dropout(GELU_erf(x)) (transformer_layers.py:217-220; ffn_modifier.py:24-26 with p = 0)"""
+
+    @staticmethod
+    def forward(ctx, x, p: float):
+        x = _f32(x)
+        y = torch.empty_like(x)
+        seed = new_seed(p)
+        call("asme_gelu_dropout_fwd", ptr(x), x.numel(), p, seed, ptr(y), stream())
+        ctx.save_for_backward(x)
+        ctx.meta = (p, seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        p, seed = ctx.meta
+        dy = _f32(dy)
+        dx = torch.empty_like(x)
+        call("asme_gelu_dropout_bwd", ptr(x), ptr(dy), x.numel(), p, seed, ptr(dx), stream())
+        return dx, None
+
+
+def gelu_dropout(x, p: float = 0.0):
+    return _GeluDropoutFn.apply(x, p)
+
+
+# ------------------------------------------------------------------------------------ attention
+class _AttentionFn(torch.autograd.Function):
+    """Attention.forward (transformer_layers.py:138-155) on a fused (B, L, 3*H*dk) QKV tensor.
+    key_valid (B, L) uint8; causal selects SASRec's tril mask (sequence_representation.py:34-48)."""
+
+    @staticmethod
+    def forward(ctx, qkv, key_valid, heads: int, causal: bool, p_drop: float):
+        B, L, three_d = qkv.shape
+        Dm = three_d // 3
+        dk = Dm // heads
+        qkv = _f32(qkv)
+        out = torch.empty(B, L, Dm, device=qkv.device, dtype=torch.float32)
+        lse = torch.empty(B * heads, L, 2, device=qkv.device, dtype=torch.float32)  # (max, 1/sum)
+        seed = new_seed(p_drop)
+        scale = 1.0 / math.sqrt(dk)
+        base = qkv.data_ptr()
+        call("asme_attention_fwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(key_valid), B,
+             heads, L, dk, int(causal), scale, p_drop, seed, ptr(out), Dm, ptr(lse), stream())
+        ctx.save_for_backward(qkv, key_valid, out, lse)
+        ctx.meta = (heads, causal, p_drop, seed, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, key_valid, out, lse = ctx.saved_tensors
+        heads, causal, p_drop, seed, scale = ctx.meta
+        B, L, three_d = qkv.shape
+        Dm = three_d // 3
+        dk = Dm // heads
+        dout = _f32(dout)
+        dqkv = torch.empty_like(qkv)
+        dsum = torch.empty(B * heads * L, device=qkv.device, dtype=torch.float32)
+        base, gb = qkv.data_ptr(), dqkv.data_ptr()
+        call("asme_attention_bwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(out), Dm,
+             ptr(dout), Dm, ptr(lse), ptr(key_valid), B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(dsum),
+             gb, three_d, gb + 4 * Dm, three_d, gb + 8 * Dm, three_d, stream())
+        return dqkv, None, None, None, None
+
+
+def attention(qkv, key_valid, heads: int, causal: bool, p_drop: float = 0.0):
+    return _AttentionFn.apply(qkv, key_valid, heads, causal, p_drop)
+
+
+# ------------------------------------------------------------------------------------ heads / losses
+class _SampledLogitsFn(torch.autograd.Function):
+    """SASRecProjectionComponent.forward training branch (sasrec/components.py:34-44)."""
+
+    @staticmethod
+    def forward(ctx, hidden, table, pos_ids, neg_ids, table_grad: Optional[TableGrad]):
+        shape = pos_ids.shape
+        V, D = table.shape
+        h2 = _f32(hidden).reshape(-1, D)
+        pos_ids, neg_ids = _i64(pos_ids), _i64(neg_ids)
+        T = h2.shape[0]
+        po = torch.empty(T, device=hidden.device, dtype=torch.float32)
+        no = torch.empty(T, device=hidden.device, dtype=torch.float32)
+        call("asme_sampled_logits_fwd", ptr(h2), ptr(table), ptr(pos_ids), ptr(neg_ids), T, D, V, ptr(po), ptr(no),
+             stream())
+        ctx.save_for_backward(h2, table, pos_ids, neg_ids)
+        ctx.table_grad = table_grad
+        ctx.hshape = hidden.shape
+        return po.view(shape), no.view(shape)
+
+    @staticmethod
+    def backward(ctx, g_pos, g_neg):
+        h2, table, pos_ids, neg_ids = ctx.saved_tensors
+        V, D = table.shape
+        T = h2.shape[0]
+        gp = torch.zeros(T, device=h2.device) if g_pos is None else _f32(g_pos).reshape(T)
+        gn = torch.zeros(T, device=h2.device) if g_neg is None else _f32(g_neg).reshape(T)
+        dh = torch.empty_like(h2) if ctx.needs_input_grad[0] else None
+        g_table = None
+        plan = ctx.table_grad.plan if ctx.table_grad is not None else None
+        if ctx.needs_input_grad[1] and plan is not None:
+            # dH pass with the real table; the table contributions go to the compact rows
+            call("asme_sampled_logits_bwd", ptr(h2), ptr(table), ptr(pos_ids), ptr(neg_ids), T, D, V, ptr(gp),
+                 ptr(gn), ptr(dh), None, stream())
+            ip, ineg = plan.inverse_of(pos_ids), plan.inverse_of(neg_ids)
+            call("asme_sampled_logits_bwd", ptr(h2), ptr(plan.grad_rows), ptr(ip), ptr(ineg), T, D, plan.capacity,
+                 ptr(gp), ptr(gn), None, ptr(plan.grad_rows), stream())
+        else:
+            if ctx.needs_input_grad[1]:
+                g_table = torch.zeros_like(table)
+            call("asme_sampled_logits_bwd", ptr(h2), ptr(table), ptr(pos_ids), ptr(neg_ids), T, D, V, ptr(gp),
+                 ptr(gn), ptr(dh), ptr(g_table), stream())
+        return (None if dh is None else dh.view(ctx.hshape)), g_table, None, None, None
+
+
+def sampled_logits(hidden, table, pos_ids, neg_ids, table_grad: Optional[TableGrad] = None):
+    return _SampledLogitsFn.apply(hidden, table, pos_ids, neg_ids, table_grad)
+
+
+class _SASRecBCEFn(torch.autograd.Function):
+    """sas_rec_binary_cross_entropy (core/losses/sasrec/sas_rec_losses.py:56-75)."""
+
+    @staticmethod
+    def forward(ctx, pos, neg, mask):
+        pos_shape, neg_shape = pos.shape, neg.shape
+        pos, neg = _f32(pos).reshape(-1), _f32(neg).reshape(-1)
+        m = mask.reshape(-1).to(torch.uint8).contiguous()
+        T = pos.numel()
+        nparts = max(1, min(1024, (T + 255) // 256))
+        ws = torch.empty(nparts, 2, device=pos.device, dtype=torch.float32)
+        out = torch.empty(2, device=pos.device, dtype=torch.float32)
+        call("asme_sasrec_bce_fwd", ptr(pos), ptr(neg), ptr(m), T, ptr(ws), nparts, ptr(out), stream())
+        ctx.save_for_backward(pos, neg, m, out)
+        ctx.shapes = (pos_shape, neg_shape)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        pos, neg, m, out = ctx.saved_tensors
+        T = pos.numel()
+        dl = _f32(dloss.reshape(1))
+        gp, gn = torch.empty_like(pos), torch.empty_like(neg)
+        call("asme_sasrec_bce_bwd", ptr(pos), ptr(neg), ptr(m), T, ptr(dl), ptr(out), ptr(gp), ptr(gn), stream())
+        return gp.view(ctx.shapes[0]), gn.view(ctx.shapes[1]), None
+
+
+def sasrec_bce(pos_logits, neg_logits, mask):
+    loss = _SASRecBCEFn.apply(pos_logits, neg_logits, mask)
+    return loss
+
+
+class _CrossEntropyFn(torch.autograd.Function):
+    """nn.CrossEntropyLoss(ignore_index=pad), mean over non-ignored rows."""
+
+    @staticmethod
+    def forward(ctx, logits, targets, ignore_index: int):
+        C = logits.shape[-1]
+        x = _f32(logits).reshape(-1, C)
+        t = _i64(targets).reshape(-1)
+        n = x.shape[0]
+        if t.numel() != n:
+            raise ValueError(f"logits rows ({n}) and targets ({t.numel()}) differ")
+        lse = torch.empty(n, device=x.device, dtype=torch.float32)
+        rl = torch.empty(n, device=x.device, dtype=torch.float32)
+        out = torch.empty(2, device=x.device, dtype=torch.float32)
+        call("asme_cross_entropy_fwd", ptr(x), C, ptr(t), ignore_index, n, C, ptr(lse), ptr(rl), ptr(out), stream())
+        ctx.save_for_backward(x, t, lse, out)
+        ctx.meta = (ignore_index, logits.shape)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        x, t, lse, out = ctx.saved_tensors
+        ignore_index, shape = ctx.meta
+        n, C = x.shape
+        dl = _f32(dloss.reshape(1))
+        g = torch.empty_like(x)
+        call("asme_cross_entropy_bwd", ptr(x), C, ptr(lse), ptr(t), ignore_index, n, C, ptr(dl), ptr(out), ptr(g), C,
+             stream())
+        return g.view(shape), None, None
+
+
+def cross_entropy(logits, targets, ignore_index: int):
+    return _CrossEntropyFn.apply(logits, targets, ignore_index)
+
+
+def target_rank(scores: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    """1-based rank of each target in its row (descending; ties -> lower id first)."""
+    s = _f32(scores)
+    t = _i64(targets)
+    n, V = s.shape
+    ranks = torch.empty(n, device=s.device, dtype=torch.int64)
+    call("asme_target_rank", ptr(s), V, ptr(t), n, V, ptr(ranks), stream())
+    return ranks

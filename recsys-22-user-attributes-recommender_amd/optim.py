@@ -1,0 +1,76 @@
+"""FusedAdam: torch.optim.Adam semantics on the gfx950 multi-tensor Adam kernel.
+
+Matches the optimizers the reference modules build (core/modules/*_training_module.py:
+configure_optimizers -> torch.optim.Adam(lr, betas, weight_decay) with L2-coupled decay):
+one launch updates every dense parameter; the item table, when its gradient arrives as a
+row-sparse `SparseTablePlan`, gets the exact dense update from the compact rows
+(asme_adam_rows_step) without ever materialising a dense (V, d) gradient.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ._lib import call, ptr, stream
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        if lr < 0.0 or eps < 0.0 or weight_decay < 0.0:
+            raise ValueError("invalid Adam hyper-parameter")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+
+    def _state(self, p):
+        st = self.state[p]
+        if not st:
+            st["step"] = 0
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            lr, eps, wd = float(group["lr"]), float(group["eps"]), float(group["weight_decay"])
+            by_step = {}
+            for p in group["params"]:
+                tg = getattr(p, "_asme_table_grad", None)
+                plan = tg.plan if tg is not None else None
+                if plan is not None:
+                    if p.grad is not None:
+                        raise RuntimeError("item table got a dense gradient while its sparse plan is active "
+                                           "(tied / full-catalogue heads need table_grad='dense')")
+                    st = self._state(p)
+                    st["step"] += 1
+                    V, D = p.shape
+                    call("asme_adam_rows_step", ptr(p), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), V, D,
+                         ptr(plan.slot_map), ptr(plan.grad_rows), lr, b1, b2, eps, wd, st["step"], stream())
+                    plan.release()
+                    tg.plan = None
+                    continue
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdam does not support torch sparse gradients")
+                st = self._state(p)
+                st["step"] += 1
+                by_step.setdefault(st["step"], []).append(p)
+            for step, ps in by_step.items():
+                n = len(ps)
+                arr = ctypes.c_void_p * n
+                P = arr(*[ptr(p) for p in ps])
+                for p in ps:
+                    if not p.grad.is_contiguous():
+                        p.grad = p.grad.contiguous()
+                G = arr(*[ptr(p.grad) for p in ps])
+                M = arr(*[ptr(self.state[p]["exp_avg"]) for p in ps])
+                Vv = arr(*[ptr(self.state[p]["exp_avg_sq"]) for p in ps])
+                N = (ctypes.c_int64 * n)(*[p.numel() for p in ps])
+                call("asme_adam_step", n, P, G, M, Vv, N, lr, b1, b2, eps, wd, step, stream())
+        return loss

@@ -1,0 +1,88 @@
+"""CPU: the drop-in boundary.  Constructor signatures equal the reference's (ASME's GenericModelFactory
+introspects them), state_dict keys equal the reference's (checkpoints / fixtures interchange), the
+registry covers the five hot-path keys, and the product path refuses to run without the GPU."""
+import inspect
+
+import pytest
+import torch
+
+from helpers import MODEL_FIXTURES, build_model, load, prefixed, state_dict
+
+# parameter lists of the reference constructors (core/models/*/..._model.py, core/modules/*.py)
+REFERENCE_SIGNATURES = {
+    "SASRecModel": ["transformer_hidden_size", "num_transformer_heads", "num_transformer_layers", "item_vocab_size",
+                    "max_seq_length", "transformer_dropout", "prefusion_attributes", "postfusion_attributes",
+                    "additional_attributes_tokenizer", "postfusion_merge_function", "embedding_pooling_type",
+                    "transformer_intermediate_size", "transformer_attention_dropout", "mode"],
+    "BERT4RecModel": ["transformer_hidden_size", "num_transformer_heads", "num_transformer_layers",
+                      "item_vocab_size", "max_seq_length", "transformer_dropout", "project_layer_type",
+                      "embedding_pooling_type", "initializer_range", "transformer_intermediate_size",
+                      "transformer_attention_dropout"],
+    "KeBERT4RecModel": ["transformer_hidden_size", "num_transformer_heads", "num_transformer_layers",
+                        "item_vocab_size", "max_seq_length", "transformer_dropout", "prefusion_attributes",
+                        "postfusion_attributes", "additional_attributes_tokenizer", "postfusion_merge_function",
+                        "positional_embedding", "embedding_pooling_type", "initializer_range",
+                        "transformer_intermediate_size", "transformer_attention_dropout"],
+    "NarmModel": ["item_vocab_size", "item_embedding_size", "global_encoder_size", "global_encoder_num_layers",
+                  "embedding_dropout", "context_dropout", "batch_first", "embedding_pooling_type"],
+    "SequenceNextItemPredictionTrainingModule": ["model", "item_tokenizer", "metrics", "learning_rate", "beta_1",
+                                                 "beta_2", "weight_decay", "loss_function"],
+    "NextItemPredictionTrainingModule": ["model", "item_tokenizer", "metrics", "learning_rate", "beta_1", "beta_2",
+                                         "weight_decay", "loss_function"],
+    "MaskedTrainingModule": ["model", "item_tokenizer", "metrics", "learning_rate", "beta_1", "beta_2",
+                             "weight_decay", "num_warmup_steps"],
+}
+REFERENCE_DEFAULTS = {
+    ("SASRecModel", "mode"): "neg_sampling",
+    ("BERT4RecModel", "project_layer_type"): "transpose_embedding",
+    ("BERT4RecModel", "initializer_range"): 0.02,
+    ("SequenceNextItemPredictionTrainingModule", "weight_decay"): 1e-3,
+    ("SequenceNextItemPredictionTrainingModule", "beta_1"): 0.99,
+    ("SequenceNextItemPredictionTrainingModule", "beta_2"): 0.998,
+    ("NextItemPredictionTrainingModule", "weight_decay"): 0,
+    ("MaskedTrainingModule", "num_warmup_steps"): 10000,
+}
+
+
+@pytest.mark.parametrize("cls_name", sorted(REFERENCE_SIGNATURES))
+def test_constructor_signatures(asme, cls_name):
+    cls = getattr(asme, cls_name)
+    params = [p for p in inspect.signature(cls.__init__).parameters if p != "self"]
+    want = REFERENCE_SIGNATURES[cls_name]
+    assert params[:len(want)] == want
+    extra = params[len(want):]
+    assert all(inspect.signature(cls.__init__).parameters[p].default is not inspect._empty for p in extra)
+    for (c, p), v in REFERENCE_DEFAULTS.items():
+        if c == cls_name:
+            assert inspect.signature(cls.__init__).parameters[p].default == v
+
+
+@pytest.mark.parametrize("name", MODEL_FIXTURES)
+def test_state_dict_keys_match_reference(asme, name):
+    z = load(name)
+    model = build_model(asme, name, z)
+    ref = state_dict(z)
+    assert set(model.state_dict()) == set(ref)
+    model.load_state_dict(ref, strict=True)
+    assert {n for n, _ in model.named_parameters()} == set(prefixed(z, "grad"))
+
+
+def test_bert4rec_has_no_position_embedding(asme):
+    """Reference trap: BERT4Rec passes embedding_pooling_type positionally into `positional_embedding`."""
+    m = asme.BERT4RecModel(transformer_hidden_size=16, num_transformer_heads=2, num_transformer_layers=1,
+                           item_vocab_size=20, max_seq_length=8, transformer_dropout=0.1)
+    assert not any("position_embedding" in k for k in m.state_dict())
+
+
+def test_registry_keys(asme):
+    assert set(asme.registry.KEYS) == {"sasrec-neg", "sasrec-cross", "bert4rec", "kebert4rec", "narm"}
+
+
+def test_forward_without_gpu_fails_loudly(asme):
+    z = load("sasrec_neg")
+    model = build_model(asme, "sasrec_neg", z)
+    seq = torch.from_numpy(z["seq"])
+    batch = asme.InputSequence(seq, seq.ne(0), {"positive_samples": torch.from_numpy(z["pos"]),
+                                                 "negative_samples": torch.from_numpy(z["neg"])})
+    with pytest.raises(asme._lib.ASMEKernelError):
+        model(batch)
