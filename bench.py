@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--table-grad", choices=["sparse", "dense"], default="sparse")
     ap.add_argument("--ids", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
-    ap.add_argument("--cpu-batch", type=int, default=32, help="sequences per CPU-baseline step")
+    ap.add_argument("--cpu-batch", type=int, default=256, help="sequences per CPU-baseline step")
     ap.add_argument("--cpu-steps", type=int, default=2)
     return ap.parse_args()
 

@@ -65,11 +65,23 @@ def test_model_train_step_matches_reference(asme, dev, name):
     if sched is not None:
         sched.step()
     for k, v in prefixed(z, "adam1").items():
+        if _analytically_zero_grad(k):
+            continue
         assert close(named[k].detach().cpu().numpy(), v, TOL), (k, "adam step 1")
     if "adam2/" + next(iter(grads)) in z.files:
         opt.step()
         for k, v in prefixed(z, "adam2").items():
+            if _analytically_zero_grad(k):
+                continue
             assert close(named[k].detach().cpu().numpy(), v, TOL), (k, "adam step 2")
+
+
+def _analytically_zero_grad(name):
+    """The key-projection bias adds the same constant to every score of a query row; softmax is
+    invariant to it, so its exact gradient is 0 and both implementations return fp32 rounding noise
+    (checked above with the absolute tolerance).  Adam's first step is ~ -lr * sign(grad), so the
+    updated value follows the sign of that noise and is not comparable."""
+    return name.endswith("attention.linear_layers.1.bias")
 
 
 @pytest.mark.parametrize("name", MODEL_FIXTURES)
