@@ -145,6 +145,20 @@ int asme_adam_rows_step(float* param, float* exp_avg, float* exp_avg_sq, int64_t
                         const int32_t* row_slot, const float* grad_rows, float lr, float beta1, float beta2,
                         float eps, float weight_decay, int64_t step, void* stream);
 
+/* Lazy dense Adam ("exact catch-up"): bit-identical to asme_adam_rows_step every step, but a row with a
+ * zero gradient is only rewritten when it is next read.  last_step (rows int32) = step each row is up to
+ * date with; hist (capacity, 8) float = per-step constants written by asme_lazy_adam_record_step. */
+int asme_lazy_adam_record_step(float* hist, int64_t step, float lr, float beta1, float beta2, float eps,
+                               float weight_decay, void* stream);
+/* replay zero-gradient steps (last_step[r], upto] for rows[0..*count) (rows == NULL: all rows 0..cap) */
+int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, int64_t cap, int32_t* last_step,
+                            float* param, float* exp_avg, float* exp_avg_sq, int64_t dim, const float* hist,
+                            int64_t upto, void* stream);
+/* step `step` with the real gradient grad_rows[s] for rows[s], s < *count (rows already at step-1) */
+int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap, const float* grad_rows,
+                         int32_t* last_step, float* param, float* exp_avg, float* exp_avg_sq, int64_t dim,
+                         const float* hist, int64_t step, void* stream);
+
 /* ---- id dedup & shard bucketing (row-sharded item table) ------------------------ */
 int64_t asme_dedup_workspace_bytes(int64_t n);
 int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_t* map, void* workspace,

@@ -173,3 +173,141 @@ ASME_API int asme_adam_rows_step(float* param, float* exp_avg, float* exp_avg_sq
                        exp_avg_sq, rows, (int)dim, row_slot, grad_rows, hp);
     ASME_LAUNCH_CHECK("asme_adam_rows_step");
 }
+
+// ------------------------------------------------------------------------------------------------
+// Lazy dense Adam ("exact catch-up").  Dense Adam (every row, every step) on a row whose gradient is
+// zero for a run of steps is a deterministic recurrence in (p, m, v) and the per-step constants.  We
+// keep, per table row, the step it is up to date with (last_step) and a device history of the per-step
+// hyper-parameters; a row is brought up to date by replaying exactly the fp32 operations the dense
+// kernel would have executed (same adam_elem, same constants, same order), only when its value is
+// needed: before a forward that gathers it, and in a full flush before anything else reads the table.
+// The result is bit-identical to running asme_adam_rows_step every step; the HBM traffic per step
+// drops from 6 x |V| x d x 4 B to 6 x U x d x 4 B (U = unique rows of the step).
+namespace {
+
+static_assert(sizeof(AdamHyper) == 8 * sizeof(float), "hist row = 8 floats");
+
+__global__ void record_step_kernel(float* __restrict__ hist, int64_t step, AdamHyper hp) {
+    if (threadIdx.x == 0) reinterpret_cast<AdamHyper*>(hist)[step] = hp;
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void lazy_catch_up_kernel(const int64_t* __restrict__ rows,
+                                                            const int32_t* __restrict__ count, int64_t cap,
+                                                            int32_t* __restrict__ last_step, float* __restrict__ p,
+                                                            float* __restrict__ m, float* __restrict__ v, int D,
+                                                            const AdamHyper* __restrict__ hist, int32_t upto) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t n = count ? (int64_t)*count : cap;
+    if (s >= n || s >= cap) return;
+    const int64_t r = rows ? rows[s] : s;
+    const int32_t t0 = last_step[r];
+    if (t0 >= upto) return;
+    float P[VPL], M[VPL], Vv[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        if (e < D) {
+            P[j] = p[r * D + e];
+            M[j] = m[r * D + e];
+            Vv[j] = v[r * D + e];
+        }
+    }
+    for (int32_t t = t0 + 1; t <= upto; ++t) {
+        const AdamHyper hp = hist[t];
+#pragma unroll
+        for (int j = 0; j < VPL; ++j)
+            if (lane + 64 * j < D) adam_elem(P[j], 0.f, M[j], Vv[j], hp);
+    }
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        if (e < D) {
+            p[r * D + e] = P[j];
+            m[r * D + e] = M[j];
+            v[r * D + e] = Vv[j];
+        }
+    }
+    if (lane == 0) last_step[r] = upto;
+}
+
+// the real-gradient update of the step's unique rows (they were caught up to step-1 before the forward)
+template <int VPL>
+__global__ __launch_bounds__(256) void lazy_apply_kernel(const int64_t* __restrict__ rows,
+                                                         const int32_t* __restrict__ count, int64_t cap,
+                                                         const float* __restrict__ grad_rows,
+                                                         int32_t* __restrict__ last_step, float* __restrict__ p,
+                                                         float* __restrict__ m, float* __restrict__ v, int D,
+                                                         const AdamHyper* __restrict__ hist, int32_t step) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= cap || s >= (int64_t)*count) return;
+    const int64_t r = rows[s];
+    const AdamHyper hp = hist[step];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        if (e < D) {
+            float P = p[r * D + e], M = m[r * D + e], Vv = v[r * D + e];
+            adam_elem(P, grad_rows[s * D + e], M, Vv, hp);
+            p[r * D + e] = P;
+            m[r * D + e] = M;
+            v[r * D + e] = Vv;
+        }
+    }
+    if (lane == 0) last_step[r] = step;
+}
+
+#define ASME_VPL_DISPATCH(VPLV, ...)                              \
+    switch (VPLV) {                                               \
+        case 1: { constexpr int VPL = 1; __VA_ARGS__; } break;    \
+        case 2: { constexpr int VPL = 2; __VA_ARGS__; } break;    \
+        case 3: { constexpr int VPL = 3; __VA_ARGS__; } break;    \
+        case 4: { constexpr int VPL = 4; __VA_ARGS__; } break;    \
+        case 5: { constexpr int VPL = 5; __VA_ARGS__; } break;    \
+        case 6: { constexpr int VPL = 6; __VA_ARGS__; } break;    \
+        case 7: { constexpr int VPL = 7; __VA_ARGS__; } break;    \
+        case 8: { constexpr int VPL = 8; __VA_ARGS__; } break;    \
+        default: set_error("hidden size must be in [1, 512]"); return -1; \
+    }
+}  // namespace
+
+// hist[step] = the Adam constants of `step` (hist: (capacity, 8) floats on the device)
+ASME_API int asme_lazy_adam_record_step(float* hist, int64_t step, float lr, float beta1, float beta2, float eps,
+                                        float weight_decay, void* stream) {
+    ASME_CHECK_ARG(hist && step >= 1, "asme_lazy_adam_record_step: bad argument");
+    const AdamHyper hp = make_hyper(lr, beta1, beta2, eps, weight_decay, step);
+    hipLaunchKernelGGL(record_step_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hist, step, hp);
+    ASME_LAUNCH_CHECK("asme_lazy_adam_record_step");
+}
+
+// bring rows[0..count) (rows == NULL: every row 0..cap) up to date through step `upto` with zero gradient
+ASME_API int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, int64_t cap, int32_t* last_step,
+                                     float* param, float* exp_avg, float* exp_avg_sq, int64_t dim, const float* hist,
+                                     int64_t upto, void* stream) {
+    ASME_CHECK_ARG(last_step && param && exp_avg && exp_avg_sq && hist, "asme_lazy_adam_catch_up: null pointer");
+    ASME_CHECK_ARG(dim >= 1 && dim <= 512 && upto >= 0 && upto < (1LL << 31), "asme_lazy_adam_catch_up: bad shape");
+    if (cap == 0 || upto == 0) return 0;
+    const dim3 grid((unsigned)((cap + 3) / 4));
+    ASME_VPL_DISPATCH((int)((dim + 63) / 64),
+                      hipLaunchKernelGGL(lazy_catch_up_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, rows,
+                                         count, cap, last_step, param, exp_avg, exp_avg_sq, (int)dim,
+                                         reinterpret_cast<const AdamHyper*>(hist), (int32_t)upto));
+    ASME_LAUNCH_CHECK("asme_lazy_adam_catch_up");
+}
+
+ASME_API int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap, const float* grad_rows,
+                                  int32_t* last_step, float* param, float* exp_avg, float* exp_avg_sq, int64_t dim,
+                                  const float* hist, int64_t step, void* stream) {
+    ASME_CHECK_ARG(rows && count && grad_rows && last_step && param && exp_avg && exp_avg_sq && hist,
+                   "asme_lazy_adam_apply: null pointer");
+    ASME_CHECK_ARG(dim >= 1 && dim <= 512 && step >= 1, "asme_lazy_adam_apply: bad shape");
+    if (cap == 0) return 0;
+    const dim3 grid((unsigned)((cap + 3) / 4));
+    ASME_VPL_DISPATCH((int)((dim + 63) / 64),
+                      hipLaunchKernelGGL(lazy_apply_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, rows, count,
+                                         cap, grad_rows, last_step, param, exp_avg, exp_avg_sq, (int)dim,
+                                         reinterpret_cast<const AdamHyper*>(hist), (int32_t)step));
+    ASME_LAUNCH_CHECK("asme_lazy_adam_apply");
+}

@@ -31,6 +31,14 @@ class SequenceRecommenderModel(nn.Module):
         self._sequence_representation_layer = sequence_representation_layer
         self._sequence_representation_modifier_layer = sequence_representation_modifier_layer
         self._projection_layer = projection_layer
+        self.register_state_dict_pre_hook(lambda module, prefix, keep_vars: module.flush_table())
+
+    def flush_table(self):
+        """Apply pending lazy-Adam updates of the item table (see ops.LazyTableState)."""
+        table = self.item_table()
+        tg = getattr(table, "_asme_table_grad", None) if table is not None else None
+        if tg is not None and tg.lazy is not None:
+            tg.lazy.flush()
 
     def encode(self, sequence) -> torch.Tensor:
         """embed -> represent -> modify; returns the representation fed to the projection."""
@@ -49,6 +57,11 @@ class SequenceRecommenderModel(nn.Module):
 
     def item_table(self) -> Optional[nn.Parameter]:
         return None
+
+    def table_grad_sparse_ok(self) -> bool:
+        """True when every read of the item table goes through the gather kernels (no tied/bilinear
+        full-catalogue head), so its gradient is row-sparse."""
+        return False
 
 
 class TransformerEncoderModel(SequenceRecommenderModel):
@@ -140,6 +153,9 @@ class SASRecModel(TransformerEncoderModel):
     def item_table(self):
         return self._sequence_embedding_layer.item_embedding_layer.get_item_embedding_weight()
 
+    def table_grad_sparse_ok(self) -> bool:
+        return True
+
 
 class BERT4RecModel(TransformerEncoderModel):
     def __init__(self, transformer_hidden_size: int, num_transformer_heads: int, num_transformer_layers: int,
@@ -165,6 +181,9 @@ class BERT4RecModel(TransformerEncoderModel):
 
     def item_table(self):
         return self._sequence_embedding_layer.get_item_embedding_weight()
+
+    def table_grad_sparse_ok(self) -> bool:
+        return isinstance(self._projection_layer, Ly.LinearProjectionLayer)
 
 
 class KeBERT4RecModel(TransformerEncoderModel):
@@ -204,6 +223,9 @@ class KeBERT4RecModel(TransformerEncoderModel):
 
     def item_table(self):
         return self._sequence_embedding_layer.item_embedding_layer.get_item_embedding_weight()
+
+    def table_grad_sparse_ok(self) -> bool:
+        return True
 
 
 # ------------------------------------------------------------------------------------ NARM

@@ -86,6 +86,9 @@ class _TableGradMixin:
     def _init_table_grad(self, mode: str):
         if mode not in ("dense", "sparse"):
             raise ValueError("table_grad must be 'dense' or 'sparse'")
+        if mode == "sparse" and not self.model.table_grad_sparse_ok():
+            raise ValueError(f"{type(self.model).__name__} reads the whole item table in its head; "
+                             "use table_grad='dense'")
         self.table_grad = mode
         self._slot_map = None
 
@@ -101,6 +104,9 @@ class _TableGradMixin:
         if tg.plan is not None and not tg.plan.consumed:
             tg.plan.release()
         tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map)
+
+    def _flush_table(self):
+        self.model.flush_table()
 
     def _update_metrics(self, targets: torch.Tensor, predictions: torch.Tensor):
         if self.metrics is not None and targets.dim() == 1:
@@ -133,6 +139,7 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         return {"loss": loss}
 
     def predict_step(self, batch, batch_idx, dataloader_idx: Optional[int] = None) -> torch.Tensor:
+        self._flush_table()
         input_seq = batch[ITEM_SEQ_ENTRY_NAME]
         meta = get_additional_meta_data(self.model, batch)
         padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
@@ -200,6 +207,7 @@ class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
         return logits[torch.arange(input_seq.shape[0], device=logits.device), seq_length]
 
     def _last_position_logits(self, batch):
+        self._flush_table()
         input_seq = batch[ITEM_SEQ_ENTRY_NAME]
         if hasattr(self.model, "forward_rows"):
             L = input_seq.shape[1]
@@ -258,6 +266,7 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         return {"loss": loss}
 
     def _get_prediction_for_masked_item(self, batch, batch_idx=None) -> torch.Tensor:
+        self._flush_table()
         input_seq = batch[ITEM_SEQ_ENTRY_NAME]
         target_mask = input_seq.eq(self.item_tokenizer.mask_token_id)
         if target_mask.dim() == 3:

@@ -54,6 +54,46 @@ class TableGrad:
 
     def __init__(self):
         self.plan: Optional["SparseTablePlan"] = None
+        self.lazy: Optional["LazyTableState"] = None
+
+
+class LazyTableState:
+    """Exact lazy dense Adam for the item table (asme_lazy_adam_*): rows are caught up to the current
+    step only when read (before a forward that gathers them, or in flush()).  Bit-identical to updating
+    every row every step (same per-element fp32 operations, same per-step constants)."""
+
+    def __init__(self, param: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor):
+        self.param, self.exp_avg, self.exp_avg_sq = param, exp_avg, exp_avg_sq
+        self.last_step = torch.zeros(param.shape[0], dtype=torch.int32, device=param.device)
+        self.hist = torch.zeros(1024, 8, dtype=torch.float32, device=param.device)
+        self.step = 0
+
+    def record(self, step: int, lr, b1, b2, eps, wd):
+        if step >= self.hist.shape[0]:
+            grown = torch.zeros(2 * self.hist.shape[0], 8, dtype=torch.float32, device=self.hist.device)
+            grown[: self.hist.shape[0]] = self.hist
+            self.hist = grown
+        call("asme_lazy_adam_record_step", ptr(self.hist), step, lr, b1, b2, eps, wd, stream())
+        self.step = step
+
+    def catch_up(self, rows: Optional[torch.Tensor] = None, count: Optional[torch.Tensor] = None, cap: int = 0):
+        if self.step == 0:
+            return
+        V, D = self.param.shape
+        if rows is None:
+            cap = V
+        call("asme_lazy_adam_catch_up", ptr(rows), ptr(count), cap, ptr(self.last_step), ptr(self.param),
+             ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist), self.step, stream())
+
+    def apply(self, plan: "SparseTablePlan", step: int):
+        D = self.param.shape[1]
+        call("asme_lazy_adam_apply", ptr(plan.unique), ptr(plan.count), plan.capacity, ptr(plan.grad_rows),
+             ptr(self.last_step), ptr(self.param), ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist),
+             step, stream())
+
+    def flush(self):
+        """bring every row up to date (before evaluation, checkpointing or any other reader)."""
+        self.catch_up(None)
 
 
 class SparseTablePlan:
@@ -81,6 +121,10 @@ class SparseTablePlan:
             self._inverse[x.data_ptr(), tuple(x.shape)] = inverse[off:off + k].view(x.shape)
             off += k
         self.consumed = False
+        tg = getattr(table, "_asme_table_grad", None)
+        if tg is not None and tg.lazy is not None:
+            # rows gathered by this step's forward must carry every earlier (zero-gradient) update
+            tg.lazy.catch_up(self.unique, self.count, self.capacity)
 
     def inverse_of(self, ids: torch.Tensor) -> torch.Tensor:
         key = (ids.data_ptr(), tuple(ids.shape))

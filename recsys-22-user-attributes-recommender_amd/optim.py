@@ -13,13 +13,24 @@ import ctypes
 import torch
 
 from ._lib import call, ptr, stream
+from .ops import LazyTableState
 
 
 class FusedAdam(torch.optim.Optimizer):
-    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 lazy_table: bool = True):
         if lr < 0.0 or eps < 0.0 or weight_decay < 0.0:
             raise ValueError("invalid Adam hyper-parameter")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        self.lazy_table = lazy_table
+
+    def flush(self):
+        """Bring lazily-updated item tables fully up to date (exact dense-Adam state)."""
+        for group in self.param_groups:
+            for p in group["params"]:
+                tg = getattr(p, "_asme_table_grad", None)
+                if tg is not None and tg.lazy is not None:
+                    tg.lazy.flush()
 
     def _state(self, p):
         st = self.state[p]
@@ -49,13 +60,24 @@ class FusedAdam(torch.optim.Optimizer):
                     st = self._state(p)
                     st["step"] += 1
                     V, D = p.shape
-                    call("asme_adam_rows_step", ptr(p), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), V, D,
-                         ptr(plan.slot_map), ptr(plan.grad_rows), lr, b1, b2, eps, wd, st["step"], stream())
+                    if self.lazy_table:
+                        if tg.lazy is None:
+                            tg.lazy = LazyTableState(p, st["exp_avg"], st["exp_avg_sq"])
+                            tg.lazy.step = st["step"] - 1
+                            tg.lazy.last_step.fill_(st["step"] - 1)  # every row is current up to now
+                        tg.lazy.record(st["step"], lr, b1, b2, eps, wd)
+                        tg.lazy.apply(plan, st["step"])
+                    else:
+                        call("asme_adam_rows_step", ptr(p), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), V, D,
+                             ptr(plan.slot_map), ptr(plan.grad_rows), lr, b1, b2, eps, wd, st["step"], stream())
                     plan.release()
                     tg.plan = None
                     continue
                 if p.grad is None:
                     continue
+                if tg is not None and tg.lazy is not None:  # switching back to dense gradients
+                    tg.lazy.flush()
+                    tg.lazy = None
                 if p.grad.is_sparse:
                     raise RuntimeError("FusedAdam does not support torch sparse gradients")
                 st = self._state(p)

@@ -224,3 +224,59 @@ def test_sparse_table_plan_equals_dense(asme, dev):
         asme.FusedAdam([p], lr=1e-2, betas=(0.99, 0.998), weight_decay=1e-3).step()
     assert _rel(p_sparse, p_dense) < 1e-5
     assert int((slot_map != -1).sum()) == 0  # map reset after the update
+
+
+def test_lazy_adam_bit_exact_vs_dense(asme, dev):
+    """Exact catch-up: lazily replayed zero-gradient steps == the dense row update every step, bitwise."""
+    torch.manual_seed(6)
+    V, D, T, steps = 2000, 64, 300, 7
+    base = torch.randn(V, D, device=dev)
+    p_lazy = torch.nn.Parameter(base.clone())
+    p_lazy._asme_table_grad = asme.ops.TableGrad()
+    p_eager = torch.nn.Parameter(base.clone())
+    p_eager._asme_table_grad = asme.ops.TableGrad()
+    o_lazy = asme.FusedAdam([p_lazy], lr=3e-3, betas=(0.99, 0.998), weight_decay=1e-3, lazy_table=True)
+    o_eager = asme.FusedAdam([p_eager], lr=3e-3, betas=(0.99, 0.998), weight_decay=1e-3, lazy_table=False)
+    map_l = torch.full((V,), -1, dtype=torch.int32, device=dev)
+    map_e = torch.full((V,), -1, dtype=torch.int32, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    for step in range(steps):
+        hi = V if step % 2 == 0 else V // 10  # alternate wide / narrow id ranges: long and short gaps
+        ids = torch.randint(0, hi, (T,), device=dev, generator=gen)
+        rows = torch.randn(T, D, device=dev, generator=gen)
+        for p, mp, opt in ((p_lazy, map_l, o_lazy), (p_eager, map_e, o_eager)):
+            plan = asme.ops.SparseTablePlan(p, [ids], mp)
+            # the forward would gather these rows now: lazily-updated rows must equal eager rows
+            if p is p_lazy:
+                assert torch.equal(p_lazy.detach()[ids], p_eager.detach()[ids])
+            asme._lib.call("asme_scatter_add_rows", rows.data_ptr(), plan.inverse_of(ids).data_ptr(), T, D,
+                           plan.grad_rows.data_ptr(), plan.capacity, 1.0, asme._lib.stream())
+            p._asme_table_grad.plan = plan
+            opt.step()
+    o_lazy.flush()
+    assert torch.equal(p_lazy.detach(), p_eager.detach())
+    st_l, st_e = o_lazy.state[p_lazy], o_eager.state[p_eager]
+    assert torch.equal(st_l["exp_avg"], st_e["exp_avg"]) and torch.equal(st_l["exp_avg_sq"], st_e["exp_avg_sq"])
+
+
+def test_sasrec_sparse_lazy_matches_dense_training(asme, dev):
+    """Three SASRec-neg training steps: table_grad='sparse' (dedup + lazy exact Adam) vs 'dense'
+    (dense gradient + dense Adam) give the same parameters (fp32 summation order differs)."""
+    from helpers import build_model, load, state_dict
+    z = load("sasrec_neg")
+    results = []
+    for mode in ("dense", "sparse"):
+        model = build_model(asme, "sasrec_neg", z)
+        model.load_state_dict(state_dict(z))
+        model.to(dev)
+        tok = asme.tokenization.Tokenizer(int(z["cfg"][5]) - 3)
+        module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
+                                                               table_grad=mode)
+        opt = module.configure_optimizers()
+        batch = {k: torch.from_numpy(z[s]).to(dev) for k, s in
+                 (("item", "seq"), ("positive_samples", "pos"), ("negative_samples", "neg"))}
+        for i in range(3):
+            asme.modules.train_step(module, opt, None, batch, i)
+        results.append({k: v.detach().cpu() for k, v in model.state_dict().items()})  # flushes lazily-updated rows
+    for k in results[0]:
+        assert _rel(results[1][k], results[0][k]) < 1e-5, k
