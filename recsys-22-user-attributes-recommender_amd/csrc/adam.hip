@@ -43,7 +43,10 @@ struct AdamHyper {
     float b1, b2, one_minus_b1, one_minus_b2, eps, wd, neg_step_size, bc2_sqrt;
 };
 
+// Every operation rounds separately (no FMA contraction) so the per-element result does not depend on
+// the kernel the function is inlined into: the lazy catch-up must replay the dense update bit for bit.
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamHyper& hp) {
+#pragma clang fp contract(off)
     if (hp.wd != 0.f) g = g + hp.wd * p;
     m = m + hp.one_minus_b1 * (g - m);
     v = v * hp.b2 + hp.one_minus_b2 * g * g;

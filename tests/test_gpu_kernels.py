@@ -279,4 +279,6 @@ def test_sasrec_sparse_lazy_matches_dense_training(asme, dev):
             asme.modules.train_step(module, opt, None, batch, i)
         results.append({k: v.detach().cpu() for k, v in model.state_dict().items()})  # flushes lazily-updated rows
     for k in results[0]:
+        if k.endswith("attention.linear_layers.1.bias"):
+            continue  # exact gradient is 0 (softmax shift invariance): Adam follows fp32 noise, see test_gpu_models
         assert _rel(results[1][k], results[0][k]) < 1e-5, k
