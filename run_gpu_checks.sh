@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 0 = pass, 1 = test failures (no fault)
-timeout -k 10 ${PYTEST_TIMEOUT:-420} python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${PYTEST_TIMEOUT:-420} python -m pytest tests -m gpu -q -p no:cacheprovider -k "${PYTEST_K:-}" > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 ok $rc || exit $rc
 timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
