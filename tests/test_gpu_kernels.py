@@ -241,8 +241,9 @@ def test_lazy_adam_bit_exact_vs_dense(asme, dev):
     map_e = torch.full((V,), -1, dtype=torch.int32, device=dev)
     gen = torch.Generator(device=dev).manual_seed(0)
     for step in range(steps):
-        hi = V if step % 2 == 0 else V // 10  # alternate wide / narrow id ranges: long and short gaps
-        ids = torch.randint(0, hi, (T,), device=dev, generator=gen)
+        hi = V if step % 2 == 0 else V // 5  # alternate wide / narrow id ranges: long and short gaps
+        # distinct ids: the compact-row scatter uses fp32 atomics, whose order (not the Adam update) varies
+        ids = torch.randperm(hi, device=dev, generator=gen)[:T]
         rows = torch.randn(T, D, device=dev, generator=gen)
         for p, mp, opt in ((p_lazy, map_l, o_lazy), (p_eager, map_e, o_eager)):
             plan = asme.ops.SparseTablePlan(p, [ids], mp)
