@@ -112,20 +112,31 @@ def main():
     V = args.items + 3
     B, L, d = args.batch, args.seq_len, args.dim
 
-    torch.manual_seed(0)
+    torch.manual_seed(rank)
+    sharded = world > 1
+    # N > 1: the item table is row-sharded over the ranks (RCCL all-to-all of ids / rows / row grads,
+    # one all_reduce of the replicated dense gradients); N = 1: the whole table on the one GPU
+    rows = asme.sharded.shard_rows(V, world, rank) if sharded else V
     with torch.device(dev):
         model = asme.SASRecModel(transformer_hidden_size=d, num_transformer_heads=args.heads,
-                                 num_transformer_layers=args.layers, item_vocab_size=V, max_seq_length=L,
+                                 num_transformer_layers=args.layers, item_vocab_size=rows, max_seq_length=L,
                                  transformer_dropout=args.dropout)
     tok = asme.tokenization.Tokenizer(args.items)
-    module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
-                                                           table_grad=args.table_grad)
+    if sharded:
+        module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok,
+                                                                              metrics=None, vocab=V)
+        module.broadcast_dense_parameters()
+        step_fn = lambda b, i: asme.sharded.train_step(module, opt, b, i)  # noqa: E731
+    else:
+        module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
+                                                               table_grad=args.table_grad)
+        step_fn = lambda b, i: asme.modules.train_step(module, opt, None, b, i)  # noqa: E731
     module.train()
     opt = module.configure_optimizers()
     batches = [synthetic_batch(B, L, V, 1234 + 7 * (rank * 2 + i), dev, args.ids) for i in range(2)]
 
     for i in range(args.warmup):
-        asme.modules.train_step(module, opt, None, batches[i % 2], i)
+        step_fn(batches[i % 2], i)
     torch.cuda.synchronize()
 
     # per-kernel device time of the dominant kernel (HIP events on the launching stream)
@@ -138,7 +149,7 @@ def main():
     t0 = time.perf_counter()
     with timer:
         for i in range(args.steps):
-            asme.modules.train_step(module, opt, None, batches[i % 2], i)
+            step_fn(batches[i % 2], i)
         # lazily deferred zero-gradient Adam updates of the item table are part of the work: apply them
         # all (exact dense-Adam state) inside the timed region
         opt.flush()
@@ -174,7 +185,8 @@ def main():
         "config": {"workload": "sasrec-neg train step", "model": "SASRec", "global_batch": B * world,
                    "batch_per_gpu": B, "seq_len": L, "items": args.items, "dim": d, "heads": args.heads,
                    "layers": args.layers, "dropout": args.dropout, "table_grad": args.table_grad,
-                   "ids": args.ids, "parallelism": f"replicas{world}" if world > 1 else "single"},
+                   "ids": args.ids,
+                   "parallelism": f"dp{world}+rowshard{world}" if sharded else "single"},
         "roofline": roof,
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kstats.items() if v["count"]},
         "cpu_baseline": None,

@@ -241,13 +241,24 @@ __global__ __launch_bounds__(256) void pos_partial_kernel(const float* __restric
     }
 }
 
-__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int64_t nrows,
-                                                          int64_t width, float* __restrict__ out, int accumulate) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= width) return;
+// column sums of a (nrows, width) matrix: a block owns 64 columns; its 16 row-groups of 64 threads each
+// sum every 16th row (coalesced 256-B row segments), then a fixed-order LDS tree adds the 16 partials.
+constexpr int kRedCols = 64, kRedGroups = 16;
+__global__ __launch_bounds__(1024) void reduce_rows_kernel(const float* __restrict__ part, int64_t nrows,
+                                                           int64_t width, float* __restrict__ out, int accumulate) {
+    __shared__ float red[kRedGroups][kRedCols];
+    const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
+    const int64_t c = (int64_t)blockIdx.x * kRedCols + col;
     float s = 0.f;
-    for (int64_t r = 0; r < nrows; ++r) s += part[r * width + c];
-    out[c] = accumulate ? out[c] + s : s;
+    if (c < width)
+        for (int64_t r = grp; r < nrows; r += kRedGroups) s += part[r * width + c];
+    red[grp][col] = s;
+    __syncthreads();
+    for (int h = kRedGroups / 2; h > 0; h >>= 1) {
+        if (grp < h) red[grp][col] += red[grp + h][col];
+        __syncthreads();
+    }
+    if (grp == 0 && c < width) out[c] = accumulate ? out[c] + red[0][col] : red[0][col];
 }
 
 template <int VPL>
@@ -373,8 +384,8 @@ ASME_API int asme_position_grad(const float* rows, int64_t batch, int64_t seq_le
     hipLaunchKernelGGL(pos_partial_kernel, dim3((unsigned)seq_len, (unsigned)n_chunks), dim3(128), 0,
                        (hipStream_t)stream, rows, batch, seq_len, (int)dim, chunk, workspace);
     const int64_t width = seq_len * dim;
-    hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       workspace, n_chunks, width, grad_pos, accumulate);
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + kRedCols - 1) / kRedCols)), dim3(1024), 0,
+                       (hipStream_t)stream, workspace, n_chunks, width, grad_pos, accumulate);
     ASME_LAUNCH_CHECK("asme_position_grad");
 }
 
@@ -382,8 +393,8 @@ ASME_API int asme_reduce_rows(const float* part, int64_t n_rows, int64_t width, 
                               void* stream) {
     ASME_CHECK_ARG(part && out, "asme_reduce_rows: null pointer");
     if (width == 0) return 0;
-    hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       part, n_rows, width, out, accumulate);
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + kRedCols - 1) / kRedCols)), dim3(1024), 0,
+                       (hipStream_t)stream, part, n_rows, width, out, accumulate);
     ASME_LAUNCH_CHECK("asme_reduce_rows");
 }
 

@@ -89,7 +89,8 @@ class TransformerEmbedding(nn.Module):
         self.dropout = nn.Dropout(p=dropout)
 
     def get_item_embedding_weight(self) -> torch.Tensor:
-        return self.item_embedding.embedding.weight
+        override = getattr(self, "_table_override", None)
+        return override if override is not None else self.item_embedding.embedding.weight
 
     def fused_args(self):
         pos = self.position_embedding.weight if self.positional_embedding_active else None

@@ -99,21 +99,23 @@ class LazyTableState:
 class SparseTablePlan:
     """Per-step dedup of every id that touches the table: slot map, unique rows, compact grad."""
 
-    def __init__(self, table: torch.Tensor, id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor):
-        dev = table.device
+    def __init__(self, table: Optional[torch.Tensor], id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor,
+                 vocab: Optional[int] = None, dim: int = 0):
+        dev = slot_map.device
         flat = torch.cat([_i64(x).reshape(-1) for x in id_sets])
         n = flat.numel()
-        self.vocab, self.dim = table.shape
+        self.vocab, self.dim = table.shape if table is not None else (vocab, dim)
         self.slot_map = slot_map
-        ws_bytes = int(_lib.load().asme_dedup_workspace_bytes(n))
-        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
         self.unique = torch.empty(n, device=dev, dtype=torch.int64)
         inverse = torch.empty(n, device=dev, dtype=torch.int64)
-        self.count = torch.empty(1, device=dev, dtype=torch.int32)
-        call("asme_dedup_ids", ptr(flat), n, self.vocab, ptr(slot_map), ptr(ws), ws_bytes, ptr(self.unique),
-             ptr(inverse), ptr(self.count), stream())
+        self.count = torch.zeros(1, device=dev, dtype=torch.int32)
+        if n > 0:
+            ws_bytes = int(_lib.load().asme_dedup_workspace_bytes(n))
+            ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+            call("asme_dedup_ids", ptr(flat), n, self.vocab, ptr(slot_map), ptr(ws), ws_bytes, ptr(self.unique),
+                 ptr(inverse), ptr(self.count), stream())
         self.capacity = n
-        self.grad_rows = torch.zeros(n, self.dim, device=dev, dtype=torch.float32)
+        self._grad_rows = None
         self._inverse = {}
         off = 0
         for x in id_sets:
@@ -121,10 +123,26 @@ class SparseTablePlan:
             self._inverse[x.data_ptr(), tuple(x.shape)] = inverse[off:off + k].view(x.shape)
             off += k
         self.consumed = False
-        tg = getattr(table, "_asme_table_grad", None)
+        tg = getattr(table, "_asme_table_grad", None) if table is not None else None
         if tg is not None and tg.lazy is not None:
             # rows gathered by this step's forward must carry every earlier (zero-gradient) update
             tg.lazy.catch_up(self.unique, self.count, self.capacity)
+
+    @classmethod
+    def for_ids(cls, vocab: int, id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor) -> "SparseTablePlan":
+        """dedup only (no table attached): unique ids in first-occurrence order + inverse per id set"""
+        return cls(None, id_sets, slot_map, vocab=vocab, dim=0)
+
+    @property
+    def grad_rows(self) -> torch.Tensor:
+        """compact (capacity, d) gradient rows, slot s <-> unique[s] (allocated on first use)"""
+        if self._grad_rows is None:
+            self._grad_rows = torch.zeros(self.capacity, self.dim, device=self.unique.device, dtype=torch.float32)
+        return self._grad_rows
+
+    def n_unique(self) -> int:
+        """number of distinct ids (device -> host sync)"""
+        return int(self.count.item())
 
     def inverse_of(self, ids: torch.Tensor) -> torch.Tensor:
         key = (ids.data_ptr(), tuple(ids.shape))
@@ -251,6 +269,13 @@ class _GatherSumFn(torch.autograd.Function):
         if has_bias:
             g_bias = _reduce_rows(dout)
         return None, g_table, g_bias, None
+
+
+def scatter_add_rows(rows: torch.Tensor, ids: torch.Tensor, dest: torch.Tensor, scale: float = 1.0):
+    """dest[ids[r]] += scale * rows[r]  (fp32 atomics)"""
+    rows, ids = _f32(rows), _i64(ids)
+    call("asme_scatter_add_rows", ptr(rows), ptr(ids), ids.numel(), rows.shape[1], ptr(dest), dest.shape[0], scale,
+         stream())
 
 
 def _reduce_rows(x: torch.Tensor) -> torch.Tensor:

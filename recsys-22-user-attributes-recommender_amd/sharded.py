@@ -1,0 +1,187 @@
+"""Row-sharded item table across ranks (one process per GPU, RCCL over xGMI) for SASRec-neg training.
+
+The reference trains under Lightning DDP: every rank holds the whole |V| x d table, its dense gradient
+is all-reduced and every rank runs dense Adam over all of it.  Here the table is
+row-sharded cyclically (global row g -> owner g % W, local row g // W, which spreads Zipf heads) and
+only the rows a step touches cross the fabric:
+
+  forward   dedup the step's ids (asme_dedup_ids) -> route unique ids to their owners (all_to_all of
+            int64 ids) -> owners bring those rows up to date (lazy exact Adam catch-up) and gather them
+            -> all_to_all of the rows back -> the model runs on the compact (U, d) table with remapped ids
+  backward  all_to_all of the compact row gradients to the owners (x 1/W: DDP gradient averaging) ->
+            owners scatter-add into their step plan -> lazy dense Adam on the shard
+  dense params (transformer, position table, LayerNorms) stay replicated; their gradients are
+            averaged with one flat all_reduce.
+Numerically this is DDP semantics: per-rank mean loss, gradients averaged over ranks, dense Adam over
+every row of the (logical) table.
+
+`RowShardExchange` is pure torch.distributed routing (works on gloo/CPU for tests); the data path
+around it (dedup, catch-up, gather, scatter, Adam) runs on the gfx950 kernels.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .modules import (ITEM_SEQ_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME,
+                      SequenceNextItemPredictionTrainingModule, get_additional_meta_data, get_padding_mask)
+from .sequence import InputSequence
+
+
+def shard_rows(vocab: int, world: int, rank: int) -> int:
+    """number of global rows {rank, rank + W, ...} < vocab owned by `rank`"""
+    return max(0, (vocab - rank + world - 1) // world)
+
+
+@dataclass
+class ExchangeState:
+    order: torch.Tensor          # permutation sorting the requester's unique ids by owner
+    send_counts: List[int]       # ids sent to each owner
+    recv_counts: List[int]       # ids received from each requester
+    recv_local: torch.Tensor     # local row ids requested from this rank, grouped by requester
+
+
+class RowShardExchange:
+    def __init__(self, vocab: int, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.vocab = vocab
+        self.local_rows = shard_rows(vocab, self.world, self.rank)
+
+    def request(self, unique: torch.Tensor) -> ExchangeState:
+        """route the requester's unique global ids to their owners"""
+        W = self.world
+        owner = unique % W
+        order = torch.argsort(owner, stable=True)
+        send_counts_t = torch.bincount(owner, minlength=W).to(torch.int64)
+        recv_counts_t = torch.empty_like(send_counts_t)
+        dist.all_to_all_single(recv_counts_t, send_counts_t, group=self.group)
+        counts = torch.stack([send_counts_t, recv_counts_t]).cpu()  # one host sync per step
+        sc, rc = counts[0].tolist(), counts[1].tolist()
+        send_local = (unique.index_select(0, order) // W).contiguous()
+        recv_local = torch.empty(sum(rc), dtype=torch.int64, device=unique.device)
+        dist.all_to_all_single(recv_local, send_local, rc, sc, group=self.group)
+        return ExchangeState(order, sc, rc, recv_local)
+
+    def reply_rows(self, st: ExchangeState, rows: torch.Tensor) -> torch.Tensor:
+        """owners' rows (aligned with st.recv_local) -> the requester's rows aligned with its unique ids"""
+        U = len(st.order)
+        got = torch.empty(U, rows.shape[1], dtype=rows.dtype, device=rows.device)
+        dist.all_to_all_single(got, rows.contiguous(), st.send_counts, st.recv_counts, group=self.group)
+        out = torch.empty_like(got)
+        out.index_copy_(0, st.order, got)
+        return out
+
+    def push_grads(self, st: ExchangeState, grad_unique: torch.Tensor) -> torch.Tensor:
+        """requester's gradient rows (aligned with its unique ids) -> owners, aligned with st.recv_local"""
+        send = grad_unique.index_select(0, st.order).contiguous()
+        recv = torch.empty(len(st.recv_local), grad_unique.shape[1], dtype=grad_unique.dtype,
+                           device=grad_unique.device)
+        dist.all_to_all_single(recv, send, st.recv_counts, st.send_counts, group=self.group)
+        return recv
+
+
+class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPredictionTrainingModule):
+    """sasrec-neg training with the item table row-sharded over the process group.
+
+    Build the model with item_vocab_size = shard_rows(V, W, rank) (the local shard); `vocab` is the
+    global |V|.  Call `after_backward()` between loss.backward() and optimizer.step() (train_step in
+    this module does it)."""
+
+    def __init__(self, model, item_tokenizer, metrics, vocab: int, learning_rate: float = 0.001,
+                 beta_1: float = 0.99, beta_2: float = 0.998, weight_decay: float = 1e-3, loss_function=None,
+                 group=None):
+        super().__init__(model, item_tokenizer, metrics, learning_rate, beta_1, beta_2, weight_decay,
+                         loss_function, table_grad="sparse")
+        self.exchange = RowShardExchange(vocab, group)
+        self.vocab = vocab
+        self.group = group
+        shard = model.item_table()
+        if shard.shape[0] != self.exchange.local_rows:
+            raise ValueError(f"model item table has {shard.shape[0]} rows, shard needs {self.exchange.local_rows}")
+        self._req_map: Optional[torch.Tensor] = None
+        self._own_map: Optional[torch.Tensor] = None
+        self._pending = None
+
+    def broadcast_dense_parameters(self, src: int = 0):
+        """make the replicated (non-table) parameters identical on every rank"""
+        shard = self.model.item_table()
+        for p in self.model.parameters():
+            if p is not shard:
+                dist.broadcast(p.data, src, group=self.group)
+
+    def _maps(self, dev):
+        if self._req_map is None:
+            self._req_map = torch.full((self.vocab,), -1, dtype=torch.int32, device=dev)
+            self._own_map = torch.full((max(1, self.exchange.local_rows),), -1, dtype=torch.int32, device=dev)
+
+    def training_step(self, batch, batch_idx):
+        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
+        pos, neg = batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]
+        shard = self.model.item_table()
+        self._maps(shard.device)
+        # 1. requester: dedup every id of the step
+        req = ops.SparseTablePlan.for_ids(self.vocab, [input_seq, pos, neg], self._req_map)
+        U = req.n_unique()
+        unique = req.unique[:U]
+        # 2. route ids to owners; owners catch their rows up (lazy Adam) and gather them
+        st = self.exchange.request(unique)
+        own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
+        with torch.no_grad():
+            rows = ops.gather_sum(st.recv_local, shard.detach(), None, skip_zero=False) if len(st.recv_local) \
+                else shard.new_empty(0, shard.shape[1])
+        compact = self.exchange.reply_rows(st, rows).requires_grad_(True)
+        compact._asme_table_grad = ops.TableGrad()
+        inv_seq, inv_pos, inv_neg = (req.inverse_of(x) for x in (input_seq, pos, neg))
+        req.release()
+        # 3. the model runs on the compact table
+        emb = self.model._sequence_embedding_layer.item_embedding_layer
+        meta = get_additional_meta_data(self.model, batch)
+        meta["positive_samples"], meta["negative_samples"] = inv_pos, inv_neg
+        padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
+        emb._table_override = compact
+        try:
+            pos_logits, neg_logits = self.model(InputSequence(inv_seq, padding_mask, meta))
+        finally:
+            emb._table_override = None
+        loss = self.loss_function(pos_logits, neg_logits, mask=input_seq.ne(self.item_tokenizer.pad_token_id))
+        self._pending = (st, own, compact)
+        return {"loss": loss}
+
+    @torch.no_grad()
+    def after_backward(self):
+        """route the compact table gradient to the owners and average the replicated gradients"""
+        st, own, compact = self._pending
+        self._pending = None
+        W = self.exchange.world
+        g = compact.grad if compact.grad is not None else torch.zeros_like(compact)
+        recv = self.exchange.push_grads(st, g)
+        shard = self.model.item_table()
+        if len(st.recv_local):
+            ops.scatter_add_rows(recv, own.inverse_of(st.recv_local), own.grad_rows, 1.0 / W)
+        shard._asme_table_grad.plan = own
+        dense = [p for p in self.model.parameters() if p is not shard and p.grad is not None]
+        if dense and W > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in dense])
+            dist.all_reduce(flat, group=self.group)
+            flat.mul_(1.0 / W)
+            off = 0
+            for p in dense:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
+
+
+def train_step(module, optimizer, batch, batch_idx: int = 0):
+    out = module.training_step(batch, batch_idx)
+    loss = out["loss"]
+    loss.backward()
+    module.after_backward()
+    optimizer.step()
+    optimizer.zero_grad(set_to_none=True)
+    return loss

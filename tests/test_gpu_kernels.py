@@ -283,3 +283,44 @@ def test_sasrec_sparse_lazy_matches_dense_training(asme, dev):
         if k.endswith("attention.linear_layers.1.bias"):
             continue  # exact gradient is 0 (softmax shift invariance): Adam follows fp32 noise, see test_gpu_models
         assert _rel(results[1][k], results[0][k]) < 1e-5, k
+
+
+def test_sharded_module_single_rank_matches_unsharded(asme, dev):
+    """The row-sharded training path (dedup -> all_to_all routing -> owner catch-up/gather -> compact
+    table -> grad push -> lazy Adam on the shard) on a 1-rank RCCL group equals plain training."""
+    import os
+    import torch.distributed as dist
+    from helpers import build_model, load, state_dict
+    z = load("sasrec_neg")
+    V = int(z["cfg"][5])
+    batch = {k: torch.from_numpy(z[s]).to(dev) for k, s in
+             (("item", "seq"), ("positive_samples", "pos"), ("negative_samples", "neg"))}
+    tok = asme.tokenization.Tokenizer(V - 3)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        out = []
+        for sharded in (False, True):
+            model = build_model(asme, "sasrec_neg", z)
+            model.load_state_dict(state_dict(z))
+            model.to(dev)
+            if sharded:
+                module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(
+                    model=model, item_tokenizer=tok, metrics=None, vocab=V)
+                opt = module.configure_optimizers()
+                for i in range(3):
+                    asme.sharded.train_step(module, opt, batch, i)
+            else:
+                module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
+                                                                       table_grad="sparse")
+                opt = module.configure_optimizers()
+                for i in range(3):
+                    asme.modules.train_step(module, opt, None, batch, i)
+            out.append({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    finally:
+        dist.destroy_process_group()
+    for k in out[0]:
+        if k.endswith("attention.linear_layers.1.bias"):
+            continue
+        assert _rel(out[1][k], out[0][k]) < 1e-5, k
