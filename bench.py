@@ -147,13 +147,26 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    last_unique = []
+    _orig_release = asme.ops.SparseTablePlan.release
+
+    def _release(plan):  # record the unique-row count of the step (for the byte accounting)
+        if plan.dim and not last_unique:
+            last_unique.append(plan.n_unique())
+        _orig_release(plan)
+
+    asme.ops.SparseTablePlan.release = _release
     with timer:
         for i in range(args.steps):
             step_fn(batches[i % 2], i)
-        # lazily deferred zero-gradient Adam updates of the item table are part of the work: apply them
-        # all (exact dense-Adam state) inside the timed region
-        opt.flush()
+    # lazily deferred zero-gradient Adam updates of the item table are part of the work: apply them all
+    # (exact dense-Adam state) inside the timed region, timed on its own
+    f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    f0.record()
+    opt.flush()
+    f1.record()
     torch.cuda.synchronize()
+    flush_ms = f0.elapsed_time(f1)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -165,17 +178,36 @@ def main():
     value = B * world * args.steps / elapsed
 
     kstats = timer.summary()
-    adam = kstats.get("asme_adam_rows_step")
-    roof = None
-    if adam and adam["count"]:
-        # algorithmic bytes per launch: read+write p, m, v over all V rows (6*V*d*4) + row_slot (V*4)
-        # + the compact gradient rows of the step's unique ids (U*d*4; U <= 3*B*L)
-        U = min(3 * B * L, V)
-        bytes_per = 6 * V * d * 4 + V * 4 + U * d * 4
-        achieved = bytes_per / (adam["avg_ms"] / 1e3) / 1e9
-        roof = {"kernel": "asme_adam_rows_step", "bound": "hbm", "achieved": round(achieved, 1),
-                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                "avg_ms": round(adam["avg_ms"], 4), "algorithmic_bytes_per_launch": bytes_per}
+    U = int(last_unique[0]) if last_unique else min(3 * B * L, V)
+    T = B * L
+    H, dk = args.heads, d // args.heads
+    # algorithmic work per launch; dense attention counts as in SURVEY §8d
+    work = {
+        "asme_attention_fwd": ("mfma", 4.0 * B * H * L * L * dk),
+        "asme_attention_bwd": ("mfma", 8.0 * B * H * L * L * dk),
+        "asme_embedding_fwd": ("hbm", T * 8 + 2 * T * d * 4 + T * 16),
+        "asme_embedding_bwd": ("hbm", T * 8 + 3 * T * d * 4 + T * 16),
+        "asme_lazy_adam_apply": ("hbm", U * 8 + U * d * 4 + 6 * U * d * 4 + U * 4),
+        "asme_lazy_adam_catch_up": ("hbm", U * 8 + 6 * U * d * 4 + 2 * U * 4),
+        "asme_gelu_dropout_bwd": ("hbm", 3 * T * 4 * d * 4),
+        "asme_adam_rows_step": ("hbm", 6 * V * d * 4 + V * 4 + U * d * 4),
+    }
+    rooflines = []
+    for name, st in kstats.items():
+        if not st["count"] or name not in work:
+            continue
+        bound, amount = work[name]
+        secs = st["avg_ms"] / 1e3
+        if bound == "mfma":
+            ach, peak, unit = amount / secs / 1e12, PEAK_FP32_MFMA_TFS, "TFLOP/s"
+        else:
+            ach, peak, unit = amount / secs / 1e9, PEAK_HBM_GBS, "GB/s"
+        rooflines.append({"kernel": name, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                          "frac": round(ach / peak, 4), "traffic": None, "avg_ms": round(st["avg_ms"], 4),
+                          "launches": st["count"], "total_ms": round(st["total_ms"], 3),
+                          ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): amount})
+    rooflines.sort(key=lambda r: -r["total_ms"])
+    roof = rooflines[0] if rooflines else None
 
     result = {
         "metric": "training sequences/sec at B=1024 L=200 |I|=10M (SASRec-neg, fwd+bwd+Adam)",
@@ -188,7 +220,8 @@ def main():
                    "ids": args.ids,
                    "parallelism": f"dp{world}+rowshard{world}" if sharded else "single"},
         "roofline": roof,
-        "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kstats.items() if v["count"]},
+        "rooflines": rooflines,
+        "flush_ms": round(flush_ms, 3),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
