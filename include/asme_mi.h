@@ -107,6 +107,14 @@ int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t l
                        int causal, float scale, float p_drop, uint64_t seed, float* dsum_ws, float* dq, int64_t ld_dq,
                        float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream);
 
+/* ---- Linear weight/bias gradient (autograd of nn.Linear in transformer_layers.py:175-220):
+ * dW (out x in) (+)= dY^T X, db (out) (+)= sum_t dY, split over the token dimension into fp32 partial
+ * slabs (workspace) summed in a fixed order.  Features and strides multiples of 4 floats. */
+int64_t asme_linear_weight_grad_workspace(int64_t n_tokens, int64_t out_features, int64_t in_features);
+int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float* x, int64_t ld_x, int64_t n_tokens,
+                            int64_t out_features, int64_t in_features, float* workspace, int64_t workspace_bytes,
+                            float* dw, float* db, int accumulate, void* stream);
+
 /* ---- heads & losses -----------------------------------------------------------------------
  * sampled head (core/models/sasrec/components.py:34-44): pos_out[t] = <hidden[t], table[pos_ids[t]]> */
 int asme_sampled_logits_fwd(const float* hidden, const float* table, const int64_t* pos_ids, const int64_t* neg_ids,

@@ -50,12 +50,15 @@ SIGNATURES = {
     "asme_lazy_adam_record_step": [p, i64, f32, f32, f32, f32, f32, p],
     "asme_lazy_adam_catch_up": [p, p, i64, p, p, p, p, i64, p, i64, p],
     "asme_lazy_adam_apply": [p, p, i64, p, p, p, p, p, i64, p, i64, p],
+    "asme_linear_weight_grad_workspace": [i64, i64, i64],
+    "asme_linear_weight_grad": [p, i64, p, i64, i64, i64, i64, p, i64, p, p, i32, p],
     "asme_dedup_workspace_bytes": [i64],
     "asme_dedup_ids": [p, i64, i64, p, p, i64, p, p, p, p],
     "asme_dedup_reset": [p, p, i64, p, p],
     "asme_owner_histogram": [p, p, i64, i32, p, p, p],
 }
-_RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64}
+_RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64,
+             "asme_linear_weight_grad_workspace": ctypes.c_int64}
 
 _lib: Optional[ctypes.CDLL] = None
 

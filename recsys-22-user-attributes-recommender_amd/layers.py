@@ -246,13 +246,13 @@ class TransformerLayer(nn.Module):
         for i, blk in enumerate(blocks):
             att, ff = blk.attention, blk.feed_forward
             w_qkv, b_qkv = att.qkv_weights()
-            qkv = F.linear(ln, w_qkv, b_qkv)
+            qkv = ops.linear(ln, w_qkv, b_qkv)
             o = ops.attention(qkv, key_valid, att.heads, causal, _p(att.dropout, tr))
-            a = F.linear(o, att.output_linear.weight, att.output_linear.bias)
+            a = ops.linear(o, att.output_linear.weight, att.output_linear.bias)
             h1, ln2 = ops.residual_ln(x, a, blk.output_sublayer.norm, _p(blk.input_sublayer.dropout, tr), 0.0)
-            f = F.linear(ln2, ff.w_1.weight, ff.w_1.bias)
+            f = ops.linear(ln2, ff.w_1.weight, ff.w_1.bias)
             g = ops.gelu_dropout(f, _p(ff.dropout, tr))
-            f2 = F.linear(g, ff.w_2.weight, ff.w_2.bias)
+            f2 = ops.linear(g, ff.w_2.weight, ff.w_2.bias)
             nxt = blocks[i + 1].input_sublayer.norm if i + 1 < len(blocks) else None
             x, ln = ops.residual_ln(h1, f2, nxt, _p(blk.output_sublayer.dropout, tr), _p(blk.dropout, tr))
         return x

@@ -289,6 +289,45 @@ def gather_sum(ids, table, bias=None, skip_zero=False):
     return _GatherSumFn.apply(ids, table, bias, skip_zero)
 
 
+# ------------------------------------------------------------------------------------ linear
+class _LinearFn(torch.autograd.Function):
+    """nn.Linear with the weight/bias gradient on the split-token MFMA kernel (asme_linear_weight_grad);
+    the forward and the input gradient are plain library GEMMs (hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        N, K = w.shape
+        dy2 = dy.reshape(-1, N)
+        x2 = x.reshape(-1, K)
+        dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dy2, x2 = _f32(dy2), _f32(x2)
+            if N % 4 == 0 and K % 4 == 0:
+                T = x2.shape[0]
+                nbytes = int(_lib.load().asme_linear_weight_grad_workspace(T, N, K))
+                ws = torch.empty(max(4, nbytes // 4), device=x.device, dtype=torch.float32)
+                dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+                db = torch.empty(N, device=x.device, dtype=torch.float32) if ctx.has_bias else None
+                call("asme_linear_weight_grad", ptr(dy2), N, ptr(x2), K, T, N, K, ptr(ws), nbytes, ptr(dw), ptr(db),
+                     0, stream())
+            else:  # shapes the kernel does not tile: library GEMM
+                dw = dy2.t() @ x2
+                db = dy2.sum(0) if ctx.has_bias else None
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    return _LinearFn.apply(x, w, b)
+
+
 # ------------------------------------------------------------------------------------ layer norm
 class _LayerNormFn(torch.autograd.Function):
     """nn.LayerNorm over the last dim (fp32, biased variance)."""

@@ -324,3 +324,21 @@ def test_sharded_module_single_rank_matches_unsharded(asme, dev):
         if k.endswith("attention.linear_layers.1.bias"):
             continue
         assert _rel(out[1][k], out[0][k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("T,N,K", [(1, 4, 4), (33, 128, 128), (1000, 384, 128), (4099, 128, 512), (70000, 512, 128),
+                                   (517, 36, 200)])
+def test_linear_weight_grad(asme, dev, T, N, K):
+    """dW = dY^T X and db = sum dY (split-token MFMA kernel) vs an fp64 reference."""
+    torch.manual_seed(T + N + K)
+    x = torch.randn(T, K, device=dev)
+    w = torch.randn(N, K, device=dev, requires_grad=True)
+    b = torch.randn(N, device=dev, requires_grad=True)
+    xx = x.clone().requires_grad_(True)
+    y = asme.ops.linear(xx, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref_w = (dy.double().t() @ x.double())
+    ref_b = dy.double().sum(0)
+    assert _rel(w.grad, ref_w) < 1e-5 and _rel(b.grad, ref_b) < 1e-5
+    assert _rel(xx.grad, dy.double() @ w.detach().double()) < 1e-5
