@@ -239,6 +239,83 @@ __global__ __launch_bounds__(256) void lazy_catch_up_kernel(const int64_t* __res
     if (lane == 0) last_step[r] = upto;
 }
 
+// float4 variant for D % 4 == 0, D <= 256: a row is D/4 lanes (16-B accesses), a wave holds 256/D rows,
+// and each lane carries four independent replay chains (more ILP for the latency-bound recurrence).
+template <int LPR>
+__global__ __launch_bounds__(256) void lazy_catch_up_v4_kernel(const int64_t* __restrict__ rows,
+                                                               const int32_t* __restrict__ count, int64_t cap,
+                                                               int32_t* __restrict__ last_step,
+                                                               float* __restrict__ p, float* __restrict__ m,
+                                                               float* __restrict__ v,
+                                                               const AdamHyper* __restrict__ hist, int32_t upto) {
+    constexpr int D = LPR * 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LPR) + lane / LPR;
+    const int64_t n = count ? (int64_t)*count : cap;
+    if (s >= n || s >= cap) return;
+    const int64_t r = rows ? rows[s] : s;
+    const int32_t t0 = last_step[r];
+    if (t0 >= upto) return;
+    const int64_t off = r * D + (lane % LPR) * 4;
+    float4 P = *reinterpret_cast<const float4*>(p + off);
+    float4 M = *reinterpret_cast<const float4*>(m + off);
+    float4 Vv = *reinterpret_cast<const float4*>(v + off);
+    for (int32_t t = t0 + 1; t <= upto; ++t) {
+        const AdamHyper hp = hist[t];
+        adam_elem(P.x, 0.f, M.x, Vv.x, hp);
+        adam_elem(P.y, 0.f, M.y, Vv.y, hp);
+        adam_elem(P.z, 0.f, M.z, Vv.z, hp);
+        adam_elem(P.w, 0.f, M.w, Vv.w, hp);
+    }
+    *reinterpret_cast<float4*>(p + off) = P;
+    *reinterpret_cast<float4*>(m + off) = M;
+    *reinterpret_cast<float4*>(v + off) = Vv;
+    if (lane % LPR == 0) last_step[r] = upto;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void lazy_apply_v4_kernel(const int64_t* __restrict__ rows,
+                                                            const int32_t* __restrict__ count, int64_t cap,
+                                                            const float* __restrict__ grad_rows,
+                                                            int32_t* __restrict__ last_step, float* __restrict__ p,
+                                                            float* __restrict__ m, float* __restrict__ v,
+                                                            const AdamHyper* __restrict__ hist, int32_t step) {
+    constexpr int D = LPR * 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LPR) + lane / LPR;
+    if (s >= cap || s >= (int64_t)*count) return;
+    const int64_t r = rows[s];
+    const AdamHyper hp = hist[step];
+    const int c = (lane % LPR) * 4;
+    const int64_t off = r * D + c;
+    float4 P = *reinterpret_cast<const float4*>(p + off);
+    float4 M = *reinterpret_cast<const float4*>(m + off);
+    float4 Vv = *reinterpret_cast<const float4*>(v + off);
+    const float4 G = *reinterpret_cast<const float4*>(grad_rows + s * D + c);
+    adam_elem(P.x, G.x, M.x, Vv.x, hp);
+    adam_elem(P.y, G.y, M.y, Vv.y, hp);
+    adam_elem(P.z, G.z, M.z, Vv.z, hp);
+    adam_elem(P.w, G.w, M.w, Vv.w, hp);
+    *reinterpret_cast<float4*>(p + off) = P;
+    *reinterpret_cast<float4*>(m + off) = M;
+    *reinterpret_cast<float4*>(v + off) = Vv;
+    if (lane % LPR == 0) last_step[r] = step;
+}
+
+#define ASME_LPR_DISPATCH(DIM, ...)                                             \
+    switch (DIM) {                                                              \
+        case 32: { constexpr int LPR = 8; __VA_ARGS__; } break;                 \
+        case 64: { constexpr int LPR = 16; __VA_ARGS__; } break;                \
+        case 128: { constexpr int LPR = 32; __VA_ARGS__; } break;               \
+        case 256: { constexpr int LPR = 64; __VA_ARGS__; } break;               \
+        default: break;                                                         \
+    }
+
+inline bool v4_ok(int64_t dim, const void* a, const void* b, const void* c) {
+    return (dim == 32 || dim == 64 || dim == 128 || dim == 256) &&
+           ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c)) & 15) == 0;
+}
+
 // the real-gradient update of the step's unique rows (they were caught up to step-1 before the forward)
 template <int VPL>
 __global__ __launch_bounds__(256) void lazy_apply_kernel(const int64_t* __restrict__ rows,
@@ -296,6 +373,15 @@ ASME_API int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, 
     ASME_CHECK_ARG(last_step && param && exp_avg && exp_avg_sq && hist, "asme_lazy_adam_catch_up: null pointer");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && upto >= 0 && upto < (1LL << 31), "asme_lazy_adam_catch_up: bad shape");
     if (cap == 0 || upto == 0) return 0;
+    if (v4_ok(dim, param, exp_avg, exp_avg_sq)) {
+        const int64_t rows_per_block = 4 * (256 / dim);
+        const dim3 g4((unsigned)((cap + rows_per_block - 1) / rows_per_block));
+        ASME_LPR_DISPATCH(dim, hipLaunchKernelGGL(lazy_catch_up_v4_kernel<LPR>, g4, dim3(256), 0,
+                                                  (hipStream_t)stream, rows, count, cap, last_step, param, exp_avg,
+                                                  exp_avg_sq, reinterpret_cast<const AdamHyper*>(hist),
+                                                  (int32_t)upto));
+        ASME_LAUNCH_CHECK("asme_lazy_adam_catch_up");
+    }
     const dim3 grid((unsigned)((cap + 3) / 4));
     ASME_VPL_DISPATCH((int)((dim + 63) / 64),
                       hipLaunchKernelGGL(lazy_catch_up_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, rows,
@@ -311,6 +397,15 @@ ASME_API int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int
                    "asme_lazy_adam_apply: null pointer");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && step >= 1, "asme_lazy_adam_apply: bad shape");
     if (cap == 0) return 0;
+    if (v4_ok(dim, param, exp_avg, exp_avg_sq) && ((uintptr_t)grad_rows & 15) == 0) {
+        const int64_t rows_per_block = 4 * (256 / dim);
+        const dim3 g4((unsigned)((cap + rows_per_block - 1) / rows_per_block));
+        ASME_LPR_DISPATCH(dim, hipLaunchKernelGGL(lazy_apply_v4_kernel<LPR>, g4, dim3(256), 0, (hipStream_t)stream,
+                                                  rows, count, cap, grad_rows, last_step, param, exp_avg,
+                                                  exp_avg_sq, reinterpret_cast<const AdamHyper*>(hist),
+                                                  (int32_t)step));
+        ASME_LAUNCH_CHECK("asme_lazy_adam_apply");
+    }
     const dim3 grid((unsigned)((cap + 3) / 4));
     ASME_VPL_DISPATCH((int)((dim + 63) / 64),
                       hipLaunchKernelGGL(lazy_apply_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, rows, count,
