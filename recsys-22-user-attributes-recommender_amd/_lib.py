@@ -35,9 +35,9 @@ SIGNATURES = {
     "asme_residual_ln_bwd": [p, i64, i64, f32, u64, f32, u64, p, p, p, p, p, p, p, i64, p],
     "asme_gelu_dropout_fwd": [p, i64, f32, u64, p, p],
     "asme_gelu_dropout_bwd": [p, p, i64, f32, u64, p, p],
-    "asme_attention_fwd": [p, p, p, i64, i64, i64, p, i64, i64, i64, i64, i32, f32, f32, u64, p, i64, p, p],
+    "asme_attention_fwd": [p, p, p, i64, i64, i64, p, i64, i64, i64, i64, i32, f32, f32, u64, p, i64, p, p, p],
     "asme_attention_bwd": [p, p, p, i64, i64, i64, p, i64, p, i64, p, p, i64, i64, i64, i64, i32, f32, f32, u64, p,
-                           p, i64, p, i64, p, i64, p],
+                           p, p, i64, p, i64, p, i64, p],
     "asme_sampled_logits_fwd": [p, p, p, p, i64, i64, i64, p, p, p],
     "asme_sampled_logits_bwd": [p, p, p, p, i64, i64, i64, p, p, p, p, p],
     "asme_sasrec_bce_fwd": [p, p, p, i64, p, i64, p, p],

@@ -54,6 +54,16 @@ __device__ __forceinline__ float4 attn_keep4(uint64_t seed, uint64_t row, int ke
 __device__ __forceinline__ float pick(const float4& v, int i) {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
+// The forward stores the attention-dropout decisions as one nibble per (query row, 4 keys)
+// (drop_mask: (B*H*L) x ceil(L/4) bytes, bit r = key 4j+r kept); the backward passes read them instead
+// of re-running Philox.
+__device__ __forceinline__ uint8_t keep_bits(const float4& f) {
+    return (uint8_t)((f.x != 0.f ? 1 : 0) | (f.y != 0.f ? 2 : 0) | (f.z != 0.f ? 4 : 0) | (f.w != 0.f ? 8 : 0));
+}
+__device__ __forceinline__ float4 bits_keep(uint8_t m, float p) {
+    const float k = 1.f / (1.f - p);
+    return make_float4(m & 1 ? k : 0.f, m & 2 ? k : 0.f, m & 4 ? k : 0.f, m & 8 ? k : 0.f);
+}
 
 // Stage the key-validity row of batch b in LDS; returns whether any key is valid and the last one.
 __device__ __forceinline__ void stage_valid(const uint8_t* __restrict__ key_valid, int b, int L, uint8_t* kv_s,
@@ -150,7 +160,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
                                                        int64_t ldv, float* __restrict__ o, int64_t ldo,
                                                        float* __restrict__ stats,
                                                        const uint8_t* __restrict__ key_valid, int H, int L,
-                                                       int causal, float scale, float p_drop, uint64_t seed) {
+                                                       int causal, float scale, float p_drop, uint64_t seed,
+                                                       uint8_t* __restrict__ drop_mask) {
     constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
     __shared__ __attribute__((aligned(16))) float Ks[kKT * S];
     __shared__ __attribute__((aligned(16))) float Vs[kKT * S];
@@ -182,6 +193,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
     for (int ct = 0; ct < NCT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     float m = kInitMax, l = 0.f;
     const uint64_t drow = (uint64_t)bh * L + (uint64_t)min(qi, L - 1);
+    const int L4 = (L + 3) / 4;
+    // wave-uniform work limits: waves whose 16 queries are all past L only help stage tiles; under a
+    // causal mask (and some admissible key) a 16-key sub-tile that starts after the wave's last query
+    // is fully masked and contributes exactly 0, so it is skipped.
+    const int wq0 = qblk + wave * 16;
+    const bool wave_live = wq0 < L;
+    const int wq_last = min(wq0 + 15, L - 1);
+    const bool skip_causal = causal && any_valid;
 
     Stage<DK> sk, sv;
     const int ntiles = (kmax + kKT - 1) / kKT;
@@ -199,6 +218,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
             sk.load(kh, ldk, k0 + kKT, L);
             sv.load(vh, ldv, k0 + kKT, L);
         }
+        if (!wave_live || (skip_causal && k0 > wq_last)) continue;
         floatx4 st[kNS];
 #pragma unroll
         for (int sub = 0; sub < kNS; ++sub) st[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -239,7 +259,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
         if (p_drop > 0.f) {
 #pragma unroll
             for (int sub = 0; sub < kNS; ++sub) {
-                const float4 f = attn_keep4(seed, drow, k0 + sub * 16 + 4 * g, p_drop);
+                const int key4 = k0 + sub * 16 + 4 * g;
+                const float4 f = attn_keep4(seed, drow, key4, p_drop);
+                if (drop_mask && qi < L && key4 < L) drop_mask[drow * L4 + key4 / 4] = keep_bits(f);
                 p[sub][0] *= f.x;
                 p[sub][1] *= f.y;
                 p[sub][2] *= f.z;
@@ -270,7 +292,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
     int64_t ldv, const float* __restrict__ o, int64_t ldo, const float* __restrict__ dout, int64_t lddo,
     const float* __restrict__ stats, float* __restrict__ dsum, float* __restrict__ dq, int64_t lddq,
-    const uint8_t* __restrict__ key_valid, int H, int L, int causal, float scale, float p_drop, uint64_t seed) {
+    const uint8_t* __restrict__ key_valid, int H, int L, int causal, float scale, float p_drop, uint64_t seed,
+    const uint8_t* __restrict__ drop_mask) {
     constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
     __shared__ __attribute__((aligned(16))) float Ks[kKT * S];
     __shared__ __attribute__((aligned(16))) float Vs[kKT * S];
@@ -307,6 +330,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const float mq = qok ? stats[((int64_t)bh * L + qi) * 2] : 0.f;
     const float iq = qok ? stats[((int64_t)bh * L + qi) * 2 + 1] : 0.f;
     const uint64_t drow = (uint64_t)bh * L + (uint64_t)min(qi, L - 1);
+    const int L4 = (L + 3) / 4;
+    const int wq0 = qblk + wave * 16;
+    const bool wave_live = wq0 < L;
+    const int wq_last = min(wq0 + 15, L - 1);
+    const bool skip_causal = causal && any_valid;
 
     floatx4 acc[NCT];
 #pragma unroll
@@ -328,6 +356,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
             sk.load(kh, ldk, k0 + kKT, L);
             sv.load(vh, ldv, k0 + kKT, L);
         }
+        if (!wave_live || (skip_causal && k0 > wq_last)) continue;
         floatx4 st[kNS], dpt[kNS];
 #pragma unroll
         for (int sub = 0; sub < kNS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -337,7 +366,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
 #pragma unroll
         for (int sub = 0; sub < kNS; ++sub) {
             float4 f = make_float4(1.f, 1.f, 1.f, 1.f);
-            if (p_drop > 0.f) f = attn_keep4(seed, drow, k0 + sub * 16 + 4 * g, p_drop);
+            const int key4 = k0 + sub * 16 + 4 * g;
+            if (p_drop > 0.f)
+                f = drop_mask ? bits_keep(key4 < L ? drop_mask[drow * L4 + key4 / 4] : (uint8_t)0, p_drop)
+                              : attn_keep4(seed, drow, key4, p_drop);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int key = k0 + sub * 16 + 4 * g + r;
@@ -367,7 +399,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
     int64_t ldv, const float* __restrict__ dout, int64_t lddo, const float* __restrict__ stats,
     const float* __restrict__ dsum, float* __restrict__ dk, int64_t lddk, float* __restrict__ dv, int64_t lddv,
-    const uint8_t* __restrict__ key_valid, int H, int L, int causal, float scale, float p_drop, uint64_t seed) {
+    const uint8_t* __restrict__ key_valid, int H, int L, int causal, float scale, float p_drop, uint64_t seed,
+    const uint8_t* __restrict__ drop_mask) {
     constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
     __shared__ __attribute__((aligned(16))) float Qs[kKT * S];
     __shared__ __attribute__((aligned(16))) float Ds[kKT * S];
@@ -397,6 +430,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) dvt[ct] = dkt[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+    const int L4 = (L + 3) / 4;
+    const int wk0 = kblk + wave * 16;
+    const bool wave_live = wk0 < L;
     // causal: queries before this key block see none of its keys (unless no key is valid at all)
     const int q_start = (causal && any_valid) ? kblk : 0;
     // keys of this block that no query can attend (past the last valid key) contribute nothing either
@@ -423,6 +459,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
             sq.load(qh, ldq, q0 + kKT, L);
             sd.load(doh, lddo, q0 + kKT, L);
         }
+        if (!wave_live) continue;
         floatx4 st[kNS], dpt[kNS];
 #pragma unroll
         for (int sub = 0; sub < kNS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -441,7 +478,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
                     const float sv_ = masked ? kMaskedScore : st[sub][r] * scale;
                     const float pr = __expf(sv_ - mx_s[ql]) * il_s[ql];
                     float f = 1.f;
-                    if (p_drop > 0.f) f = pick(attn_keep4(seed, (uint64_t)bh * L + qq, kj & ~3, p_drop), kj & 3);
+                    if (p_drop > 0.f) {
+                        const uint64_t row = (uint64_t)bh * L + qq;
+                        f = drop_mask ? ((drop_mask[row * L4 + kj / 4] >> (kj & 3)) & 1 ? 1.f / (1.f - p_drop) : 0.f)
+                                      : pick(attn_keep4(seed, row, kj & ~3, p_drop), kj & 3);
+                    }
                     pv = pr * f;
                     dsv = masked ? 0.f : pr * (dpt[sub][r] * f - dsum_s[ql]);
                 }
@@ -480,7 +521,7 @@ bool aligned16(const void* p, int64_t ld) { return ((uintptr_t)p & 15) == 0 && (
 ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k,
                                 int64_t ld_v, const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len,
                                 int64_t head_dim, int causal, float scale, float p_drop, uint64_t seed, float* out,
-                                int64_t ld_out, float* lse, void* stream) {
+                                int64_t ld_out, float* lse, uint8_t* drop_mask, void* stream) {
     ASME_CHECK_ARG(q && k && v && out && lse, "asme_attention_fwd: null pointer");
     ASME_CHECK_ARG(seq_len >= 1 && seq_len <= kMaxL, "asme_attention_fwd: seq_len must be in [1, 1024]");
     ASME_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "asme_attention_fwd: dropout p must be in [0,1)");
@@ -490,7 +531,7 @@ ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, 
     const dim3 grid((unsigned)((seq_len + kQB - 1) / kQB), (unsigned)(batch * heads));
     ASME_DK_DISPATCH(head_dim, hipLaunchKernelGGL(attn_fwd_kernel<DK>, grid, dim3(256), 0, (hipStream_t)stream, q, k,
                                                   v, ld_q, ld_k, ld_v, out, ld_out, lse, key_valid, (int)heads,
-                                                  (int)seq_len, causal, scale, p_drop, seed));
+                                                  (int)seq_len, causal, scale, p_drop, seed, drop_mask));
     ASME_LAUNCH_CHECK("asme_attention_fwd");
 }
 
@@ -498,8 +539,8 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
                                 int64_t ld_v, const float* out, int64_t ld_out, const float* dout, int64_t ld_dout,
                                 const float* lse, const uint8_t* key_valid, int64_t batch, int64_t heads,
                                 int64_t seq_len, int64_t head_dim, int causal, float scale, float p_drop,
-                                uint64_t seed, float* dsum_ws, float* dq, int64_t ld_dq, float* dk, int64_t ld_dk,
-                                float* dv, int64_t ld_dv, void* stream) {
+                                uint64_t seed, const uint8_t* drop_mask, float* dsum_ws, float* dq, int64_t ld_dq,
+                                float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream) {
     ASME_CHECK_ARG(q && k && v && out && dout && lse && dsum_ws && dq && dk && dv, "asme_attention_bwd: null pointer");
     ASME_CHECK_ARG(seq_len >= 1 && seq_len <= kMaxL, "asme_attention_bwd: seq_len must be in [1, 1024]");
     ASME_CHECK_ARG(aligned16(dq, ld_dq) && aligned16(dk, ld_dk) && aligned16(dv, ld_dv) && aligned16(q, ld_q) &&
@@ -513,9 +554,9 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
         head_dim,
         hipLaunchKernelGGL(attn_bwd_dq_kernel<DK>, grid, dim3(256), 0, s, q, k, v, ld_q, ld_k, ld_v, out, ld_out, dout,
                            ld_dout, lse, dsum_ws, dq, ld_dq, key_valid, (int)heads, (int)seq_len, causal, scale,
-                           p_drop, seed);
+                           p_drop, seed, drop_mask);
         hipLaunchKernelGGL(attn_bwd_dkdv_kernel<DK>, grid, dim3(256), 0, s, q, k, v, ld_q, ld_k, ld_v, dout,
                            ld_dout, lse, dsum_ws, dk, ld_dk, dv, ld_dv, key_valid, (int)heads, (int)seq_len, causal,
-                           scale, p_drop, seed));
+                           scale, p_drop, seed, drop_mask));
     ASME_LAUNCH_CHECK("asme_attention_bwd");
 }

@@ -10,7 +10,7 @@
 //
 // Layout: table (V, D) fp32 row-major; tokens t = b*L + s; activations (T, D) fp32.
 // One 64-lane wave owns one token row; lane l holds elements l + 64*j (coalesced 256-B segments).
-#include "common.h"
+#include "rows.h"
 
 using namespace asme;
 
@@ -18,198 +18,158 @@ namespace {
 
 constexpr int kWavesPerBlock = 4;
 
-template <int VPL>
-__device__ __forceinline__ void ln_stats(const float (&x)[VPL], int lane, int D, float eps, float& mean,
-                                         float& rstd) {
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) s += (lane + 64 * j < D) ? x[j] : 0.f;
-    mean = wave_sum(s) / (float)D;
-    float q = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const float c = (lane + 64 * j < D) ? x[j] - mean : 0.f;
-        q += c * c;
-    }
-    rstd = rsqrtf(wave_sum(q) / (float)D + eps);
-}
-
-template <int VPL>
+// One token row per LPR-lane group (rows.h): x = E[id] + P[pos]; y1 = LN1(x); z = drop1(y1) + extra;
+// out = drop2(LN2(z)).  stats[t] = (mean1, rstd1, mean2, rstd2).
+template <class R>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float eps1, float p1,
     uint64_t s1, const float* __restrict__ extra, const float* __restrict__ w2, const float* __restrict__ b2,
     float eps2, float p2, uint64_t s2, float* __restrict__ out, float* __restrict__ stats, int* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR;
+    const int64_t t = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * R::RPW + lane / R::LPR;
     if (t >= T) return;
     int64_t id = ids[t];
     if (id < 0 || id >= V) {
-        if (lane == 0 && err) atomicOr(err, 1);
+        if (sub == 0 && err) atomicOr(err, 1);
         id = 0;
     }
-    const float* row = table + id * D;
-    const float* prow = pos ? pos + (t % L) * D : nullptr;
-    float x[VPL];
+    RowVals<R> x, tmp;
+    row_load<R>(table + id * D, sub, D, x);
+    if (pos) {
+        row_load<R>(pos + (t % L) * D, sub, D, tmp);
 #pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        x[j] = e < D ? row[e] + (prow ? prow[e] : 0.f) : 0.f;
+        for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+            for (int i = 0; i < R::W; ++i) x[j][i] += tmp[j][i];
     }
     float m1 = 0.f, r1 = 1.f, m2 = 0.f, r2 = 1.f;
     if (w1) {
-        ln_stats<VPL>(x, lane, D, eps1, m1, r1);
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) x[j] = (x[j] - m1) * r1 * w1[e] + b1[e];
-        }
+        row_ln_stats<R>(x, sub, D, eps1, m1, r1);
+        row_normalise<R>(x, sub, D, m1, r1, tmp);
+        row_affine<R>(tmp, sub, D, w1, b1, x);
     }
     if (p1 > 0.f) {
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) x[j] *= dropout_factor(s1, 1u, (uint64_t)t * D + lane + 64 * j, p1);
+        row_keep<R>(s1, 1u, (uint64_t)t * D, sub, p1, tmp);
+        row_mul<R>(x, tmp);
     }
     if (extra) {
+        row_load<R>(extra + t * D, sub, D, tmp);
 #pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) x[j] += extra[t * D + e];
-        }
+        for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+            for (int i = 0; i < R::W; ++i) x[j][i] += tmp[j][i];
     }
     if (w2) {
-        ln_stats<VPL>(x, lane, D, eps2, m2, r2);
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) x[j] = (x[j] - m2) * r2 * w2[e] + b2[e];
-        }
+        row_ln_stats<R>(x, sub, D, eps2, m2, r2);
+        row_normalise<R>(x, sub, D, m2, r2, tmp);
+        row_affine<R>(tmp, sub, D, w2, b2, x);
     }
     if (p2 > 0.f) {
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) x[j] *= dropout_factor(s2, 2u, (uint64_t)t * D + lane + 64 * j, p2);
+        row_keep<R>(s2, 2u, (uint64_t)t * D, sub, p2, tmp);
+        row_mul<R>(x, tmp);
     }
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        if (e < D) out[t * D + e] = x[j];
-    }
-    if (lane == 0 && stats) {
-        stats[t * 4 + 0] = m1;
-        stats[t * 4 + 1] = r1;
-        stats[t * 4 + 2] = m2;
-        stats[t * 4 + 3] = r2;
-    }
+    row_store<R>(out + t * D, sub, D, x);
+    if (sub == 0 && stats)
+        *reinterpret_cast<float4*>(stats + t * 4) = make_float4(m1, r1, m2, r2);
 }
 
-// LayerNorm input-gradient for one row held by a wave: gx = rstd * (gy*w - mean(gy*w) - xhat*mean(gy*w*xhat))
-template <int VPL>
-__device__ __forceinline__ void ln_bwd_row(const float (&gy)[VPL], const float (&xhat)[VPL], const float* w, float rstd,
-                                           int lane, int D, float (&gx)[VPL]) {
-    float a = 0.f, b = 0.f;
-    float dxh[VPL];
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        dxh[j] = e < D ? gy[j] * w[e] : 0.f;
-        a += dxh[j];
-        b += dxh[j] * xhat[j];
-    }
-    a = wave_sum(a) / (float)D;
-    b = wave_sum(b) / (float)D;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) gx[j] = rstd * (dxh[j] - a - xhat[j] * b);
-}
-
-template <int VPL>
+// Recomputes the forward from the saved row statistics; d_rows[t] = dL/dx (the gradient of the
+// gathered row AND of the position row), d_extra[t] = dL/dz; block partials of (dw1, db1, dw2, db2).
+template <class R>
 __global__ __launch_bounds__(256) void emb_bwd_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1, uint64_t s1,
     const float* __restrict__ extra, const float* __restrict__ w2, float p2, uint64_t s2,
     const float* __restrict__ dout, const float* __restrict__ stats, float* __restrict__ d_rows,
     float* __restrict__ d_extra, float* __restrict__ partials) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    float acc[4][VPL];
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR, wave = threadIdx.x >> 6;
+    float acc[4][R::NV][R::W];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) acc[k][j] = 0.f;
+    for (int k = 0; k < 4; ++k) row_zero<R>(acc[k]);
 
-    for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave; t < T; t += (int64_t)gridDim.x * kWavesPerBlock) {
-        int64_t id = ids[t];
-        if (id < 0 || id >= V) id = 0;
-        const float* row = table + id * D;
-        const float* prow = pos ? pos + (t % L) * D : nullptr;
-        const float m1 = stats[t * 4 + 0], r1 = stats[t * 4 + 1], m2 = stats[t * 4 + 2], r2 = stats[t * 4 + 3];
-        float xh1[VPL], f1[VPL], xh2[VPL], g[VPL];
+    for (int64_t t0 = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * R::RPW; t0 < T;
+         t0 += (int64_t)gridDim.x * kWavesPerBlock * R::RPW) {
+        const int64_t t = t0 + lane / R::LPR;
+        const bool live = t < T;
+        RowVals<R> x, xh1, f1, xh2, g, tmp;
+        float4 st = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (live) {
+            int64_t id = ids[t];
+            if (id < 0 || id >= V) id = 0;
+            st = *reinterpret_cast<const float4*>(stats + t * 4);
+            row_load<R>(table + id * D, sub, D, x);
+            if (pos) {
+                row_load<R>(pos + (t % L) * D, sub, D, tmp);
 #pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            const bool ok = e < D;
-            const float x0 = ok ? row[e] + (prow ? prow[e] : 0.f) : 0.f;
-            xh1[j] = ok ? (w1 ? (x0 - m1) * r1 : x0) : 0.f;
-            const float y1 = ok ? (w1 ? xh1[j] * w1[e] + b1[e] : x0) : 0.f;
-            f1[j] = p1 > 0.f ? dropout_factor(s1, 1u, (uint64_t)t * D + e, p1) : 1.f;
-            const float z = y1 * f1[j] + ((extra && ok) ? extra[t * D + e] : 0.f);
-            xh2[j] = ok ? (w2 ? (z - m2) * r2 : z) : 0.f;
-            const float f2 = p2 > 0.f ? dropout_factor(s2, 2u, (uint64_t)t * D + e, p2) : 1.f;
-            g[j] = ok ? dout[t * D + e] * f2 : 0.f;
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < R::W; ++i) x[j][i] += tmp[j][i];
+            }
+            row_load<R>(dout + t * D, sub, D, g);
+        } else {
+            row_zero<R>(x);
+            row_zero<R>(g);
         }
-        float gz[VPL];
+        // recompute z = drop1(LN1(x)) + extra
+        if (w1) {
+            row_normalise<R>(x, sub, D, st.x, st.y, xh1);
+            row_affine<R>(xh1, sub, D, w1, b1, x);
+        } else {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) xh1[j][i] = x[j][i];
+        }
+        if (p1 > 0.f) {
+            row_keep<R>(s1, 1u, (uint64_t)t * D, sub, p1, f1);
+            row_mul<R>(x, f1);
+        }
+        if (extra && live) {
+            row_load<R>(extra + t * D, sub, D, tmp);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) x[j][i] += tmp[j][i];
+        }
+        if (w2) row_normalise<R>(x, sub, D, st.z, st.w, xh2);
+        if (p2 > 0.f) {
+            row_keep<R>(s2, 2u, (uint64_t)t * D, sub, p2, tmp);
+            row_mul<R>(g, tmp);
+        }
+        RowVals<R> gz;
         if (w2) {
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) {
-                acc[2][j] += g[j] * xh2[j];
-                acc[3][j] += g[j];
-            }
-            ln_bwd_row<VPL>(g, xh2, w2, r2, lane, D, gz);
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) {
+                    acc[2][j][i] += g[j][i] * xh2[j][i];
+                    acc[3][j][i] += g[j][i];
+                }
+            row_ln_bwd<R>(g, xh2, w2, st.w, sub, D, gz);
         } else {
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) gz[j] = g[j];
-        }
-        if (d_extra) {
+            for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) {
-                const int e = lane + 64 * j;
-                if (e < D) d_extra[t * D + e] = gz[j];
-            }
+                for (int i = 0; i < R::W; ++i) gz[j][i] = g[j][i];
         }
-        float gy1[VPL], gx0[VPL];
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) gy1[j] = gz[j] * f1[j];
+        if (d_extra && live) row_store<R>(d_extra + t * D, sub, D, gz);
+        if (p1 > 0.f) row_mul<R>(gz, f1);  // gz is now d y1
         if (w1) {
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) {
-                acc[0][j] += gy1[j] * xh1[j];
-                acc[1][j] += gy1[j];
-            }
-            ln_bwd_row<VPL>(gy1, xh1, w1, r1, lane, D, gx0);
-        } else {
+            for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) gx0[j] = gy1[j];
-        }
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) d_rows[t * D + e] = gx0[j];
+                for (int i = 0; i < R::W; ++i) {
+                    acc[0][j][i] += gz[j][i] * xh1[j][i];
+                    acc[1][j][i] += gz[j][i];
+                }
+            row_ln_bwd<R>(gz, xh1, w1, st.y, sub, D, g);
+            if (live) row_store<R>(d_rows + t * D, sub, D, g);
+        } else if (live) {
+            row_store<R>(d_rows + t * D, sub, D, gz);
         }
     }
-    if (!partials) return;
-    // block-level reduction of the 4 LayerNorm parameter-gradient accumulators (deterministic order)
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][4][D]
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) red[(wave * 4 + k) * D + e] = acc[k][j];
-        }
-    __syncthreads();
-    for (int c = threadIdx.x; c < 4 * D; c += blockDim.x) {
-        float s = 0.f;
-        for (int w = 0; w < kWavesPerBlock; ++w) s += red[w * 4 * D + c];
-        partials[(int64_t)blockIdx.x * 4 * D + c] = s;
-    }
+    if (partials) write_row_partials<R, 4, kWavesPerBlock>(acc, lane, wave, D, partials);
 }
 
 template <int VPL>
@@ -336,11 +296,15 @@ ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t se
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && seq_len >= 1 && n_tokens >= 0, "asme_embedding_fwd: bad shape");
     ASME_CHECK_ARG(p1 >= 0.f && p1 < 1.f && p2 >= 0.f && p2 < 1.f, "asme_embedding_fwd: dropout p must be in [0,1)");
     if (n_tokens == 0) return 0;
-    const dim3 grid((unsigned)((n_tokens + kWavesPerBlock - 1) / kWavesPerBlock));
-    ASME_VPL_DISPATCH(vpl_of(dim),
-                      hipLaunchKernelGGL(emb_fwd_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, ids, n_tokens,
-                                         seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, ln1_eps, p1, seed1,
-                                         extra, ln2_w, ln2_b, ln2_eps, p2, seed2, out, stats, err_flag));
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
+            hipLaunchKernelGGL(emb_fwd_kernel<R>, dim3((unsigned)((n_tokens + rows - 1) / rows)), dim3(256), 0,
+                               (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w,
+                               ln1_b, ln1_eps, p1, seed1, extra, ln2_w, ln2_b, ln2_eps, p2, seed2, out, stats,
+                               err_flag);
+        }))
+        return -1;
     ASME_LAUNCH_CHECK("asme_embedding_fwd");
 }
 
@@ -355,13 +319,17 @@ ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t se
     ASME_CHECK_ARG(dim >= 1 && dim <= 512, "asme_embedding_bwd: bad shape");
     ASME_CHECK_ARG(!partials || n_partials >= 1, "asme_embedding_bwd: n_partials must be >= 1");
     if (n_tokens == 0) return 0;
-    int64_t nb = (n_tokens + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (partials) nb = n_partials;  // grid-stride; one partial row per block
     const size_t lds = partials ? (size_t)kWavesPerBlock * 4 * dim * sizeof(float) : 0;
-    ASME_VPL_DISPATCH(vpl_of(dim),
-                      hipLaunchKernelGGL(emb_bwd_kernel<VPL>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream,
-                                         ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1,
-                                         seed1, extra, ln2_w, p2, seed2, dout, stats, d_rows, d_extra, partials));
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
+            // grid-stride with one partial row per block when the LN parameter grads are wanted
+            const int64_t nb = partials ? n_partials : (n_tokens + rows - 1) / rows;
+            hipLaunchKernelGGL(emb_bwd_kernel<R>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, ids,
+                               n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1, seed1, extra,
+                               ln2_w, p2, seed2, dout, stats, d_rows, d_extra, partials);
+        }))
+        return -1;
     ASME_LAUNCH_CHECK("asme_embedding_bwd");
 }
 

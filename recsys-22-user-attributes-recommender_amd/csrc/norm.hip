@@ -11,207 +11,182 @@
 //     s   = dropout_b( res + dropout_a(y) )      (stream value, the residual for the next sublayer)
 //     out = LN(s)                                (input of the next sublayer; optional)
 // so a transformer block costs two of these plus the GEMMs and the attention kernel.
-#include "common.h"
+#include "rows.h"
 
 using namespace asme;
 
 namespace {
 constexpr int kWaves = 4;
 
-template <int VPL>
-__device__ __forceinline__ void row_ln(float (&x)[VPL], int lane, int D, float eps, const float* w, const float* b,
-                                       float (&y)[VPL], float& mean, float& rstd) {
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) s += (lane + 64 * j < D) ? x[j] : 0.f;
-    mean = wave_sum(s) / (float)D;
-    float q = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const float c = (lane + 64 * j < D) ? x[j] - mean : 0.f;
-        q += c * c;
-    }
-    rstd = rsqrtf(wave_sum(q) / (float)D + eps);
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        y[j] = e < D ? (x[j] - mean) * rstd * w[e] + b[e] : 0.f;
-    }
-}
-
-template <int VPL>
-__device__ __forceinline__ void row_ln_bwd(const float (&gy)[VPL], const float (&xhat)[VPL], const float* w,
-                                           float rstd, int lane, int D, float (&gx)[VPL]) {
-    float a = 0.f, b = 0.f, dxh[VPL];
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        dxh[j] = e < D ? gy[j] * w[e] : 0.f;
-        a += dxh[j];
-        b += dxh[j] * xhat[j];
-    }
-    a = wave_sum(a) / (float)D;
-    b = wave_sum(b) / (float)D;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) gx[j] = rstd * (dxh[j] - a - xhat[j] * b);
-}
-
-template <int VPL>
-__device__ __forceinline__ void write_partials(float (&acc)[2][VPL], int lane, int wave, int D, float* partials) {
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [kWaves][2][D]
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) red[(wave * 2 + k) * D + e] = acc[k][j];
-        }
-    __syncthreads();
-    for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) {
-        float s = 0.f;
-        for (int w = 0; w < kWaves; ++w) s += red[w * 2 * D + c];
-        partials[(int64_t)blockIdx.x * 2 * D + c] = s;
-    }
-}
-
 // ------------------------------------------------------------ plain LayerNorm
-template <int VPL>
+template <class R>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, int64_t T, int D,
                                                      const float* __restrict__ w, const float* __restrict__ b,
                                                      float eps, float* __restrict__ y, float* __restrict__ stats) {
-    const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-    if (t >= T) return;
-    float v[VPL], o[VPL], m, r;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        v[j] = e < D ? x[t * D + e] : 0.f;
-    }
-    row_ln<VPL>(v, lane, D, eps, w, b, o, m, r);
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        if (e < D) y[t * D + e] = o[j];
-    }
-    if (lane == 0) {
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR;
+    const int64_t t = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * R::RPW + lane / R::LPR;
+    if (t >= T) return;  // whole row groups leave together
+    RowVals<R> v, xh, o;
+    float m, r;
+    row_load<R>(x + t * D, sub, D, v);
+    row_ln_stats<R>(v, sub, D, eps, m, r);
+    row_normalise<R>(v, sub, D, m, r, xh);
+    row_affine<R>(xh, sub, D, w, b, o);
+    row_store<R>(y + t * D, sub, D, o);
+    if (sub == 0) {
         stats[t * 2] = m;
         stats[t * 2 + 1] = r;
     }
 }
 
-template <int VPL>
+template <class R>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, int64_t T, int D,
                                                      const float* __restrict__ w, const float* __restrict__ stats,
                                                      const float* __restrict__ dy, float* __restrict__ dx,
                                                      int accumulate, float* __restrict__ partials) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    float acc[2][VPL];
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) acc[0][j] = acc[1][j] = 0.f;
-    for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < T; t += (int64_t)gridDim.x * kWaves) {
-        const float m = stats[t * 2], r = stats[t * 2 + 1];
-        float xh[VPL], g[VPL], gx[VPL];
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            xh[j] = e < D ? (x[t * D + e] - m) * r : 0.f;
-            g[j] = e < D ? dy[t * D + e] : 0.f;
-            acc[0][j] += g[j] * xh[j];
-            acc[1][j] += g[j];
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR, wave = threadIdx.x >> 6;
+    float acc[2][R::NV][R::W];
+    row_zero<R>(acc[0]);
+    row_zero<R>(acc[1]);
+    for (int64_t t0 = ((int64_t)blockIdx.x * kWaves + wave) * R::RPW; t0 < T;
+         t0 += (int64_t)gridDim.x * kWaves * R::RPW) {
+        const int64_t t = t0 + lane / R::LPR;
+        const bool live = t < T;
+        RowVals<R> v, xh, g, gx;
+        const float m = live ? stats[t * 2] : 0.f, r = live ? stats[t * 2 + 1] : 0.f;
+        if (live) {
+            row_load<R>(x + t * D, sub, D, v);
+            row_load<R>(dy + t * D, sub, D, g);
+        } else {
+            row_zero<R>(v);
+            row_zero<R>(g);
         }
-        row_ln_bwd<VPL>(g, xh, w, r, lane, D, gx);
+        row_normalise<R>(v, sub, D, m, r, xh);
 #pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) dx[t * D + e] = accumulate ? dx[t * D + e] + gx[j] : gx[j];
+        for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+            for (int i = 0; i < R::W; ++i) {
+                acc[0][j][i] += g[j][i] * xh[j][i];
+                acc[1][j][i] += g[j][i];
+            }
+        row_ln_bwd<R>(g, xh, w, r, sub, D, gx);
+        if (!live) continue;
+        if (accumulate) {
+            RowVals<R> old;
+            row_load<R>(dx + t * D, sub, D, old);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) gx[j][i] += old[j][i];
         }
+        row_store<R>(dx + t * D, sub, D, gx);
     }
-    write_partials<VPL>(acc, lane, wave, D, partials);
+    write_row_partials<R, 2, kWaves>(acc, lane, wave, D, partials);
 }
 
 // ------------------------------------------------------------ residual + dropout(s) + LayerNorm
-template <int VPL>
+template <class R>
 __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(
     const float* __restrict__ res, const float* __restrict__ y, int64_t T, int D, float pa, uint64_t sa, float pb,
     uint64_t sb, const float* __restrict__ w, const float* __restrict__ b, float eps, float* __restrict__ s_out,
     float* __restrict__ ln_out, float* __restrict__ stats) {
-    const int lane = threadIdx.x & 63;
-    const int64_t t = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR;
+    const int64_t t = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * R::RPW + lane / R::LPR;
     if (t >= T) return;
-    float v[VPL];
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-        const int e = lane + 64 * j;
-        const uint64_t idx = (uint64_t)t * D + e;
-        float a = e < D ? y[t * D + e] : 0.f;
-        if (pa > 0.f) a *= dropout_factor(sa, 3u, idx, pa);
-        float h = (e < D ? res[t * D + e] : 0.f) + a;
-        if (pb > 0.f) h *= dropout_factor(sb, 4u, idx, pb);
-        v[j] = h;
-        if (e < D) s_out[t * D + e] = h;
+    RowVals<R> a, h, f;
+    row_load<R>(y + t * D, sub, D, a);
+    row_load<R>(res + t * D, sub, D, h);
+    if (pa > 0.f) {
+        row_keep<R>(sa, 3u, (uint64_t)t * D, sub, pa, f);
+        row_mul<R>(a, f);
     }
-    if (w) {
-        float o[VPL], m, r;
-        row_ln<VPL>(v, lane, D, eps, w, b, o, m, r);
 #pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e < D) ln_out[t * D + e] = o[j];
-        }
-        if (lane == 0) {
+    for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+        for (int i = 0; i < R::W; ++i) h[j][i] += a[j][i];
+    if (pb > 0.f) {
+        row_keep<R>(sb, 4u, (uint64_t)t * D, sub, pb, f);
+        row_mul<R>(h, f);
+    }
+    row_store<R>(s_out + t * D, sub, D, h);
+    if (w) {
+        float m, r;
+        row_ln_stats<R>(h, sub, D, eps, m, r);
+        row_normalise<R>(h, sub, D, m, r, a);
+        row_affine<R>(a, sub, D, w, b, f);
+        row_store<R>(ln_out + t * D, sub, D, f);
+        if (sub == 0) {
             stats[t * 2] = m;
             stats[t * 2 + 1] = r;
         }
     }
 }
 
-template <int VPL>
+template <class R>
 __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
     const float* __restrict__ s, int64_t T, int D, float pa, uint64_t sa, float pb, uint64_t sb,
     const float* __restrict__ w, const float* __restrict__ stats, const float* __restrict__ d_s,
     const float* __restrict__ d_ln, float* __restrict__ d_res, float* __restrict__ d_y,
     float* __restrict__ partials) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    float acc[2][VPL];
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) acc[0][j] = acc[1][j] = 0.f;
-    for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < T; t += (int64_t)gridDim.x * kWaves) {
-        float g[VPL];
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            g[j] = (d_s && e < D) ? d_s[t * D + e] : 0.f;
-        }
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR, wave = threadIdx.x >> 6;
+    float acc[2][R::NV][R::W];
+    row_zero<R>(acc[0]);
+    row_zero<R>(acc[1]);
+    for (int64_t t0 = ((int64_t)blockIdx.x * kWaves + wave) * R::RPW; t0 < T;
+         t0 += (int64_t)gridDim.x * kWaves * R::RPW) {
+        const int64_t t = t0 + lane / R::LPR;
+        const bool live = t < T;
+        RowVals<R> g;
+        if (live && d_s)
+            row_load<R>(d_s + t * D, sub, D, g);
+        else
+            row_zero<R>(g);
         if (w && d_ln) {
-            const float m = stats[t * 2], r = stats[t * 2 + 1];
-            float xh[VPL], gl[VPL], gx[VPL];
-#pragma unroll
-            for (int j = 0; j < VPL; ++j) {
-                const int e = lane + 64 * j;
-                xh[j] = e < D ? (s[t * D + e] - m) * r : 0.f;
-                gl[j] = e < D ? d_ln[t * D + e] : 0.f;
-                acc[0][j] += gl[j] * xh[j];
-                acc[1][j] += gl[j];
+            const float m = live ? stats[t * 2] : 0.f, r = live ? stats[t * 2 + 1] : 0.f;
+            RowVals<R> v, xh, gl, gx;
+            if (live) {
+                row_load<R>(s + t * D, sub, D, v);
+                row_load<R>(d_ln + t * D, sub, D, gl);
+            } else {
+                row_zero<R>(v);
+                row_zero<R>(gl);
             }
-            row_ln_bwd<VPL>(gl, xh, w, r, lane, D, gx);
+            row_normalise<R>(v, sub, D, m, r, xh);
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) g[j] += gx[j];
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) {
+                    acc[0][j][i] += gl[j][i] * xh[j][i];
+                    acc[1][j][i] += gl[j][i];
+                }
+            row_ln_bwd<R>(gl, xh, w, r, sub, D, gx);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) g[j][i] += gx[j][i];
         }
-#pragma unroll
-        for (int j = 0; j < VPL; ++j) {
-            const int e = lane + 64 * j;
-            if (e >= D) continue;
-            const uint64_t idx = (uint64_t)t * D + e;
-            float dh = g[j];
-            if (pb > 0.f) dh *= dropout_factor(sb, 4u, idx, pb);
-            d_res[t * D + e] = dh;
-            if (d_y) d_y[t * D + e] = pa > 0.f ? dh * dropout_factor(sa, 3u, idx, pa) : dh;
+        if (!live) continue;
+        RowVals<R> f;
+        if (pb > 0.f) {
+            row_keep<R>(sb, 4u, (uint64_t)t * D, sub, pb, f);
+            row_mul<R>(g, f);
+        }
+        row_store<R>(d_res + t * D, sub, D, g);
+        if (d_y) {
+            if (pa > 0.f) {
+                row_keep<R>(sa, 3u, (uint64_t)t * D, sub, pa, f);
+                row_mul<R>(g, f);
+            }
+            row_store<R>(d_y + t * D, sub, D, g);
         }
     }
-    if (partials) write_partials<VPL>(acc, lane, wave, D, partials);
+    if (partials) write_row_partials<R, 2, kWaves>(acc, lane, wave, D, partials);
+}
+
+template <class R>
+inline unsigned row_blocks(int64_t T) {
+    const int64_t rows = (int64_t)kWaves * R::RPW;
+    return (unsigned)((T + rows - 1) / rows);
 }
 
 // ------------------------------------------------------------ GELU(erf) + dropout, elementwise (float4)
@@ -266,29 +241,18 @@ __global__ __launch_bounds__(256) void gelu_dropout_bwd_kernel(const float* __re
     }
 }
 
-inline int vpl_of(int64_t D) { return (int)((D + 63) / 64); }
-
-#define ASME_VPL_DISPATCH(VPLV, ...)                              \
-    switch (VPLV) {                                               \
-        case 1: { constexpr int VPL = 1; __VA_ARGS__; } break;    \
-        case 2: { constexpr int VPL = 2; __VA_ARGS__; } break;    \
-        case 3: { constexpr int VPL = 3; __VA_ARGS__; } break;    \
-        case 4: { constexpr int VPL = 4; __VA_ARGS__; } break;    \
-        case 5: { constexpr int VPL = 5; __VA_ARGS__; } break;    \
-        case 6: { constexpr int VPL = 6; __VA_ARGS__; } break;    \
-        case 7: { constexpr int VPL = 7; __VA_ARGS__; } break;    \
-        case 8: { constexpr int VPL = 8; __VA_ARGS__; } break;    \
-        default: set_error("hidden size must be in [1, 512]"); return -1; \
-    }
 }  // namespace
 
 ASME_API int asme_layernorm_fwd(const float* x, int64_t n_rows, int64_t dim, const float* w, const float* b,
                                 float eps, float* y, float* stats, void* stream) {
     ASME_CHECK_ARG(x && w && b && y && stats, "asme_layernorm_fwd: null pointer");
     if (n_rows == 0) return 0;
-    const dim3 grid((unsigned)((n_rows + kWaves - 1) / kWaves));
-    ASME_VPL_DISPATCH(vpl_of(dim), hipLaunchKernelGGL(ln_fwd_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, x,
-                                                      n_rows, (int)dim, w, b, eps, y, stats));
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            hipLaunchKernelGGL(ln_fwd_kernel<R>, dim3(row_blocks<R>(n_rows)), dim3(256), 0, (hipStream_t)stream, x,
+                               n_rows, (int)dim, w, b, eps, y, stats);
+        }))
+        return -1;
     ASME_LAUNCH_CHECK("asme_layernorm_fwd");
 }
 
@@ -298,10 +262,12 @@ ASME_API int asme_layernorm_bwd(const float* x, int64_t n_rows, int64_t dim, con
     ASME_CHECK_ARG(x && w && stats && dy && dx && partials && n_partials >= 1, "asme_layernorm_bwd: bad argument");
     if (n_rows == 0) return 0;
     const size_t lds = (size_t)kWaves * 2 * dim * sizeof(float);
-    ASME_VPL_DISPATCH(vpl_of(dim),
-                      hipLaunchKernelGGL(ln_bwd_kernel<VPL>, dim3((unsigned)n_partials), dim3(256), lds,
-                                         (hipStream_t)stream, x, n_rows, (int)dim, w, stats, dy, dx, accumulate,
-                                         partials));
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            hipLaunchKernelGGL(ln_bwd_kernel<R>, dim3((unsigned)n_partials), dim3(256), lds, (hipStream_t)stream, x,
+                               n_rows, (int)dim, w, stats, dy, dx, accumulate, partials);
+        }))
+        return -1;
     ASME_LAUNCH_CHECK("asme_layernorm_bwd");
 }
 
@@ -312,11 +278,13 @@ ASME_API int asme_residual_ln_fwd(const float* res, const float* y, int64_t n_ro
     ASME_CHECK_ARG(!w || (b && ln_out && stats), "asme_residual_ln_fwd: LayerNorm outputs missing");
     ASME_CHECK_ARG(p_a >= 0.f && p_a < 1.f && p_b >= 0.f && p_b < 1.f, "asme_residual_ln_fwd: bad dropout p");
     if (n_rows == 0) return 0;
-    const dim3 grid((unsigned)((n_rows + kWaves - 1) / kWaves));
-    ASME_VPL_DISPATCH(vpl_of(dim),
-                      hipLaunchKernelGGL(residual_ln_fwd_kernel<VPL>, grid, dim3(256), 0, (hipStream_t)stream, res, y,
-                                         n_rows, (int)dim, p_a, seed_a, p_b, seed_b, w, b, eps, s_out, ln_out,
-                                         stats));
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            hipLaunchKernelGGL(residual_ln_fwd_kernel<R>, dim3(row_blocks<R>(n_rows)), dim3(256), 0,
+                               (hipStream_t)stream, res, y, n_rows, (int)dim, p_a, seed_a, p_b, seed_b, w, b, eps,
+                               s_out, ln_out, stats);
+        }))
+        return -1;
     ASME_LAUNCH_CHECK("asme_residual_ln_fwd");
 }
 
@@ -329,12 +297,15 @@ ASME_API int asme_residual_ln_bwd(const float* s, int64_t n_rows, int64_t dim, f
                    "asme_residual_ln_bwd: LayerNorm inputs missing");
     if (n_rows == 0) return 0;
     const bool ln = w && d_ln;
-    const int64_t nb = ln ? n_partials : (n_rows + kWaves - 1) / kWaves;
     const size_t lds = ln ? (size_t)kWaves * 2 * dim * sizeof(float) : 0;
-    ASME_VPL_DISPATCH(vpl_of(dim),
-                      hipLaunchKernelGGL(residual_ln_bwd_kernel<VPL>, dim3((unsigned)nb), dim3(256), lds,
-                                         (hipStream_t)stream, s, n_rows, (int)dim, p_a, seed_a, p_b, seed_b, w, stats,
-                                         d_s, ln ? d_ln : nullptr, d_res, d_y, ln ? partials : nullptr));
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            const unsigned nb = ln ? (unsigned)n_partials : row_blocks<R>(n_rows);
+            hipLaunchKernelGGL(residual_ln_bwd_kernel<R>, dim3(nb), dim3(256), lds, (hipStream_t)stream, s, n_rows,
+                               (int)dim, p_a, seed_a, p_b, seed_b, w, stats, d_s, ln ? d_ln : nullptr, d_res, d_y,
+                               ln ? partials : nullptr);
+        }))
+        return -1;
     ASME_LAUNCH_CHECK("asme_residual_ln_bwd");
 }
 

@@ -458,15 +458,17 @@ class _AttentionFn(torch.autograd.Function):
         seed = new_seed(p_drop)
         scale = 1.0 / math.sqrt(dk)
         base = qkv.data_ptr()
+        mask = torch.empty(B * heads * L * ((L + 3) // 4), device=qkv.device, dtype=torch.uint8) if p_drop > 0 \
+            else None
         call("asme_attention_fwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(key_valid), B,
-             heads, L, dk, int(causal), scale, p_drop, seed, ptr(out), Dm, ptr(lse), stream())
-        ctx.save_for_backward(qkv, key_valid, out, lse)
+             heads, L, dk, int(causal), scale, p_drop, seed, ptr(out), Dm, ptr(lse), ptr(mask), stream())
+        ctx.save_for_backward(qkv, key_valid, out, lse, mask)
         ctx.meta = (heads, causal, p_drop, seed, scale)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, key_valid, out, lse = ctx.saved_tensors
+        qkv, key_valid, out, lse, mask = ctx.saved_tensors
         heads, causal, p_drop, seed, scale = ctx.meta
         B, L, three_d = qkv.shape
         Dm = three_d // 3
@@ -476,8 +478,8 @@ class _AttentionFn(torch.autograd.Function):
         dsum = torch.empty(B * heads * L, device=qkv.device, dtype=torch.float32)
         base, gb = qkv.data_ptr(), dqkv.data_ptr()
         call("asme_attention_bwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(out), Dm,
-             ptr(dout), Dm, ptr(lse), ptr(key_valid), B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(dsum),
-             gb, three_d, gb + 4 * Dm, three_d, gb + 8 * Dm, three_d, stream())
+             ptr(dout), Dm, ptr(lse), ptr(key_valid), B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(mask),
+             ptr(dsum), gb, three_d, gb + 4 * Dm, three_d, gb + 8 * Dm, three_d, stream())
         return dqkv, None, None, None, None
 
 

@@ -33,7 +33,7 @@ def test_argument_validation_is_loud(asme):
     assert rc == -1
     assert b"null pointer" in lib.asme_mi_last_error()
     with pytest.raises(asme._lib.ASMEKernelError):
-        asme._lib.call("asme_attention_fwd", 8, 8, 8, 0, 0, 0, None, 1, 1, 2000, 64, 1, 1.0, 0.0, 0, 8, 0, 8, None)
+        asme._lib.call("asme_attention_fwd", 8, 8, 8, 0, 0, 0, None, 1, 1, 2000, 64, 1, 1.0, 0.0, 0, 8, 0, 8, None, None)
 
 
 def test_dedup_workspace_query_is_host_only(asme):

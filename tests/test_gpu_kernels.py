@@ -65,6 +65,35 @@ def test_attention_dropout_deterministic(asme, dev):
     assert not torch.allclose(a, c)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_dropout_mask_matches_regeneration(asme, dev, causal):
+    """The backward reading the forward's stored keep-nibbles equals the backward regenerating them."""
+    torch.manual_seed(1)
+    B, L, H, dk = 3, 67, 2, 64
+    D = H * dk
+    qkv = torch.randn(B, L, 3 * D, device=dev)
+    valid = (torch.arange(L).unsqueeze(0) < torch.tensor([L, 30, 0]).unsqueeze(1)).to(torch.uint8).to(dev)
+    dout = torch.randn(B, L, D, device=dev)
+    out = torch.empty(B, L, D, device=dev)
+    stats = torch.empty(B * H, L, 2, device=dev)
+    mask = torch.empty(B * H * L * ((L + 3) // 4), device=dev, dtype=torch.uint8)
+    call, ptr, st = asme._lib.call, asme._lib.ptr, asme._lib.stream
+    b, scale, seed = qkv.data_ptr(), dk ** -0.5, 1234567
+    call("asme_attention_fwd", b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(valid), B, H, L, dk, int(causal),
+         scale, 0.25, seed, ptr(out), D, ptr(stats), ptr(mask), st())
+    grads = []
+    for m in (mask, None):
+        g = torch.zeros_like(qkv)
+        dsum = torch.empty(B * H * L, device=dev)
+        gb = g.data_ptr()
+        call("asme_attention_bwd", b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(out), D, ptr(dout), D,
+             ptr(stats), ptr(valid), B, H, L, dk, int(causal), scale, 0.25, seed, ptr(m), ptr(dsum), gb, 3 * D,
+             gb + 4 * D, 3 * D, gb + 8 * D, 3 * D, st())
+        grads.append(g)
+    torch.cuda.synchronize()
+    assert torch.equal(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("D", [16, 32, 64, 128, 200])
 def test_embedding_fused_double_ln(asme, dev, D):
     """SASRec embedding: LN2(LN1(E[ids] + P) + extra) and its gradients."""
