@@ -95,9 +95,9 @@ int asme_gelu_dropout_bwd(const float* x, const float* dy, int64_t n, float p, u
  * Masked scores are exactly -1e9 (reference masked_fill); out (n_tokens, heads*head_dim) with
  * stride ld_out; lse (batch*heads, seq_len, 2) = (row max, 1/row sum of exp) of the scaled, masked
  * scores (kept separate so a row with no admissible key keeps its exact 1/L weights).
- * head_dim in {16, 32, 64, 128}; seq_len <= 1024.  drop_mask (nullable; (batch*heads*seq_len) x
- * ceil(seq_len/4) bytes): the forward records the dropout decisions (a nibble per query row and 4
- * keys) which the backward then reads instead of regenerating them. */
+ * head_dim in {16, 32, 64, 128}; seq_len <= 1024.  drop_mask (nullable; asme_attention_dropout_mask_bytes()
+ * bytes): the forward records the dropout decisions (query-major nibbles + key-major 16-bit words) which
+ * the backward then reads instead of regenerating them. */
 int asme_attention_fwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k, int64_t ld_v,
                        const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
                        int causal, float scale, float p_drop, uint64_t seed, float* out, int64_t ld_out, float* lse,
@@ -108,6 +108,12 @@ int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t l
                        const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
                        int causal, float scale, float p_drop, uint64_t seed, const uint8_t* drop_mask, float* dsum_ws,
                        float* dq, int64_t ld_dq, float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream);
+/* Attention kernel selection: 0 = automatic (one workgroup per (batch, head) with the head's operands
+ * resident in LDS whenever 2*ceil(L/16)*16*(dk+4)*4 B fits 160 KiB, else the 64-row streaming kernels),
+ * 1 = streaming kernels only.  Returns the previous mode.  Process-wide; for tests and A/B timing. */
+int asme_attention_set_mode(int mode);
+/* Size of the drop_mask buffer for asme_attention_fwd/bwd (p_drop > 0). */
+int64_t asme_attention_dropout_mask_bytes(int64_t batch, int64_t heads, int64_t seq_len);
 
 /* ---- Linear weight/bias gradient (autograd of nn.Linear in transformer_layers.py:175-220):
  * dW (out x in) (+)= dY^T X, db (out) (+)= sum_t dY, split over the token dimension into fp32 partial

@@ -25,6 +25,7 @@
 // ds_read_b32 (LDS row stride dk+4: both patterns bank-conflict free for the 32-lane halves).
 // Every 16-key sub-tile of a 64-key tile has its own accumulator, so consecutive MFMAs are independent.
 #include "common.h"
+#include <type_traits>
 
 using namespace asme;
 
@@ -43,13 +44,23 @@ __device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Attention dropout decisions.  One Philox4x32-10 block serves 8 (query row, key) pairs: the block of
+// (row, key/32, (key/4)%4) yields 8 16-bit uniforms, word r / half h deciding key 32*(key/32) + 16*h +
+// 4*((key/4)%4) + r, so a lane holding keys 4g..4g+3 of two adjacent 16-key sub-tiles needs one block.
+// Key kept iff uniform16 >= round(p * 65536) (keep probability within 2^-16 of 1-p), scaled by 1/(1-p).
+__device__ __forceinline__ u32x4 attn_philox(uint64_t seed, uint64_t row, int key) {
+    u32x4 c{(uint32_t)(((key >> 5) << 2) | ((key >> 2) & 3)), (uint32_t)row, (uint32_t)(row >> 32), 0x61747466u};
+    return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+__device__ __forceinline__ uint32_t drop_threshold(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+__device__ __forceinline__ float4 keep_from(const u32x4& r, int half, uint32_t thr, float k) {
+    const int sh = half ? 16 : 0;
+    return make_float4(((r.x >> sh) & 0xFFFFu) >= thr ? k : 0.f, ((r.y >> sh) & 0xFFFFu) >= thr ? k : 0.f,
+                       ((r.z >> sh) & 0xFFFFu) >= thr ? k : 0.f, ((r.w >> sh) & 0xFFFFu) >= thr ? k : 0.f);
+}
 // keep factors (0 or 1/(1-p)) for the 4 keys key4 .. key4+3 (key4 % 4 == 0) of query row `row`
 __device__ __forceinline__ float4 attn_keep4(uint64_t seed, uint64_t row, int key4, float p) {
-    u32x4 c{(uint32_t)(key4 >> 2), (uint32_t)row, (uint32_t)(row >> 32), 0x61747466u};
-    u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const float s = 5.9604644775390625e-08f, k = 1.f / (1.f - p);
-    return make_float4((float)(r.x >> 8) * s >= p ? k : 0.f, (float)(r.y >> 8) * s >= p ? k : 0.f,
-                       (float)(r.z >> 8) * s >= p ? k : 0.f, (float)(r.w >> 8) * s >= p ? k : 0.f);
+    return keep_from(attn_philox(seed, row, key4), (key4 >> 4) & 1, drop_threshold(p), 1.f / (1.f - p));
 }
 __device__ __forceinline__ float pick(const float4& v, int i) {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
@@ -63,6 +74,31 @@ __device__ __forceinline__ uint8_t keep_bits(const float4& f) {
 __device__ __forceinline__ float4 bits_keep(uint8_t m, float p) {
     const float k = 1.f / (1.f - p);
     return make_float4(m & 1 ? k : 0.f, m & 2 ? k : 0.f, m & 4 ? k : 0.f, m & 8 ? k : 0.f);
+}
+// A second, key-major copy serves the dK/dV pass, whose lanes own keys: u16 word (key row, 16-query
+// group j) of (B*H*L) x ceil(L/16), bit i = query 16j+i kept.  It follows the nibble image, 256-B aligned.
+__host__ __device__ inline int64_t mask_nibble_bytes(int64_t bh, int L) { return bh * L * ((L + 3) / 4); }
+__host__ __device__ inline int64_t mask_total_bytes(int64_t bh, int L) {
+    return ((mask_nibble_bytes(bh, L) + 255) & ~(int64_t)255) + bh * L * ((L + 15) / 16) * 2;
+}
+__device__ __forceinline__ uint16_t* mask_keys(uint8_t* m, int64_t bh_total, int L) {
+    return reinterpret_cast<uint16_t*>(m + ((mask_nibble_bytes(bh_total, L) + 255) & ~(int64_t)255));
+}
+// Forward-side store of one 16-key sub-tile's decisions (lane: query row c16 of group q0/16, keys
+// key4..key4+3 with key4 = ks + 4g): the nibble for the dQ pass, and via ballots the key-major words.
+__device__ __forceinline__ void store_drop_bits(uint8_t* __restrict__ nib, uint16_t* __restrict__ keyw, int bh,
+                                                int L, int qi, int q0, int ks, int g, int c16, const float4& f) {
+    const int L4 = (L + 3) / 4, Lg = (L + 15) / 16;
+    const int key4 = ks + 4 * g;
+    if (qi < L && key4 < L) nib[((int64_t)bh * L + qi) * L4 + key4 / 4] = keep_bits(f);
+    const float fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint64_t bal = __ballot(fv[r] != 0.f);  // bit 16g + c16: (key ks+4g+r, query q0+c16)
+        const int key = key4 + r;
+        if (c16 == 0 && key < L)
+            keyw[((int64_t)bh * L + key) * Lg + q0 / 16] = (uint16_t)(bal >> (16 * g));
+    }
 }
 
 // Stage the key-validity row of batch b in LDS; returns whether any key is valid and the last one.
@@ -119,34 +155,34 @@ __device__ __forceinline__ void load_row_slice(const float* __restrict__ rowp, b
 }
 
 // acc[sub] += Tile[sub*16 + c16][slice g] . f  (16 x 16 result per sub-tile, rows of the tile on C/D rows)
-template <int DK>
+template <int DK, int NS = kNS>
 __device__ __forceinline__ void rows_times_slice(const float* __restrict__ tile, int g, int c16,
-                                                 const float (&f)[DK / 4], floatx4 (&acc)[kNS]) {
+                                                 const float (&f)[DK / 4], floatx4 (&acc)[NS]) {
     constexpr int S = DK + 4, DQ = DK / 4;
 #pragma unroll
     for (int s4 = 0; s4 < DQ / 4; ++s4) {
-        float4 a[kNS];
+        float4 a[NS];
 #pragma unroll
-        for (int sub = 0; sub < kNS; ++sub)
+        for (int sub = 0; sub < NS; ++sub)
             a[sub] = *reinterpret_cast<const float4*>(tile + (sub * 16 + c16) * S + g * DQ + 4 * s4);
 #pragma unroll
-        for (int sub = 0; sub < kNS; ++sub) acc[sub] = mfma16(a[sub].x, f[4 * s4], acc[sub]);
+        for (int sub = 0; sub < NS; ++sub) acc[sub] = mfma16(a[sub].x, f[4 * s4], acc[sub]);
 #pragma unroll
-        for (int sub = 0; sub < kNS; ++sub) acc[sub] = mfma16(a[sub].y, f[4 * s4 + 1], acc[sub]);
+        for (int sub = 0; sub < NS; ++sub) acc[sub] = mfma16(a[sub].y, f[4 * s4 + 1], acc[sub]);
 #pragma unroll
-        for (int sub = 0; sub < kNS; ++sub) acc[sub] = mfma16(a[sub].z, f[4 * s4 + 2], acc[sub]);
+        for (int sub = 0; sub < NS; ++sub) acc[sub] = mfma16(a[sub].z, f[4 * s4 + 2], acc[sub]);
 #pragma unroll
-        for (int sub = 0; sub < kNS; ++sub) acc[sub] = mfma16(a[sub].w, f[4 * s4 + 3], acc[sub]);
+        for (int sub = 0; sub < NS; ++sub) acc[sub] = mfma16(a[sub].w, f[4 * s4 + 3], acc[sub]);
     }
 }
 
 // out[ct] += Tile^T[ct-th 16 columns][rows] . w  where w[sub][s] is the weight of tile row sub*16 + 4g + s
-template <int DK>
+template <int DK, int NS = kNS>
 __device__ __forceinline__ void cols_times_weights(const float* __restrict__ tile, int g, int c16,
-                                                   const float (&w)[kNS][4], floatx4 (&out)[DK / 16]) {
+                                                   const float (&w)[NS][4], floatx4 (&out)[DK / 16]) {
     constexpr int S = DK + 4, NCT = DK / 16;
 #pragma unroll
-    for (int sub = 0; sub < kNS; ++sub)
+    for (int sub = 0; sub < NS; ++sub)
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -193,7 +229,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
     for (int ct = 0; ct < NCT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     float m = kInitMax, l = 0.f;
     const uint64_t drow = (uint64_t)bh * L + (uint64_t)min(qi, L - 1);
-    const int L4 = (L + 3) / 4;
     // wave-uniform work limits: waves whose 16 queries are all past L only help stage tiles; under a
     // causal mask (and some admissible key) a 16-key sub-tile that starts after the wave's last query
     // is fully masked and contributes exactly 0, so it is skipped.
@@ -257,11 +292,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) acc[ct] *= alpha;
         if (p_drop > 0.f) {
+            const uint32_t thr = drop_threshold(p_drop);
+            const float kf = 1.f / (1.f - p_drop);
+            uint16_t* keyw = drop_mask ? mask_keys(drop_mask, (int64_t)gridDim.y, L) : nullptr;
+            u32x4 rnd;
 #pragma unroll
             for (int sub = 0; sub < kNS; ++sub) {
                 const int key4 = k0 + sub * 16 + 4 * g;
-                const float4 f = attn_keep4(seed, drow, key4, p_drop);
-                if (drop_mask && qi < L && key4 < L) drop_mask[drow * L4 + key4 / 4] = keep_bits(f);
+                if ((sub & 1) == 0) rnd = attn_philox(seed, drow, key4);  // k0 % 64 == 0: pairs share a block
+                const float4 f = keep_from(rnd, sub & 1, thr, kf);
+                if (drop_mask) store_drop_bits(drop_mask, keyw, bh, L, qi, wq0, k0 + sub * 16, g, c16, f);
                 p[sub][0] *= f.x;
                 p[sub][1] *= f.y;
                 p[sub][2] *= f.z;
@@ -430,8 +470,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) dvt[ct] = dkt[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    const int L4 = (L + 3) / 4;
     const int wk0 = kblk + wave * 16;
+    const uint16_t* keyw_row = drop_mask ? mask_keys(const_cast<uint8_t*>(drop_mask), (int64_t)gridDim.y, L) +
+                                               ((int64_t)bh * L + min(kj, L - 1)) * ((L + 15) / 16)
+                                         : nullptr;
     const bool wave_live = wk0 < L;
     // causal: queries before this key block see none of its keys (unless no key is valid at all)
     const int q_start = (causal && any_valid) ? kblk : 0;
@@ -479,9 +521,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
                     const float pr = __expf(sv_ - mx_s[ql]) * il_s[ql];
                     float f = 1.f;
                     if (p_drop > 0.f) {
-                        const uint64_t row = (uint64_t)bh * L + qq;
-                        f = drop_mask ? ((drop_mask[row * L4 + kj / 4] >> (kj & 3)) & 1 ? 1.f / (1.f - p_drop) : 0.f)
-                                      : pick(attn_keep4(seed, row, kj & ~3, p_drop), kj & 3);
+                        f = drop_mask ? ((keyw_row[qq >> 4] >> (qq & 15)) & 1 ? 1.f / (1.f - p_drop) : 0.f)
+                                      : pick(attn_keep4(seed, (uint64_t)bh * L + qq, kj & ~3, p_drop), kj & 3);
                     }
                     pv = pr * f;
                     dsv = masked ? 0.f : pr * (dpt[sub][r] * f - dsum_s[ql]);
@@ -503,6 +544,412 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
                 make_float4(dvt[ct][0], dvt[ct][1], dvt[ct][2], dvt[ct][3]);
         }
     }
+}
+
+// ==================================================================================================
+// Resident variants: one 8-wave workgroup per (batch, head) keeps the whole streamed operand pair of
+// that head in LDS (K,V for the forward / dQ pass; Q,dO plus the per-query statistics for dK/dV) and
+// the waves claim 16-row groups from an LDS counter, most expensive first under a causal mask.  No
+// per-tile barriers, each K/V row is read from HBM once per head (not once per 64-query block), and
+// fully-masked 16-key sub-tiles are skipped.  Used when 2 * ceil(L/16)*16 * (dk+4) * 4 B fits the
+// 160 KiB LDS (L <= 300 at dk = 64); the streaming kernels above cover the rest.
+constexpr int kResThreads = 512;
+
+__host__ __device__ inline int res_rows(int L) { return (L + 15) & ~15; }
+inline size_t res_lds_bytes(int L, int DK, bool with_stats) {
+    const size_t Lp = (size_t)res_rows(L);
+    return 2 * Lp * (DK + 4) * sizeof(float) + (with_stats ? 3 * Lp * sizeof(float) : 0) + (Lp + 31) / 32 * 4 + 16;
+}
+
+// rows [0, Lp) of two (L x DK) operands into padded LDS images (rows >= L zeroed); 8 float4 in flight
+template <int DK>
+__device__ __forceinline__ void load_pair_resident(const float* __restrict__ a, int64_t lda,
+                                                   const float* __restrict__ b, int64_t ldb, int L, int Lp,
+                                                   float* __restrict__ As, float* __restrict__ Bs) {
+    constexpr int C4 = DK / 4, S = DK + 4;
+    const int n4 = Lp * C4;
+    for (int base = threadIdx.x; base < n4; base += kResThreads * 4) {
+        float4 ra[4], rb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = base + u * kResThreads, row = idx / C4, c = (idx % C4) * 4;
+            const bool ok = idx < n4 && row < L;
+            ra[u] = ok ? *reinterpret_cast<const float4*>(a + (int64_t)row * lda + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[u] = ok ? *reinterpret_cast<const float4*>(b + (int64_t)row * ldb + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = base + u * kResThreads, row = idx / C4, c = (idx % C4) * 4;
+            if (idx < n4) {
+                *reinterpret_cast<float4*>(As + row * S + c) = ra[u];
+                *reinterpret_cast<float4*>(Bs + row * S + c) = rb[u];
+            }
+        }
+    }
+}
+
+// key-validity bits (kvw: bit i of word i/32) + (last valid key, work counter) control words
+__device__ __forceinline__ void stage_valid_res(const uint8_t* __restrict__ key_valid, int b, int L, int Lp,
+                                                uint32_t* kvw, int* ctl) {
+    if (threadIdx.x == 0) {
+        ctl[0] = -1;
+        ctl[1] = 0;
+    }
+    for (int w = threadIdx.x; w < (Lp + 31) / 32; w += blockDim.x) kvw[w] = 0u;
+    __syncthreads();
+    for (int i = threadIdx.x; i < L; i += blockDim.x) {
+        const bool v = key_valid ? key_valid[(int64_t)b * L + i] != 0 : true;
+        if (v) {
+            atomicOr(kvw + (i >> 5), 1u << (i & 31));
+            atomicMax(ctl, i);
+        }
+    }
+}
+// this lane's 4 validity bits for keys ks + 4g .. +3 (ks % 16 == 0)
+__device__ __forceinline__ uint32_t valid_bits4(const uint32_t* kvw, int ks, int g) {
+    return (kvw[ks >> 5] >> ((ks & 16) + 4 * g)) & 0xFu;
+}
+
+__device__ __forceinline__ int claim_group(int* ctl, int lane) {
+    int gi = 0;
+    if (lane == 0) gi = atomicAdd(ctl + 1, 1);
+    return __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
+}
+
+template <int DK>
+__global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
+    int64_t ldv, float* __restrict__ o, int64_t ldo, float* __restrict__ stats, const uint8_t* __restrict__ key_valid,
+    int H, int L, int causal, float scale, float p_drop, uint64_t seed, uint8_t* __restrict__ drop_mask) {
+    constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int Lp = res_rows(L);
+    float* Ks = lds;
+    float* Vs = Ks + Lp * S;
+    uint32_t* kvw = reinterpret_cast<uint32_t*>(Vs + Lp * S);
+    int* ctl = reinterpret_cast<int*>(kvw + (Lp + 31) / 32);
+
+    const int bh = blockIdx.x, b = bh / H, h = bh % H;
+    const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+    const int64_t tok0 = (int64_t)b * L;
+    const float* qh = q + tok0 * ldq + h * DK;
+
+    stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
+    load_pair_resident<DK>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks, Vs);
+    __syncthreads();
+    const int last_valid = ctl[0];
+    const bool any_valid = last_valid >= 0;
+    const int kend = any_valid ? last_valid + 1 : L;
+    const int ngroups = Lp / 16;
+    uint16_t* keyw = drop_mask ? mask_keys(drop_mask, (int64_t)gridDim.x, L) : nullptr;
+
+    for (;;) {
+        const int gi = claim_group(ctl, lane);
+        if (gi >= ngroups) break;
+        const int q0 = (causal ? ngroups - 1 - gi : gi) * 16;
+        const int qi = q0 + c16;
+        // keys past kmax are masked for all 16 queries (and some key is admissible): exact zeros
+        const int kmax = (causal && any_valid) ? min(kend, q0 + 16) : kend;
+        const int nsub = (kmax + 15) / 16;
+        float qf[DQ];
+        load_row_slice<DK>(qh + (int64_t)qi * ldq, qi < L, g, qf);
+        floatx4 acc[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+        float m = kInitMax, l = 0.f;
+        const uint64_t drow = (uint64_t)bh * L + (uint64_t)min(qi, L - 1);
+        // a chunk of NS 16-key sub-tiles starting at key k0 (online softmax across chunks)
+        auto chunk = [&](auto ns_tag, int k0) {
+            constexpr int NS = decltype(ns_tag)::value;
+            floatx4 st[NS];
+#pragma unroll
+            for (int sub = 0; sub < NS; ++sub) st[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
+            rows_times_slice<DK, NS>(Ks + k0 * S, g, c16, qf, st);
+            float p[NS][4];
+            float tmax = kInitMax;
+#pragma unroll
+            for (int sub = 0; sub < NS; ++sub) {
+                const uint32_t vb = valid_bits4(kvw, k0 + sub * 16, g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = k0 + sub * 16 + 4 * g + r;
+                    float sv_ = -INFINITY;  // not a key: contributes nothing
+                    if (key < L) {
+                        const bool masked = !((vb >> r) & 1u) || (causal && key > qi);
+                        sv_ = masked ? kMaskedScore : st[sub][r] * scale;
+                    }
+                    p[sub][r] = sv_;
+                    tmax = fmaxf(tmax, sv_);
+                }
+            }
+            tmax = group4_max(tmax);
+            const float mnew = fmaxf(m, tmax);
+            const float alpha = __expf(m - mnew);
+            float rs = 0.f;
+#pragma unroll
+            for (int sub = 0; sub < NS; ++sub)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    p[sub][r] = __expf(p[sub][r] - mnew);
+                    rs += p[sub][r];
+                }
+            rs = group4_sum(rs);
+            l = l * alpha + rs;
+            m = mnew;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct) acc[ct] *= alpha;
+            if (p_drop > 0.f) {
+                const uint32_t thr = drop_threshold(p_drop);
+                const float kf = 1.f / (1.f - p_drop);
+                u32x4 rnd;
+#pragma unroll
+                for (int sub = 0; sub < NS; ++sub) {
+                    const int key4 = k0 + sub * 16 + 4 * g;
+                    // NS == 4 chunks start at multiples of 64 keys, so sub-tile pairs share a block
+                    if (NS == 1 || (sub & 1) == 0) rnd = attn_philox(seed, drow, key4);
+                    const float4 f = keep_from(rnd, (key4 >> 4) & 1, thr, kf);
+                    if (drop_mask) store_drop_bits(drop_mask, keyw, bh, L, qi, q0, k0 + sub * 16, g, c16, f);
+                    p[sub][0] *= f.x;
+                    p[sub][1] *= f.y;
+                    p[sub][2] *= f.z;
+                    p[sub][3] *= f.w;
+                }
+            }
+            cols_times_weights<DK, NS>(Vs + k0 * S, g, c16, p, acc);
+        };
+        // keys >= nsub*16 are beyond kmax: no sub-tile past it is computed
+        int c0 = 0;
+        for (; c0 + kNS <= nsub; c0 += kNS) chunk(std::integral_constant<int, kNS>{}, c0 * 16);
+        for (; c0 < nsub; ++c0) chunk(std::integral_constant<int, 1>{}, c0 * 16);
+        if (qi < L) {
+            const float inv = 1.f / l;
+            float* orow = o + (tok0 + qi) * ldo + h * DK;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+                *reinterpret_cast<float4*>(orow + ct * 16 + 4 * g) =
+                    make_float4(acc[ct][0] * inv, acc[ct][1] * inv, acc[ct][2] * inv, acc[ct][3] * inv);
+            if (g == 0) {
+                stats[((int64_t)bh * L + qi) * 2] = m;
+                stats[((int64_t)bh * L + qi) * 2 + 1] = inv;
+            }
+        }
+    }
+}
+
+template <int DK>
+__global__ __launch_bounds__(kResThreads) void attn_bwd_dq_res_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
+    int64_t ldv, const float* __restrict__ o, int64_t ldo, const float* __restrict__ dout, int64_t lddo,
+    const float* __restrict__ stats, float* __restrict__ dsum, float* __restrict__ dq, int64_t lddq,
+    const uint8_t* __restrict__ key_valid, int H, int L, int causal, float scale, float p_drop, uint64_t seed,
+    const uint8_t* __restrict__ drop_mask) {
+    constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int Lp = res_rows(L);
+    float* Ks = lds;
+    float* Vs = Ks + Lp * S;
+    uint32_t* kvw = reinterpret_cast<uint32_t*>(Vs + Lp * S);
+    int* ctl = reinterpret_cast<int*>(kvw + (Lp + 31) / 32);
+
+    const int bh = blockIdx.x, b = bh / H, h = bh % H;
+    const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+    const int64_t tok0 = (int64_t)b * L;
+
+    stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
+    load_pair_resident<DK>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks, Vs);
+    __syncthreads();
+    const int last_valid = ctl[0];
+    const bool any_valid = last_valid >= 0;
+    const int kend = any_valid ? last_valid + 1 : L;
+    const int ngroups = Lp / 16;
+    const int L4 = (L + 3) / 4;
+
+    for (;;) {
+        const int gi = claim_group(ctl, lane);
+        if (gi >= ngroups) break;
+        const int q0 = (causal ? ngroups - 1 - gi : gi) * 16;
+        const int qi = q0 + c16;
+        const bool qok = qi < L;
+        const int kmax = (causal && any_valid) ? min(kend, q0 + 16) : kend;
+        const int nsub = (kmax + 15) / 16;
+        float qf[DQ], df[DQ], of[DQ];
+        load_row_slice<DK>(q + (tok0 + qi) * ldq + h * DK, qok, g, qf);
+        load_row_slice<DK>(dout + (tok0 + qi) * lddo + h * DK, qok, g, df);
+        load_row_slice<DK>(o + (tok0 + qi) * ldo + h * DK, qok, g, of);
+        float dsv = 0.f;
+#pragma unroll
+        for (int s = 0; s < DQ; ++s) dsv += df[s] * of[s];
+        dsv = group4_sum(dsv);
+        if (qok && g == 0) dsum[(int64_t)bh * L + qi] = dsv;
+        const float mq = qok ? stats[((int64_t)bh * L + qi) * 2] : 0.f;
+        const float iq = qok ? stats[((int64_t)bh * L + qi) * 2 + 1] : 0.f;
+        const uint64_t drow = (uint64_t)bh * L + (uint64_t)min(qi, L - 1);
+        floatx4 acc[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+        auto chunk = [&](auto ns_tag, int k0) {
+            constexpr int NS = decltype(ns_tag)::value;
+            floatx4 st[NS], dpt[NS];
+#pragma unroll
+            for (int sub = 0; sub < NS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
+            rows_times_slice<DK, NS>(Ks + k0 * S, g, c16, qf, st);
+            rows_times_slice<DK, NS>(Vs + k0 * S, g, c16, df, dpt);
+            float ds[NS][4];
+#pragma unroll
+            for (int sub = 0; sub < NS; ++sub) {
+                float4 f = make_float4(1.f, 1.f, 1.f, 1.f);
+                const int key4 = k0 + sub * 16 + 4 * g;
+                if (p_drop > 0.f)
+                    f = drop_mask ? bits_keep(key4 < L ? drop_mask[drow * L4 + key4 / 4] : (uint8_t)0, p_drop)
+                                  : attn_keep4(seed, drow, key4, p_drop);
+                const uint32_t vb = valid_bits4(kvw, k0 + sub * 16, g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = key4 + r;
+                    float val = 0.f;
+                    if (key < L && qok) {
+                        const bool masked = !((vb >> r) & 1u) || (causal && key > qi);
+                        const float sv_ = masked ? kMaskedScore : st[sub][r] * scale;
+                        const float pr = __expf(sv_ - mq) * iq;
+                        val = masked ? 0.f : pr * (dpt[sub][r] * pick(f, r) - dsv);
+                    }
+                    ds[sub][r] = val;
+                }
+            }
+            cols_times_weights<DK, NS>(Ks + k0 * S, g, c16, ds, acc);
+        };
+        int c0 = 0;
+        for (; c0 + kNS <= nsub; c0 += kNS) chunk(std::integral_constant<int, kNS>{}, c0 * 16);
+        for (; c0 < nsub; ++c0) chunk(std::integral_constant<int, 1>{}, c0 * 16);
+        if (qok) {
+            float* row = dq + (tok0 + qi) * lddq + h * DK;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+                *reinterpret_cast<float4*>(row + ct * 16 + 4 * g) =
+                    make_float4(acc[ct][0] * scale, acc[ct][1] * scale, acc[ct][2] * scale, acc[ct][3] * scale);
+        }
+    }
+}
+
+template <int DK>
+__global__ __launch_bounds__(kResThreads) void attn_bwd_dkdv_res_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
+    int64_t ldv, const float* __restrict__ dout, int64_t lddo, const float* __restrict__ stats,
+    const float* __restrict__ dsum, float* __restrict__ dk, int64_t lddk, float* __restrict__ dv, int64_t lddv,
+    const uint8_t* __restrict__ key_valid, int H, int L, int causal, float scale, float p_drop, uint64_t seed,
+    const uint8_t* __restrict__ drop_mask) {
+    constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int Lp = res_rows(L);
+    float* Qs = lds;
+    float* Ds = Qs + Lp * S;
+    float* mx_s = Ds + Lp * S;
+    float* il_s = mx_s + Lp;
+    float* dsum_s = il_s + Lp;
+    uint32_t* kvw = reinterpret_cast<uint32_t*>(dsum_s + Lp);
+    int* ctl = reinterpret_cast<int*>(kvw + (Lp + 31) / 32);
+
+    const int bh = blockIdx.x, b = bh / H, h = bh % H;
+    const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+    const int64_t tok0 = (int64_t)b * L;
+
+    stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
+    load_pair_resident<DK>(q + tok0 * ldq + h * DK, ldq, dout + tok0 * lddo + h * DK, lddo, L, Lp, Qs, Ds);
+    for (int i = threadIdx.x; i < Lp; i += kResThreads) {
+        const bool ok = i < L;
+        mx_s[i] = ok ? stats[((int64_t)bh * L + i) * 2] : 0.f;
+        il_s[i] = ok ? stats[((int64_t)bh * L + i) * 2 + 1] : 0.f;
+        dsum_s[i] = ok ? dsum[(int64_t)bh * L + i] : 0.f;
+    }
+    __syncthreads();
+    const int last_valid = ctl[0];
+    const bool any_valid = last_valid >= 0;
+    const int ngroups = Lp / 16;
+
+    for (;;) {
+        const int gi = claim_group(ctl, lane);
+        if (gi >= ngroups) break;
+        const int kb = gi * 16;  // causal: earlier key groups see more queries -> claimed first
+        const int kj = kb + c16;
+        const bool key_ok = kj < L;
+        floatx4 dvt[NCT], dkt[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) dvt[ct] = dkt[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // padding keys past the last valid one receive no probability from any query
+        const bool dead = any_valid && kb > last_valid;
+        if (!dead) {
+            float kf[DQ], vf[DQ];
+            load_row_slice<DK>(k + (tok0 + kj) * ldk + h * DK, key_ok, g, kf);
+            load_row_slice<DK>(v + (tok0 + kj) * ldv + h * DK, key_ok, g, vf);
+            const bool key_masked_pad = key_ok ? !((kvw[kj >> 5] >> (kj & 31)) & 1u) : true;
+            const uint16_t* keyw_row = drop_mask ? mask_keys(const_cast<uint8_t*>(drop_mask), (int64_t)gridDim.x, L) +
+                                                       ((int64_t)bh * L + min(kj, L - 1)) * ((L + 15) / 16)
+                                                 : nullptr;
+            const int q_start = (causal && any_valid) ? kb : 0;  // earlier queries see none of these keys
+            const int nsub = (Lp - q_start) / 16;
+            auto chunk = [&](auto ns_tag, int qb) {
+                constexpr int NS = decltype(ns_tag)::value;
+                floatx4 st[NS], dpt[NS];
+#pragma unroll
+                for (int sub = 0; sub < NS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
+                rows_times_slice<DK, NS>(Qs + qb * S, g, c16, kf, st);
+                rows_times_slice<DK, NS>(Ds + qb * S, g, c16, vf, dpt);
+                float pd[NS][4], ds[NS][4];
+#pragma unroll
+                for (int sub = 0; sub < NS; ++sub) {
+                    const int q4 = qb + sub * 16 + 4 * g;  // this lane's 4 query rows q4 .. q4+3
+                    const float4 mx4 = *reinterpret_cast<const float4*>(mx_s + q4);
+                    const float4 il4 = *reinterpret_cast<const float4*>(il_s + q4);
+                    const float4 ds4 = *reinterpret_cast<const float4*>(dsum_s + q4);
+                    const uint32_t mw = (p_drop > 0.f && drop_mask) ? keyw_row[(qb >> 4) + sub] >> (4 * g) : 0u;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int qq = q4 + r;
+                        float pv = 0.f, dsv = 0.f;
+                        if (qq < L && key_ok) {
+                            const bool masked = key_masked_pad || (causal && kj > qq);
+                            const float sv_ = masked ? kMaskedScore : st[sub][r] * scale;
+                            const float pr = __expf(sv_ - pick(mx4, r)) * pick(il4, r);
+                            float f = 1.f;
+                            if (p_drop > 0.f) {
+                                f = drop_mask ? ((mw >> r) & 1u ? 1.f / (1.f - p_drop) : 0.f)
+                                              : pick(attn_keep4(seed, (uint64_t)bh * L + qq, kj & ~3, p_drop), kj & 3);
+                            }
+                            pv = pr * f;
+                            dsv = masked ? 0.f : pr * (dpt[sub][r] * f - pick(ds4, r));
+                        }
+                        pd[sub][r] = pv;
+                        ds[sub][r] = dsv;
+                    }
+                }
+                cols_times_weights<DK, NS>(Ds + qb * S, g, c16, pd, dvt);  // dV^T += dO^T P
+                cols_times_weights<DK, NS>(Qs + qb * S, g, c16, ds, dkt);  // dK^T += Q^T dS
+            };
+            int c0 = 0;
+            for (; c0 + kNS <= nsub; c0 += kNS) chunk(std::integral_constant<int, kNS>{}, q_start + c0 * 16);
+            for (; c0 < nsub; ++c0) chunk(std::integral_constant<int, 1>{}, q_start + c0 * 16);
+        }
+        if (key_ok) {
+            float* krow = dk + (tok0 + kj) * lddk + h * DK;
+            float* vrow = dv + (tok0 + kj) * lddv + h * DK;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct) {
+                *reinterpret_cast<float4*>(krow + ct * 16 + 4 * g) =
+                    make_float4(dkt[ct][0] * scale, dkt[ct][1] * scale, dkt[ct][2] * scale, dkt[ct][3] * scale);
+                *reinterpret_cast<float4*>(vrow + ct * 16 + 4 * g) =
+                    make_float4(dvt[ct][0], dvt[ct][1], dvt[ct][2], dvt[ct][3]);
+            }
+        }
+    }
+}
+
+int g_attention_mode = 0;  // 0 auto, 1 streaming kernels only, 2 resident kernels when they fit
+
+template <class K>
+bool res_prepare(K kernel, size_t lds) {
+    if (lds > 160 * 1024) return false;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds) == hipSuccess;
 }
 
 #define ASME_DK_DISPATCH(DKV, ...)                                  \
@@ -529,9 +976,16 @@ ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, 
                    "asme_attention_fwd: operands must be 16-B aligned with ld % 4 == 0");
     if (batch == 0) return 0;
     const dim3 grid((unsigned)((seq_len + kQB - 1) / kQB), (unsigned)(batch * heads));
-    ASME_DK_DISPATCH(head_dim, hipLaunchKernelGGL(attn_fwd_kernel<DK>, grid, dim3(256), 0, (hipStream_t)stream, q, k,
-                                                  v, ld_q, ld_k, ld_v, out, ld_out, lse, key_valid, (int)heads,
-                                                  (int)seq_len, causal, scale, p_drop, seed, drop_mask));
+    const size_t lds = res_lds_bytes((int)seq_len, (int)head_dim, false);
+    ASME_DK_DISPATCH(head_dim,
+        if (g_attention_mode != 1 && res_prepare(attn_fwd_res_kernel<DK>, lds))
+            hipLaunchKernelGGL(attn_fwd_res_kernel<DK>, dim3((unsigned)(batch * heads)), dim3(kResThreads), lds,
+                               (hipStream_t)stream, q, k, v, ld_q, ld_k, ld_v, out, ld_out, lse, key_valid,
+                               (int)heads, (int)seq_len, causal, scale, p_drop, seed, drop_mask);
+        else
+            hipLaunchKernelGGL(attn_fwd_kernel<DK>, grid, dim3(256), 0, (hipStream_t)stream, q, k, v, ld_q, ld_k,
+                               ld_v, out, ld_out, lse, key_valid, (int)heads, (int)seq_len, causal, scale, p_drop,
+                               seed, drop_mask));
     ASME_LAUNCH_CHECK("asme_attention_fwd");
 }
 
@@ -550,13 +1004,39 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
     if (batch == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)((seq_len + kQB - 1) / kQB), (unsigned)(batch * heads));
+    const dim3 rgrid((unsigned)(batch * heads));
+    const size_t lds_dq = res_lds_bytes((int)seq_len, (int)head_dim, false);
+    const size_t lds_kv = res_lds_bytes((int)seq_len, (int)head_dim, true);
     ASME_DK_DISPATCH(
         head_dim,
+        if (g_attention_mode != 1 && res_prepare(attn_bwd_dq_res_kernel<DK>, lds_dq) &&
+            res_prepare(attn_bwd_dkdv_res_kernel<DK>, lds_kv)) {
+            hipLaunchKernelGGL(attn_bwd_dq_res_kernel<DK>, rgrid, dim3(kResThreads), lds_dq, s, q, k, v, ld_q, ld_k,
+                               ld_v, out, ld_out, dout, ld_dout, lse, dsum_ws, dq, ld_dq, key_valid, (int)heads,
+                               (int)seq_len, causal, scale, p_drop, seed, drop_mask);
+            hipLaunchKernelGGL(attn_bwd_dkdv_res_kernel<DK>, rgrid, dim3(kResThreads), lds_kv, s, q, k, v, ld_q, ld_k,
+                               ld_v, dout, ld_dout, lse, dsum_ws, dk, ld_dk, dv, ld_dv, key_valid, (int)heads,
+                               (int)seq_len, causal, scale, p_drop, seed, drop_mask);
+        } else {
         hipLaunchKernelGGL(attn_bwd_dq_kernel<DK>, grid, dim3(256), 0, s, q, k, v, ld_q, ld_k, ld_v, out, ld_out, dout,
                            ld_dout, lse, dsum_ws, dq, ld_dq, key_valid, (int)heads, (int)seq_len, causal, scale,
                            p_drop, seed, drop_mask);
         hipLaunchKernelGGL(attn_bwd_dkdv_kernel<DK>, grid, dim3(256), 0, s, q, k, v, ld_q, ld_k, ld_v, dout,
                            ld_dout, lse, dsum_ws, dk, ld_dk, dv, ld_dv, key_valid, (int)heads, (int)seq_len, causal,
-                           scale, p_drop, seed, drop_mask));
+                           scale, p_drop, seed, drop_mask);
+        });
     ASME_LAUNCH_CHECK("asme_attention_bwd");
+}
+
+// bytes of the drop_mask buffer the forward fills when p_drop > 0 (nibble image + key-major words)
+ASME_API int64_t asme_attention_dropout_mask_bytes(int64_t batch, int64_t heads, int64_t seq_len) {
+    return mask_total_bytes(batch * heads, (int)seq_len);
+}
+
+// 0 = automatic (resident kernels whenever the head's operands fit LDS), 1 = streaming kernels only,
+// 2 = same as 0 (kept distinct for tests).  Returns the previous mode.
+ASME_API int asme_attention_set_mode(int mode) {
+    const int prev = g_attention_mode;
+    g_attention_mode = mode;
+    return prev;
 }

@@ -443,6 +443,10 @@ def gelu_dropout(x, p: float = 0.0):
 
 
 # ------------------------------------------------------------------------------------ attention
+def _mask_bytes(batch: int, heads: int, seq_len: int) -> int:
+    return int(_lib.load().asme_attention_dropout_mask_bytes(batch, heads, seq_len))
+
+
 class _AttentionFn(torch.autograd.Function):
     """Attention.forward (transformer_layers.py:138-155) on a fused (B, L, 3*H*dk) QKV tensor.
     key_valid (B, L) uint8; causal selects SASRec's tril mask (sequence_representation.py:34-48)."""
@@ -458,8 +462,7 @@ class _AttentionFn(torch.autograd.Function):
         seed = new_seed(p_drop)
         scale = 1.0 / math.sqrt(dk)
         base = qkv.data_ptr()
-        mask = torch.empty(B * heads * L * ((L + 3) // 4), device=qkv.device, dtype=torch.uint8) if p_drop > 0 \
-            else None
+        mask = torch.empty(_mask_bytes(B, heads, L), device=qkv.device, dtype=torch.uint8) if p_drop > 0 else None
         call("asme_attention_fwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(key_valid), B,
              heads, L, dk, int(causal), scale, p_drop, seed, ptr(out), Dm, ptr(lse), ptr(mask), stream())
         ctx.save_for_backward(qkv, key_valid, out, lse, mask)

@@ -27,10 +27,17 @@ def _attn_ref(q, k, v, valid, causal):
     return torch.matmul(F.softmax(s, -1), v)
 
 
+@pytest.fixture(params=[0, 1], ids=["auto", "streaming"])
+def attn_mode(request, asme):
+    prev = asme._lib.load().asme_attention_set_mode(request.param)
+    yield request.param
+    asme._lib.load().asme_attention_set_mode(prev)
+
+
 @pytest.mark.parametrize("dk", [16, 32, 64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("L", [1, 7, 16, 50, 67, 200])
-def test_attention_fwd_bwd(asme, dev, dk, causal, L):
+def test_attention_fwd_bwd(asme, dev, dk, causal, L, attn_mode):
     torch.manual_seed(L * 7 + dk + causal)
     B, H = 3, 2
     D = H * dk
@@ -66,7 +73,7 @@ def test_attention_dropout_deterministic(asme, dev):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-def test_attention_dropout_mask_matches_regeneration(asme, dev, causal):
+def test_attention_dropout_mask_matches_regeneration(asme, dev, causal, attn_mode):
     """The backward reading the forward's stored keep-nibbles equals the backward regenerating them."""
     torch.manual_seed(1)
     B, L, H, dk = 3, 67, 2, 64
@@ -76,7 +83,7 @@ def test_attention_dropout_mask_matches_regeneration(asme, dev, causal):
     dout = torch.randn(B, L, D, device=dev)
     out = torch.empty(B, L, D, device=dev)
     stats = torch.empty(B * H, L, 2, device=dev)
-    mask = torch.empty(B * H * L * ((L + 3) // 4), device=dev, dtype=torch.uint8)
+    mask = torch.empty(asme.ops._mask_bytes(B, H, L), device=dev, dtype=torch.uint8)
     call, ptr, st = asme._lib.call, asme._lib.ptr, asme._lib.stream
     b, scale, seed = qkv.data_ptr(), dk ** -0.5, 1234567
     call("asme_attention_fwd", b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(valid), B, H, L, dk, int(causal),
@@ -92,6 +99,28 @@ def test_attention_dropout_mask_matches_regeneration(asme, dev, causal):
         grads.append(g)
     torch.cuda.synchronize()
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_resident_matches_streaming_with_dropout(asme, dev, causal):
+    """Both kernel families draw the same dropout masks (keyed by row and key), so they agree."""
+    torch.manual_seed(3)
+    B, L, H, dk = 4, 200, 2, 64
+    qkv = torch.randn(B, L, 3 * H * dk, device=dev)
+    valid = (torch.arange(L).unsqueeze(0) < torch.tensor([200, 150, 1, 0]).unsqueeze(1)).to(torch.uint8).to(dev)
+    g = torch.randn(B, L, H * dk, device=dev)
+    lib = asme._lib.load()
+    res = []
+    for mode in (0, 1):
+        prev = lib.asme_attention_set_mode(mode)
+        x = qkv.clone().requires_grad_(True)
+        torch.manual_seed(11)
+        out = asme.ops.attention(x, valid, H, causal, 0.2)
+        out.backward(g)
+        lib.asme_attention_set_mode(prev)
+        res.append((out.detach(), x.grad))
+    assert _rel(res[0][0], res[1][0]) < 1e-5
+    assert _rel(res[0][1], res[1][1]) < 1e-4
 
 
 @pytest.mark.parametrize("D", [16, 32, 64, 128, 200])
