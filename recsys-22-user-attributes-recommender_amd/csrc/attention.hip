@@ -75,29 +75,32 @@ __device__ __forceinline__ float4 bits_keep(uint8_t m, float p) {
     const float k = 1.f / (1.f - p);
     return make_float4(m & 1 ? k : 0.f, m & 2 ? k : 0.f, m & 4 ? k : 0.f, m & 8 ? k : 0.f);
 }
-// A second, key-major copy serves the dK/dV pass, whose lanes own keys: u16 word (key row, 16-query
-// group j) of (B*H*L) x ceil(L/16), bit i = query 16j+i kept.  It follows the nibble image, 256-B aligned.
+// A second copy serves the dK/dV pass, whose lanes own keys: u16 words [B*H][ceil(L/16) query groups]
+// [4*ceil(L/4) keys], bit i of word (j, key) = query 16j+i kept.  It follows the nibble image, 256-B aligned.
 __host__ __device__ inline int64_t mask_nibble_bytes(int64_t bh, int L) { return bh * L * ((L + 3) / 4); }
+__host__ __device__ inline int mask_key_stride(int L) { return 4 * ((L + 3) / 4); }
 __host__ __device__ inline int64_t mask_total_bytes(int64_t bh, int L) {
-    return ((mask_nibble_bytes(bh, L) + 255) & ~(int64_t)255) + bh * L * ((L + 15) / 16) * 2;
+    return ((mask_nibble_bytes(bh, L) + 255) & ~(int64_t)255) + bh * ((L + 15) / 16) * mask_key_stride(L) * 2;
 }
 __device__ __forceinline__ uint16_t* mask_keys(uint8_t* m, int64_t bh_total, int L) {
     return reinterpret_cast<uint16_t*>(m + ((mask_nibble_bytes(bh_total, L) + 255) & ~(int64_t)255));
 }
 // Forward-side store of one 16-key sub-tile's decisions (lane: query row c16 of group q0/16, keys
-// key4..key4+3 with key4 = ks + 4g): the nibble for the dQ pass, and via ballots the key-major words.
+// key4..key4+3 with key4 = ks + 4g): the nibble for the dQ pass, and via ballots the key-major words
+// (one 8-byte store of 4 keys' words per lane group).
 __device__ __forceinline__ void store_drop_bits(uint8_t* __restrict__ nib, uint16_t* __restrict__ keyw, int bh,
                                                 int L, int qi, int q0, int ks, int g, int c16, const float4& f) {
-    const int L4 = (L + 3) / 4, Lg = (L + 15) / 16;
+    const int L4 = (L + 3) / 4;
     const int key4 = ks + 4 * g;
     if (qi < L && key4 < L) nib[((int64_t)bh * L + qi) * L4 + key4 / 4] = keep_bits(f);
-    const float fv[4] = {f.x, f.y, f.z, f.w};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint64_t bal = __ballot(fv[r] != 0.f);  // bit 16g + c16: (key ks+4g+r, query q0+c16)
-        const int key = key4 + r;
-        if (c16 == 0 && key < L)
-            keyw[((int64_t)bh * L + key) * Lg + q0 / 16] = (uint16_t)(bal >> (16 * g));
+    // bit 16g + c16 of each ballot: (key ks+4g+r, query q0+c16)
+    const uint64_t b0 = __ballot(f.x != 0.f), b1 = __ballot(f.y != 0.f), b2 = __ballot(f.z != 0.f),
+                   b3 = __ballot(f.w != 0.f);
+    if (c16 == 0 && key4 < L) {
+        const int sh = 16 * g;
+        const uint64_t w = ((b0 >> sh) & 0xFFFFull) | (((b1 >> sh) & 0xFFFFull) << 16) |
+                           (((b2 >> sh) & 0xFFFFull) << 32) | (((b3 >> sh) & 0xFFFFull) << 48);
+        *reinterpret_cast<uint64_t*>(keyw + ((int64_t)bh * ((L + 15) / 16) + q0 / 16) * mask_key_stride(L) + key4) = w;
     }
 }
 
@@ -471,9 +474,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
     for (int ct = 0; ct < NCT; ++ct) dvt[ct] = dkt[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     const int wk0 = kblk + wave * 16;
-    const uint16_t* keyw_row = drop_mask ? mask_keys(const_cast<uint8_t*>(drop_mask), (int64_t)gridDim.y, L) +
-                                               ((int64_t)bh * L + min(kj, L - 1)) * ((L + 15) / 16)
+    // key-major dropout words of this lane's key: group j at keyw_key[j * mask_key_stride(L)]
+    const uint16_t* keyw_key = drop_mask ? mask_keys(const_cast<uint8_t*>(drop_mask), (int64_t)gridDim.y, L) +
+                                               (int64_t)bh * ((L + 15) / 16) * mask_key_stride(L) + min(kj, L - 1)
                                          : nullptr;
+    const int kstride = mask_key_stride(L);
     const bool wave_live = wk0 < L;
     // causal: queries before this key block see none of its keys (unless no key is valid at all)
     const int q_start = (causal && any_valid) ? kblk : 0;
@@ -521,7 +526,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
                     const float pr = __expf(sv_ - mx_s[ql]) * il_s[ql];
                     float f = 1.f;
                     if (p_drop > 0.f) {
-                        f = drop_mask ? ((keyw_row[qq >> 4] >> (qq & 15)) & 1 ? 1.f / (1.f - p_drop) : 0.f)
+                        f = drop_mask ? ((keyw_key[(qq >> 4) * kstride] >> (qq & 15)) & 1 ? 1.f / (1.f - p_drop) : 0.f)
                                       : pick(attn_keep4(seed, (uint64_t)bh * L + qq, kj & ~3, p_drop), kj & 3);
                     }
                     pv = pr * f;
@@ -610,6 +615,17 @@ __device__ __forceinline__ uint32_t valid_bits4(const uint32_t* kvw, int ks, int
     return (kvw[ks >> 5] >> ((ks & 16) + 4 * g)) & 0xFu;
 }
 
+// wave-uniform: every key of [k0, k0+n) exists, is valid and (causal) precedes every query >= q0
+__device__ __forceinline__ bool chunk_unmasked(const uint32_t* kvw, int k0, int n, int L, int causal, int q0) {
+    if (k0 + n > L || (causal && k0 + n - 1 > q0)) return false;
+    bool ok = true;
+    for (int ks = k0; ks < k0 + n; ks += 16) {
+        const uint32_t w = __builtin_amdgcn_readfirstlane(kvw[ks >> 5]);
+        ok = ok && ((w >> (ks & 16)) & 0xFFFFu) == 0xFFFFu;
+    }
+    return ok;
+}
+
 __device__ __forceinline__ int claim_group(int* ctl, int lane) {
     int gi = 0;
     if (lane == 0) gi = atomicAdd(ctl + 1, 1);
@@ -667,19 +683,29 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
             rows_times_slice<DK, NS>(Ks + k0 * S, g, c16, qf, st);
             float p[NS][4];
             float tmax = kInitMax;
+            if (chunk_unmasked(kvw, k0, NS * 16, L, causal, q0)) {
 #pragma unroll
-            for (int sub = 0; sub < NS; ++sub) {
-                const uint32_t vb = valid_bits4(kvw, k0 + sub * 16, g);
+                for (int sub = 0; sub < NS; ++sub)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = k0 + sub * 16 + 4 * g + r;
-                    float sv_ = -INFINITY;  // not a key: contributes nothing
-                    if (key < L) {
-                        const bool masked = !((vb >> r) & 1u) || (causal && key > qi);
-                        sv_ = masked ? kMaskedScore : st[sub][r] * scale;
+                    for (int r = 0; r < 4; ++r) {
+                        p[sub][r] = st[sub][r] * scale;
+                        tmax = fmaxf(tmax, p[sub][r]);
                     }
-                    p[sub][r] = sv_;
-                    tmax = fmaxf(tmax, sv_);
+            } else {
+#pragma unroll
+                for (int sub = 0; sub < NS; ++sub) {
+                    const uint32_t vb = valid_bits4(kvw, k0 + sub * 16, g);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int key = k0 + sub * 16 + 4 * g + r;
+                        float sv_ = -INFINITY;  // not a key: contributes nothing
+                        if (key < L) {
+                            const bool masked = !((vb >> r) & 1u) || (causal && key > qi);
+                            sv_ = masked ? kMaskedScore : st[sub][r] * scale;
+                        }
+                        p[sub][r] = sv_;
+                        tmax = fmaxf(tmax, sv_);
+                    }
                 }
             }
             tmax = group4_max(tmax);
@@ -882,9 +908,10 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dkdv_res_kernel(
             load_row_slice<DK>(k + (tok0 + kj) * ldk + h * DK, key_ok, g, kf);
             load_row_slice<DK>(v + (tok0 + kj) * ldv + h * DK, key_ok, g, vf);
             const bool key_masked_pad = key_ok ? !((kvw[kj >> 5] >> (kj & 31)) & 1u) : true;
-            const uint16_t* keyw_row = drop_mask ? mask_keys(const_cast<uint8_t*>(drop_mask), (int64_t)gridDim.x, L) +
-                                                       ((int64_t)bh * L + min(kj, L - 1)) * ((L + 15) / 16)
+            const uint16_t* keyw_key = drop_mask ? mask_keys(const_cast<uint8_t*>(drop_mask), (int64_t)gridDim.x, L) +
+                                                       (int64_t)bh * ((L + 15) / 16) * mask_key_stride(L) + min(kj, L - 1)
                                                  : nullptr;
+            const int kstride = mask_key_stride(L);
             const int q_start = (causal && any_valid) ? kb : 0;  // earlier queries see none of these keys
             const int nsub = (Lp - q_start) / 16;
             auto chunk = [&](auto ns_tag, int qb) {
@@ -901,7 +928,7 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dkdv_res_kernel(
                     const float4 mx4 = *reinterpret_cast<const float4*>(mx_s + q4);
                     const float4 il4 = *reinterpret_cast<const float4*>(il_s + q4);
                     const float4 ds4 = *reinterpret_cast<const float4*>(dsum_s + q4);
-                    const uint32_t mw = (p_drop > 0.f && drop_mask) ? keyw_row[(qb >> 4) + sub] >> (4 * g) : 0u;
+                    const uint32_t mw = (p_drop > 0.f && drop_mask) ? keyw_key[((qb >> 4) + sub) * kstride] >> (4 * g) : 0u;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int qq = q4 + r;

@@ -56,13 +56,21 @@ __device__ __forceinline__ float lane16_sum(float v) {
 struct u32x4 {
     uint32_t x, y, z, w;
 };
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32, truth table a^b^c
+}
+// Each round's two 32x32->64 products are single v_mad_u64_u32 (instead of a mul_hi + mul_lo pair) and
+// the key mix a single v_bitop3_b32 (keys must be wave-uniform: kernel arguments).
 __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
-    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+    const uint64_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+    k0 = __builtin_amdgcn_readfirstlane(k0);
+    k1 = __builtin_amdgcn_readfirstlane(k1);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-        uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
-        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        const uint64_t p0 = M0 * c.x, p1 = M1 * c.z;
+        c = u32x4{xor3((uint32_t)(p1 >> 32), c.y, k0), (uint32_t)p1, xor3((uint32_t)(p0 >> 32), c.w, k1),
+                  (uint32_t)p0};
         k0 += W0;
         k1 += W1;
     }
