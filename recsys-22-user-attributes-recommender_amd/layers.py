@@ -28,8 +28,13 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import ops
+from . import fused, ops
 from .sequence import get_attribute
+
+
+# Run the transformer stack as one fused autograd function (fused.py) when its shapes allow;
+# False forces the per-op path (the fused path is tested against it).
+FUSED_STACK = True
 
 
 def _p(module: nn.Module, training: bool) -> float:
@@ -242,6 +247,9 @@ class TransformerLayer(nn.Module):
         if len(blocks) == 0:
             return x
         tr = self.training
+        b0 = blocks[0]
+        if FUSED_STACK and fused.fusable(x.shape[-1], b0.feed_forward.w_1.weight.shape[0], b0.attention.heads, x):
+            return fused.transformer_stack(x, key_valid, blocks, causal, tr)
         ln = ops.layer_norm(x, blocks[0].input_sublayer.norm)
         for i, blk in enumerate(blocks):
             att, ff = blk.attention, blk.feed_forward
