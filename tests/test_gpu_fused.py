@@ -23,7 +23,7 @@ def _run(asme, layer, x, valid, causal, fused_on, seed):
         grads = {n: p.grad.clone() for n, p in layer.named_parameters() if p.grad is not None}
         return y.detach(), xx.grad.clone(), grads
     finally:
-        asme.layers.FUSED_STACK = True
+        asme.layers.FUSED_STACK = False
 
 
 @pytest.mark.parametrize("causal", [True, False])
