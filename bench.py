@@ -142,7 +142,8 @@ def main():
     # per-kernel device time of the dominant kernel (HIP events on the launching stream)
     timer = asme._lib.KernelTimer(["asme_adam_rows_step", "asme_attention_fwd", "asme_attention_bwd",
                                    "asme_embedding_fwd", "asme_embedding_bwd", "asme_lazy_adam_catch_up",
-                                   "asme_lazy_adam_apply", "asme_gelu_dropout_bwd"])
+                                   "asme_lazy_adam_apply", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
+                                   "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -181,17 +182,36 @@ def main():
     U = int(last_unique[0]) if last_unique else min(3 * B * L, V)
     T = B * L
     H, dk = args.heads, d // args.heads
-    # algorithmic work per launch; dense attention counts as in SURVEY §8d
+    ffn = 4 * d
+    # algorithmic work per launch.  Attention: causal pairs only (L(L+1)/2 per head), the
+    # forward = 2 matmul passes (QK^T, PV), the backward = 5 (recomputed S, dP, dV, dK, dQ) -- the kernels
+    # spend 2 more (dP and S again in the dK/dV pass), which is overhead, not algorithmic work.
+    pairs = B * H * L * (L + 1) / 2.0
+    # weight-gradient GEMMs: 4 per block (QKV, O, FFN in, FFN out), averaged per launch
+    wg_flops = 2.0 * T * (3 * d * d + d * d + ffn * d + d * ffn)
     work = {
-        "asme_attention_fwd": ("mfma", 4.0 * B * H * L * L * dk),
-        "asme_attention_bwd": ("mfma", 8.0 * B * H * L * L * dk),
+        "asme_attention_fwd": ("mfma", 2 * 2.0 * pairs * dk),
+        "asme_attention_bwd": ("mfma", 5 * 2.0 * pairs * dk),
+        "asme_linear_weight_grad": ("mfma", wg_flops / 4),
+        "asme_gelu_dropout_fwd": ("hbm", 2 * T * ffn * 4),
+        "asme_residual_ln_fwd": ("hbm", 4 * T * d * 4 + T * 8),
+        "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),
         "asme_embedding_fwd": ("hbm", T * 8 + 2 * T * d * 4 + T * 16),
         "asme_embedding_bwd": ("hbm", T * 8 + 3 * T * d * 4 + T * 16),
         "asme_lazy_adam_apply": ("hbm", U * 8 + U * d * 4 + 6 * U * d * 4 + U * 4),
         "asme_lazy_adam_catch_up": ("hbm", U * 8 + 6 * U * d * 4 + 2 * U * 4),
-        "asme_gelu_dropout_bwd": ("hbm", 3 * T * 4 * d * 4),
+        "asme_gelu_dropout_bwd": ("hbm", 3 * T * ffn * 4),
         "asme_adam_rows_step": ("hbm", 6 * V * d * 4 + V * 4 + U * d * 4),
     }
+    # HBM traffic per launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE, gfx950
+    # corrections of MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py) for this exact configuration
+    traffic = {}
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tp):
+        with open(tp) as f:
+            tj = json.load(f)
+        if tj.get("config") == {"batch": B, "seq_len": L, "items": args.items, "dim": d, "layers": args.layers}:
+            traffic = tj.get("bytes_per_launch", {})
     rooflines = []
     for name, st in kstats.items():
         if not st["count"] or name not in work:
@@ -203,7 +223,7 @@ def main():
         else:
             ach, peak, unit = amount / secs / 1e9, PEAK_HBM_GBS, "GB/s"
         rooflines.append({"kernel": name, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
-                          "frac": round(ach / peak, 4), "traffic": None, "avg_ms": round(st["avg_ms"], 4),
+                          "frac": round(ach / peak, 4), "traffic": traffic.get(name), "avg_ms": round(st["avg_ms"], 4),
                           "launches": st["count"], "total_ms": round(st["total_ms"], 3),
                           ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): amount})
     rooflines.sort(key=lambda r: -r["total_ms"])

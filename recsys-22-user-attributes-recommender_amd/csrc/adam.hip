@@ -58,6 +58,29 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
     p = p + hp.neg_step_size * (m * __builtin_amdgcn_rcpf(denom));
 }
 
+// The same update on 4 consecutive elements as two packed pairs (v_pk_mul_f32 / v_pk_add_f32: IEEE
+// results identical to adam_elem's scalar ops, same order, no contraction) -- half the VALU issue of the
+// scalar form, which is what bounds the lazy replay.
+typedef float float2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void adam_elem2(float2v& p, float2v g, float2v& m, float2v& v, const AdamHyper& hp) {
+#pragma clang fp contract(off)
+    if (hp.wd != 0.f) g = g + hp.wd * p;
+    m = m + hp.one_minus_b1 * (g - m);
+    v = v * hp.b2 + hp.one_minus_b2 * g * g;
+    const float2v s = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+    const float2v d = s * hp.inv_bc2_sqrt + hp.eps;
+    const float2v r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    p = p + hp.neg_step_size * (m * r);
+}
+__device__ __forceinline__ void adam_elem4(float4& P, const float4& G, float4& M, float4& V, const AdamHyper& hp) {
+    float2v p0 = {P.x, P.y}, p1 = {P.z, P.w}, m0 = {M.x, M.y}, m1 = {M.z, M.w}, v0 = {V.x, V.y}, v1 = {V.z, V.w};
+    adam_elem2(p0, float2v{G.x, G.y}, m0, v0, hp);
+    adam_elem2(p1, float2v{G.z, G.w}, m1, v1, hp);
+    P = make_float4(p0.x, p0.y, p1.x, p1.y);
+    M = make_float4(m0.x, m0.y, m1.x, m1.y);
+    V = make_float4(v0.x, v0.y, v1.x, v1.y);
+}
+
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamList L, AdamHyper hp) {
     const int64_t blk = blockIdx.x;
     int ti = 0;
@@ -76,10 +99,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamList L, AdamHyper h
             const float4 G = g ? *reinterpret_cast<const float4*>(g + i) : make_float4(0.f, 0.f, 0.f, 0.f);
             float4 M = *reinterpret_cast<const float4*>(m + i);
             float4 Vv = *reinterpret_cast<const float4*>(v + i);
-            adam_elem(P.x, G.x, M.x, Vv.x, hp);
-            adam_elem(P.y, G.y, M.y, Vv.y, hp);
-            adam_elem(P.z, G.z, M.z, Vv.z, hp);
-            adam_elem(P.w, G.w, M.w, Vv.w, hp);
+            adam_elem4(P, G, M, Vv, hp);
             *reinterpret_cast<float4*>(p + i) = P;
             *reinterpret_cast<float4*>(m + i) = M;
             *reinterpret_cast<float4*>(v + i) = Vv;
@@ -108,10 +128,7 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(float* __restrict__ p, f
         float4 P = *reinterpret_cast<const float4*>(p + e);
         float4 M = *reinterpret_cast<const float4*>(m + e);
         float4 Vv = *reinterpret_cast<const float4*>(v + e);
-        adam_elem(P.x, G.x, M.x, Vv.x, hp);
-        adam_elem(P.y, G.y, M.y, Vv.y, hp);
-        adam_elem(P.z, G.z, M.z, Vv.z, hp);
-        adam_elem(P.w, G.w, M.w, Vv.w, hp);
+        adam_elem4(P, G, M, Vv, hp);
         *reinterpret_cast<float4*>(p + e) = P;
         *reinterpret_cast<float4*>(m + e) = M;
         *reinterpret_cast<float4*>(v + e) = Vv;
@@ -252,21 +269,36 @@ __global__ __launch_bounds__(256) void lazy_catch_up_v4_kernel(const int64_t* __
     const int lane = threadIdx.x & 63;
     const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LPR) + lane / LPR;
     const int64_t n = count ? (int64_t)*count : cap;
-    if (s >= n || s >= cap) return;
-    const int64_t r = rows ? rows[s] : s;
-    const int32_t t0 = last_step[r];
-    if (t0 >= upto) return;
+    const bool in_range = s < n && s < cap;
+    const int64_t r = in_range ? (rows ? rows[s] : s) : 0;
+    const int32_t t0 = in_range ? last_step[r] : upto;
+    // The rows of a wave have different last steps: replay over the wave's whole range with a uniform step
+    // counter (hist[t] is then a scalar load, not a per-lane gather) and let each lane apply only its own
+    // steps.  All lanes of a row agree, so the per-row result is exactly the per-row replay.
+    int32_t t_lo = t0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t_lo = min(t_lo, __shfl_xor(t_lo, o, 64));
+    t_lo = __builtin_amdgcn_readfirstlane(t_lo);
+    if (t_lo >= upto) return;  // wave-uniform
+    const bool live = t0 < upto;
     const int64_t off = r * D + (lane % LPR) * 4;
-    float4 P = *reinterpret_cast<const float4*>(p + off);
-    float4 M = *reinterpret_cast<const float4*>(m + off);
-    float4 Vv = *reinterpret_cast<const float4*>(v + off);
-    for (int32_t t = t0 + 1; t <= upto; ++t) {
-        const AdamHyper hp = hist[t];
-        adam_elem(P.x, 0.f, M.x, Vv.x, hp);
-        adam_elem(P.y, 0.f, M.y, Vv.y, hp);
-        adam_elem(P.z, 0.f, M.z, Vv.z, hp);
-        adam_elem(P.w, 0.f, M.w, Vv.w, hp);
+    float4 P = make_float4(0.f, 0.f, 0.f, 0.f), M = P, Vv = P;
+    if (live) {
+        P = *reinterpret_cast<const float4*>(p + off);
+        M = *reinterpret_cast<const float4*>(m + off);
+        Vv = *reinterpret_cast<const float4*>(v + off);
     }
+    const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int32_t t = t_lo + 1; t <= upto; ++t) {
+        float4 P2 = P, M2 = M, V2 = Vv;
+        adam_elem4(P2, Z, M2, V2, hist[t]);
+        if (t > t0) {
+            P = P2;
+            M = M2;
+            Vv = V2;
+        }
+    }
+    if (!live) return;
     *reinterpret_cast<float4*>(p + off) = P;
     *reinterpret_cast<float4*>(m + off) = M;
     *reinterpret_cast<float4*>(v + off) = Vv;
@@ -292,10 +324,7 @@ __global__ __launch_bounds__(256) void lazy_apply_v4_kernel(const int64_t* __res
     float4 M = *reinterpret_cast<const float4*>(m + off);
     float4 Vv = *reinterpret_cast<const float4*>(v + off);
     const float4 G = *reinterpret_cast<const float4*>(grad_rows + s * D + c);
-    adam_elem(P.x, G.x, M.x, Vv.x, hp);
-    adam_elem(P.y, G.y, M.y, Vv.y, hp);
-    adam_elem(P.z, G.z, M.z, Vv.z, hp);
-    adam_elem(P.w, G.w, M.w, Vv.w, hp);
+    adam_elem4(P, G, M, Vv, hp);
     *reinterpret_cast<float4*>(p + off) = P;
     *reinterpret_cast<float4*>(m + off) = M;
     *reinterpret_cast<float4*>(v + off) = Vv;
