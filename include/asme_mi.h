@@ -214,6 +214,28 @@ int asme_linear_dx_residual_ln_bwd(const float* dy, int64_t ld_dy, int64_t n_row
                                    const float* d_in, float p_a, uint64_t seed_a, float p_b, uint64_t seed_b,
                                    float* d_res, float* d_y, float* partials, void* stream);
 
+
+/* ---- Full-catalogue evaluation (csrc/catalog.hip), no (queries x |V|) logits.  Reference:
+ * SASRecProjectionComponent inference (sasrec/components.py:46-61), ItemEmbeddingProjectionLayer
+ * (layers.py:138-143), AllItemsSampler + argsort + get_true_positives (metrics_sampler.py:51-72,
+ * metrics/common.py:4-27).  score(q, i) = H[q] . E[i] (+ bias[i]); dim in {32, 64, 128}. */
+/* ranks[q] = 1 + #{i : score > score(target), or equal with i < target}; counts_ws: nq int32 */
+int asme_catalog_rank(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* E, int64_t ld_e, int64_t V,
+                      const float* bias, const int64_t* targets, int32_t* counts_ws, int64_t* ranks, void* stream);
+int64_t asme_catalog_topk_workspace(int64_t nq, int64_t V, int64_t dim);
+/* k <= 16 best (score, item) per query, descending, ties to the lower id; row j of E is item
+ * j * id_stride + id_offset (1, 0 for a whole table; W, rank for a cyclic row shard) */
+int asme_catalog_topk(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* E, int64_t ld_e, int64_t V,
+                      const float* bias, int64_t id_stride, int64_t id_offset, int64_t k, void* ws, int64_t ws_bytes,
+                      float* out_val, int64_t* out_idx, void* stream);
+/* sharded ranks: target scores from the gathered target rows (same MFMA sequence as the shard scans), then
+ * per-shard counts of items above the target (global ids); rank = 1 + all-reduced sum of the counts */
+int asme_catalog_target_scores(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* rows,
+                               int64_t ld_rows, const float* row_bias, float* tscore, void* stream);
+int asme_catalog_count_above(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* E, int64_t ld_e,
+                             int64_t V_local, const float* bias, const int64_t* targets, const float* tscore,
+                             int64_t id_stride, int64_t id_offset, int32_t* counts, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -573,17 +573,18 @@ __device__ __forceinline__ void load_pair_resident(const float* __restrict__ a, 
                                                    float* __restrict__ As, float* __restrict__ Bs) {
     constexpr int C4 = DK / 4, S = DK + 4;
     const int n4 = Lp * C4;
-    for (int base = threadIdx.x; base < n4; base += kResThreads * 4) {
-        float4 ra[4], rb[4];
+    // all loads of a batch are issued before the first store: at L = 200, dk = 64 one batch covers the head
+    for (int base = threadIdx.x; base < n4; base += kResThreads * 8) {
+        float4 ra[8], rb[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
             const int idx = base + u * kResThreads, row = idx / C4, c = (idx % C4) * 4;
             const bool ok = idx < n4 && row < L;
             ra[u] = ok ? *reinterpret_cast<const float4*>(a + (int64_t)row * lda + c) : make_float4(0.f, 0.f, 0.f, 0.f);
             rb[u] = ok ? *reinterpret_cast<const float4*>(b + (int64_t)row * ldb + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
             const int idx = base + u * kResThreads, row = idx / C4, c = (idx % C4) * 4;
             if (idx < n4) {
                 *reinterpret_cast<float4*>(As + row * S + c) = ra[u];

@@ -141,7 +141,11 @@ class RankingMetricsContainer(torch.nn.Module):
     def update(self, input_seq, targets: torch.Tensor, predictions: torch.Tensor, mask=None) -> Dict[str, torch.Tensor]:
         if targets.dim() != 1:
             raise NotImplementedError("multi-target (basket) evaluation is outside the MI355X hot path")
-        ranks = ops.target_rank(predictions.float(), targets)
+        return self.update_ranks(ops.target_rank(predictions.float(), targets))
+
+    def update_ranks(self, ranks: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Accumulate from the targets' 1-based ranks directly (the fused full-catalogue path,
+        ops.catalog_rank / sharded.catalog_ranks, never materialises the predictions)."""
         out = {}
         for m in self.metrics:
             per_row = m.from_ranks(ranks)

@@ -49,6 +49,12 @@ class SequenceRecommenderModel(nn.Module):
     def forward(self, sequence):
         return self._projection_layer(self.encode(sequence), sequence)
 
+    def catalog_query(self, sequence):
+        """(queries (N, d), item table (|V|, d), bias or None) such that the full-catalogue scores the
+        inference forward would produce are queries . table^T (+ bias) -- for the fused evaluation
+        (ops.catalog_rank) that never builds them.  None when the projection is not of that form."""
+        return None
+
     def required_metadata_keys(self) -> List[str]:
         return []
 
@@ -149,6 +155,20 @@ class SASRecModel(TransformerEncoderModel):
 
     def required_metadata_keys(self):
         return self.additional_metadata_keys
+
+    def catalog_query(self, sequence):
+        """last valid position's representation vs the item table (SASRecProjectionComponent inference,
+        sasrec/components.py:46-61); the 'full' mode's Linear head is weight + bias over |V| outputs."""
+        rep = self.encode(sequence)
+        idx = sequence.padding_mask.sum(-1) - 1
+        last = rep[torch.arange(rep.shape[0], device=rep.device), idx]
+        proj = self._projection_layer
+        if isinstance(proj, Ly.SASRecProjectionComponent):
+            return last, proj.embedding.get_item_embedding_weight(), None
+        lin = getattr(proj, "linear", None)
+        if isinstance(lin, nn.Linear):
+            return last, lin.weight, lin.bias
+        return None
 
     def item_table(self):
         return self._sequence_embedding_layer.item_embedding_layer.get_item_embedding_weight()

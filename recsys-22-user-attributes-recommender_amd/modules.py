@@ -49,6 +49,11 @@ except Exception:  # pragma: no cover - Lightning is not part of this image
             pass
 
 
+# catalogue size from which validation ranks targets with the fused kernel by default (a (1024, 2^20)
+# fp32 prediction tensor is 4 GiB; the reference materialises (B, |V|, d) even before that)
+FUSED_EVAL_MIN_ITEMS = 1 << 20
+
+
 def get_padding_mask(sequence: torch.Tensor, tokenizer) -> torch.Tensor:
     if sequence.dim() > 2:
         sequence = sequence.max(dim=2).values
@@ -116,7 +121,7 @@ class _TableGradMixin:
 class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
     def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
                  beta_2: float = 0.998, weight_decay: float = 1e-3,
-                 loss_function=None, table_grad: str = "dense"):
+                 loss_function=None, table_grad: str = "dense", fused_eval: Optional[bool] = None):
         super().__init__()
         self.model = model
         self.learning_rate, self.beta_1, self.beta_2, self.weight_decay = learning_rate, beta_1, beta_2, weight_decay
@@ -124,6 +129,9 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         self.metrics = metrics
         self.loss_function = loss_function if loss_function is not None else SASRecBinaryCrossEntropyLoss()
         self._init_table_grad(table_grad)
+        # fused_eval: rank the targets with asme_catalog_rank instead of materialising (B, |V|) predictions
+        # (None = automatically from |V| >= FUSED_EVAL_MIN_ITEMS); validation then returns predictions=None
+        self.fused_eval = fused_eval
 
     def training_step(self, batch, batch_idx):
         input_seq = batch[ITEM_SEQ_ENTRY_NAME]
@@ -148,8 +156,32 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         meta["positive_samples"] = items
         return self.model(InputSequence(input_seq, padding_mask, meta))
 
+    def _use_fused_eval(self, targets) -> bool:
+        if targets.dim() != 1 or self.metrics is None or not hasattr(self.metrics, "update_ranks"):
+            return False
+        if self.fused_eval is not None:
+            return bool(self.fused_eval)
+        return self.model.item_table().shape[0] >= FUSED_EVAL_MIN_ITEMS
+
+    def catalog_ranks(self, batch) -> torch.Tensor:
+        """1-based full-catalogue rank of each sequence's target (ties to the lower id) with the scores
+        streamed through asme_catalog_rank -- no (B, |V|) predictions."""
+        self._flush_table()
+        input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
+        meta = get_additional_meta_data(self.model, batch)
+        padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
+        q = self.model.catalog_query(InputSequence(input_seq, padding_mask, meta))
+        if q is None:
+            raise NotImplementedError("model projection is not a dot product with an item table")
+        h, table, bias = q
+        return ops.catalog_rank(h, table, targets, bias)
+
     def validation_step(self, batch, batch_idx):
         input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
+        if self._use_fused_eval(targets):
+            with torch.no_grad():
+                self.metrics.update_ranks(self.catalog_ranks(batch))
+            return build_eval_step_return_dict(input_seq, None, targets)
         prediction = self.predict_step(batch, batch_idx)
         self._update_metrics(targets, prediction)
         mask = None if targets.dim() == 1 else ~targets.eq(self.item_tokenizer.pad_token_id)

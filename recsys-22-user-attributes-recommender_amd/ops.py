@@ -614,3 +614,65 @@ def target_rank(scores: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
     ranks = torch.empty(n, device=s.device, dtype=torch.int64)
     call("asme_target_rank", ptr(s), V, ptr(t), n, V, ptr(ranks), stream())
     return ranks
+
+
+# ------------------------------------------------------------------------------------ full-catalogue eval
+def catalog_rank(hidden: torch.Tensor, table: torch.Tensor, targets: torch.Tensor,
+                 bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rank (1-based, ties to the lower id) of each row's target among all |V| items scored as
+    hidden . table^T (+ bias) -- the (rows, |V|) logits are never materialised (asme_catalog_rank).
+    Reference: SASRecProjectionComponent inference + AllItemsSampler + argsort (sasrec/components.py:46-61,
+    metrics/common.py:4-27)."""
+    h = _f32(hidden)
+    E = _f32(table)
+    n, d = h.shape
+    V = E.shape[0]
+    tg = _i64(targets).reshape(n)
+    counts = torch.empty(n, device=h.device, dtype=torch.int32)
+    ranks = torch.empty(n, device=h.device, dtype=torch.int64)
+    call("asme_catalog_rank", ptr(h), h.stride(0), n, d, ptr(E), E.stride(0), V,
+         ptr(_f32(bias)) if bias is not None else None, ptr(tg), ptr(counts), ptr(ranks), stream())
+    return ranks
+
+
+def catalog_topk(hidden: torch.Tensor, table: torch.Tensor, k: int, bias: Optional[torch.Tensor] = None,
+                 id_stride: int = 1, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The k (<= 16) best (score, item) per row over all |V| items, scores descending, ties to the lower id
+    (asme_catalog_topk; no (rows, |V|) logits)."""
+    h = _f32(hidden)
+    E = _f32(table)
+    n, d = h.shape
+    V = E.shape[0]
+    nbytes = int(_lib.load().asme_catalog_topk_workspace(n, V, d))
+    ws = torch.empty(max(16, nbytes), device=h.device, dtype=torch.uint8)
+    vals = torch.empty(n, k, device=h.device, dtype=torch.float32)
+    idx = torch.empty(n, k, device=h.device, dtype=torch.int64)
+    call("asme_catalog_topk", ptr(h), h.stride(0), n, d, ptr(E), E.stride(0), V,
+         ptr(_f32(bias)) if bias is not None else None, id_stride, id_offset, k, ptr(ws), nbytes, ptr(vals), ptr(idx),
+         stream())
+    return vals, idx
+
+
+def catalog_target_scores(hidden: torch.Tensor, target_rows: torch.Tensor,
+                          target_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """score of each row's target from its gathered table row, computed by the same MFMA sequence as the
+    shard scan (so the owner's scan compares bit-identically against it)."""
+    h, rows = _f32(hidden), _f32(target_rows)
+    n, d = h.shape
+    out = torch.empty(n, device=h.device, dtype=torch.float32)
+    call("asme_catalog_target_scores", ptr(h), h.stride(0), n, d, ptr(rows), rows.stride(0),
+         ptr(_f32(target_bias)) if target_bias is not None else None, ptr(out), stream())
+    return out
+
+
+def catalog_count_above(hidden: torch.Tensor, table_shard: torch.Tensor, targets: torch.Tensor,
+                        target_scores: torch.Tensor, id_stride: int, id_offset: int,
+                        bias_shard: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """#items of this table shard (local row j = item j*id_stride + id_offset) ranked above each row's target."""
+    h, E = _f32(hidden), _f32(table_shard)
+    n, d = h.shape
+    counts = torch.empty(n, device=h.device, dtype=torch.int32)
+    call("asme_catalog_count_above", ptr(h), h.stride(0), n, d, ptr(E), E.stride(0), E.shape[0],
+         ptr(_f32(bias_shard)) if bias_shard is not None else None, ptr(_i64(targets).reshape(n)),
+         ptr(_f32(target_scores)), id_stride, id_offset, ptr(counts), stream())
+    return counts

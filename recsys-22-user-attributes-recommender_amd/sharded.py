@@ -185,3 +185,55 @@ def train_step(module, optimizer, batch, batch_idx: int = 0):
     optimizer.step()
     optimizer.zero_grad(set_to_none=True)
     return loss
+
+
+# ------------------------------------------------------------------------------------ sharded evaluation
+def _gather_queries(x: torch.Tensor, group) -> torch.Tensor:
+    W = dist.get_world_size(group)
+    out = [torch.empty_like(x) for _ in range(W)]
+    dist.all_gather(out, x.contiguous(), group=group)
+    return torch.cat(out, 0)
+
+
+def catalog_ranks(exchange: RowShardExchange, hidden: torch.Tensor, targets: torch.Tensor,
+                  table_shard: torch.Tensor) -> torch.Tensor:
+    """Full-catalogue rank of every query's target with the item table row-sharded.
+
+    Every rank holds its own queries (hidden (n, d), targets (n,), n equal on all ranks).  The target rows
+    come from their owners (one all_to_all pair), the target scores are computed once by the same MFMA
+    sequence the shard scans use; every rank then counts, for the queries of ALL ranks, the items of ITS
+    shard that rank above the target (asme_catalog_count_above, no logits); one all_reduce(sum) of the
+    int32 counts gives the global ranks.  The table shard must be up to date (flush the lazy Adam first)."""
+    group, W, rank = exchange.group, exchange.world, exchange.rank
+    uniq, inv = torch.unique(targets, return_inverse=True)
+    st = exchange.request(uniq)
+    got = exchange.reply_rows(st, table_shard.index_select(0, st.recv_local))
+    tscore = ops.catalog_target_scores(hidden, got.index_select(0, inv))
+    h_all = _gather_queries(hidden, group)
+    t_all = _gather_queries(targets.to(torch.int64), group)
+    s_all = _gather_queries(tscore, group)
+    counts = ops.catalog_count_above(h_all, table_shard, t_all, s_all, W, rank)
+    dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    n = hidden.shape[0]
+    return counts[rank * n:(rank + 1) * n].to(torch.int64) + 1
+
+
+def catalog_topk(exchange: RowShardExchange, hidden: torch.Tensor, table_shard: torch.Tensor, k: int):
+    """Global top-k (score desc, item id asc) over the row-sharded table: every rank scores all ranks'
+    queries against its shard (asme_catalog_topk with global ids), the (k) candidates per shard are
+    all-gathered and merged."""
+    group, W, rank = exchange.group, exchange.world, exchange.rank
+    n = hidden.shape[0]
+    h_all = _gather_queries(hidden, group)
+    v, i = ops.catalog_topk(h_all, table_shard, k, id_stride=W, id_offset=rank)
+    vs = [torch.empty_like(v) for _ in range(W)]
+    is_ = [torch.empty_like(i) for _ in range(W)]
+    dist.all_gather(vs, v, group=group)
+    dist.all_gather(is_, i, group=group)
+    cand_v = torch.cat([x[rank * n:(rank + 1) * n] for x in vs], 1)
+    cand_i = torch.cat([x[rank * n:(rank + 1) * n] for x in is_], 1)
+    # (score desc, id asc): sort by id, then stably by score
+    o1 = torch.argsort(cand_i, dim=1, stable=True)
+    cand_v, cand_i = cand_v.gather(1, o1), cand_i.gather(1, o1)
+    o2 = torch.argsort(-cand_v, dim=1, stable=True)
+    return cand_v.gather(1, o2)[:, :k], cand_i.gather(1, o2)[:, :k]

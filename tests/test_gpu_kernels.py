@@ -400,3 +400,31 @@ def test_linear_weight_grad(asme, dev, T, N, K):
     ref_b = dy.double().sum(0)
     assert _rel(w.grad, ref_w) < 1e-5 and _rel(b.grad, ref_b) < 1e-5
     assert _rel(xx.grad, dy.double() @ w.detach().double()) < 1e-5
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("nq,V", [(5, 37), (130, 1000), (300, 4099)])
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_catalog_rank_and_topk(asme, dev, d, nq, V, with_bias):
+    """Fused full-catalogue scoring vs materialised logits (torch fp32) + the reference rank rule."""
+    torch.manual_seed(d + nq + V)
+    H = torch.randn(nq, d, device=dev)
+    E = torch.randn(V, d, device=dev)
+    bias = torch.randn(V, device=dev) if with_bias else None
+    targets = torch.randint(0, V, (nq,), device=dev)
+    logits = H @ E.t() + (bias if bias is not None else 0)
+    t = logits.gather(1, targets[:, None])
+    ref_rank = 1 + (logits > t).sum(1)  # continuous random scores: no ties
+    ranks = asme.ops.catalog_rank(H, E, targets, bias)
+    # fused and materialised scores round differently: allow a one-place swap at near-equal scores
+    gap = (logits - t).abs()
+    near = ((gap < 1e-4 * logits.abs().max()) & (gap > 0)).sum(1)
+    assert ((ranks - ref_rank).abs() <= near).all()
+    assert (ranks == ref_rank).float().mean() > 0.97
+    k = 10 if V >= 10 else V
+    vals, idx = asme.ops.catalog_topk(H, E, k, bias)
+    ref_v, ref_i = torch.topk(logits, k, dim=1)
+    assert torch.allclose(vals, ref_v, rtol=1e-5, atol=1e-4)
+    assert (idx == ref_i).float().mean() > 0.97
+    # the returned scores are the fused scores of the returned items
+    assert torch.allclose(vals, logits.gather(1, idx), rtol=1e-5, atol=1e-4)
