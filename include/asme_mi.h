@@ -236,6 +236,25 @@ int asme_catalog_count_above(const float* H, int64_t ld_h, int64_t nq, int64_t d
                              int64_t V_local, const float* bias, const int64_t* targets, const float* tscore,
                              int64_t id_stride, int64_t id_offset, int32_t* counts, void* stream);
 
+
+/* ---- Deterministic table gradient (csrc/sharding.hip; SURVEY §8b embedding_scatter_add_bwd
+ * mode=deterministic; reference: autograd embedding_dense_backward).  Occurrences grouped per unique row
+ * by a stable radix sort, then ordered sums: bit-reproducible, no atomics, no zero fill. */
+int64_t asme_occurrence_csr_workspace(int64_t n);
+/* inverse (n int64 slots < cap) -> order (n int32 occurrences grouped by slot, increasing within a slot),
+ * sorted_slot (n int32, slot of order[i]), seg_off (cap + 1 int32) */
+int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap, void* workspace, int64_t workspace_bytes,
+                        int32_t* order, int32_t* sorted_slot, int32_t* seg_off, void* stream);
+int64_t asme_table_grad_workspace(int64_t n, int64_t dim);
+/* grad_rows[s] = out_scale * sum over slot s's occurrences of contribution rows, fixed summation order
+ * (32-occurrence chunks, then chunk partials in order); contribution k covers flat occurrences
+ * [c_off[k], c_off[k]+c_n[k]) with row t = c_rows[k][t] (* c_scale[k][t]); <= 4, host arrays */
+int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, const int32_t* seg_off,
+                           const int32_t* count, int64_t n, int64_t cap, int64_t dim, int n_contrib,
+                           const int64_t* c_off, const int64_t* c_n, const float* const* c_rows,
+                           const float* const* c_scale, float out_scale, void* workspace, int64_t workspace_bytes,
+                           float* grad_rows, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,10 @@ SIGNATURES = {
     "asme_residual_ln_fwd": [p, p, i64, i64, f32, u64, f32, u64, p, p, f32, p, p, p, p],
     "asme_residual_ln_bwd": [p, i64, i64, f32, u64, f32, u64, p, p, p, p, p, p, p, i64, p],
     "asme_attention_set_mode": [i32],
+    "asme_occurrence_csr_workspace": [i64],
+    "asme_occurrence_csr": [p, i64, i64, p, i64, p, p, p, p],
+    "asme_table_grad_workspace": [i64, i64],
+    "asme_table_grad_reduce": [p, p, p, p, i64, i64, i64, i32, p, p, p, p, f32, p, i64, p, p],
     "asme_catalog_rank": [p, i64, i64, i64, p, i64, i64, p, p, p, p, p],
     "asme_catalog_topk_workspace": [i64, i64, i64],
     "asme_catalog_topk": [p, i64, i64, i64, p, i64, i64, p, i64, i64, i64, p, i64, p, p, p],
@@ -74,7 +78,8 @@ SIGNATURES = {
 _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64,
              "asme_linear_weight_grad_workspace": ctypes.c_int64,
              "asme_attention_dropout_mask_bytes": ctypes.c_int64, "asme_linear_partials_rows": ctypes.c_int64,
-             "asme_catalog_topk_workspace": ctypes.c_int64}
+             "asme_catalog_topk_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
+             "asme_table_grad_workspace": ctypes.c_int64}
 
 _lib: Optional[ctypes.CDLL] = None
 

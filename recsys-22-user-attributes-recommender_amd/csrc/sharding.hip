@@ -128,3 +128,244 @@ ASME_API int asme_owner_histogram(const int64_t* unique, const int32_t* count, i
                        world, owner, counts);
     ASME_LAUNCH_CHECK("asme_owner_histogram");
 }
+
+// ---------------------------------------------------------------------------------------------------
+// Deterministic table gradient (SURVEY §8b `embedding_scatter_add_bwd(..., mode=deterministic)`, A19).
+// Reference: autograd's embedding_dense_backward sums every occurrence's gradient row into the table
+// row.  Here the step's occurrences (the dedup inverse, slot per occurrence) are grouped by slot with a
+// stable radix sort (slot, occurrence) -> per-slot lists in increasing occurrence order; each unique
+// row's gradient is then the ordered sum over its list (no atomics: bit-reproducible run to run, and
+// the compact gradient buffer needs no zero fill).
+namespace {
+
+// occurrences without a slot (inverse -1: id outside the table) get the sentinel key cap: sorted last
+__global__ void csr_prep_kernel(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
+                                int32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t k = inverse[i];
+    keys[i] = (int32_t)(k >= 0 && k < cap ? k : cap);
+    vals[i] = (int32_t)i;
+}
+
+// seg_off[k] = first sorted position of slot k, seg_off[last + 1] = end of the last slot's list
+__global__ void csr_bounds_kernel(const int32_t* __restrict__ keys, int64_t n, int64_t cap,
+                                  int32_t* __restrict__ seg_off) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t k = keys[i];
+    if (i == 0 || keys[i - 1] != k) {
+        if (k < cap) seg_off[k] = (int32_t)i;
+        if (i > 0 && keys[i - 1] < cap) seg_off[keys[i - 1] + 1] = (int32_t)i;
+    }
+    if (i == n - 1 && k < cap) seg_off[k + 1] = (int32_t)n;
+}
+
+constexpr int kMaxContrib = 4;
+constexpr int kChunk = 32;  // occurrences per reduction group: bounds the serial work of any group
+
+struct Contribs {
+    int64_t off[kMaxContrib];       // first flat occurrence index of the contribution
+    int64_t n[kMaxContrib];         // occurrences covered
+    const float* rows[kMaxContrib]; // (n, dim): the rows themselves, or h for scaled contributions
+    const float* scale[kMaxContrib];// nullable: contribution t = scale[t] * rows[t]
+    int count;
+};
+
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+    a.x += b.x;
+    a.y += b.y;
+    a.z += b.z;
+    a.w += b.w;
+}
+
+__device__ __forceinline__ float4 scale4(const float4& a, float s) {
+    return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
+}
+
+// Pass 1: one 32-lane group per chunk of kChunk consecutive sorted occurrences (float4 per lane).  A slot
+// whose occurrence list lies inside the chunk gets its final row; the list cut by the chunk's start is
+// left in head[chunk], the list cut by its end in tail[chunk] (a chunk inside one list: head).  Each lane
+// first resolves one occurrence (slot, source row, scale: coalesced loads) into LDS; the group then walks
+// the chunk with eight row gathers in flight.
+constexpr int kChunkGroups = 8;  // 32-lane groups per 256-thread block
+__global__ __launch_bounds__(256) void grad_chunk_kernel(const int32_t* __restrict__ order,
+                                                         const int32_t* __restrict__ slot,
+                                                         const int32_t* __restrict__ seg_off, int64_t n,
+                                                         int64_t cap, int dim, Contribs C, float out_scale,
+                                                         float* __restrict__ grad_rows, float* __restrict__ head,
+                                                         float* __restrict__ tail) {
+    __shared__ int32_t s_slot[kChunkGroups][kChunk];
+    __shared__ const float* s_src[kChunkGroups][kChunk];
+    __shared__ float s_sc[kChunkGroups][kChunk];
+    const int lane = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int64_t c = (int64_t)blockIdx.x * kChunkGroups + g;
+    const int64_t i0 = c * kChunk;
+    const int64_t i1 = i0 + kChunk < n ? i0 + kChunk : n;
+    {
+        const int64_t i = i0 + lane;
+        int32_t sl = -1;
+        const float* src = nullptr;
+        float sc = 1.f;
+        if (i < i1) {
+            const int32_t k = slot[i];
+            if (k < cap) {
+                sl = k;
+                const int64_t o = order[i];
+                const float* sp = nullptr;
+                int64_t t = 0;
+#pragma unroll
+                for (int q = 0; q < kMaxContrib; ++q)  // constant indices: the table stays in SGPRs
+                    if (q < C.count && o >= C.off[q] && o < C.off[q] + C.n[q]) {
+                        t = o - C.off[q];
+                        src = C.rows[q] + t * dim;
+                        sp = C.scale[q];
+                    }
+                if (sp) sc = sp[t];
+            }
+        }
+        s_slot[g][lane] = sl;
+        s_src[g][lane] = src;
+        s_sc[g][lane] = sc;
+    }
+    __syncthreads();
+    if (i0 >= n) return;
+    const int32_t first = s_slot[g][0];
+    if (first < 0) return;  // only slot-less occurrences from here on
+    const int cnt = (int)(i1 - i0);
+    for (int c0 = 4 * lane; c0 < dim; c0 += 128) {
+        int32_t cur = first;
+        bool started = seg_off[cur] == i0;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto flush = [&](bool ended) {
+            if (started && ended)
+                *reinterpret_cast<float4*>(grad_rows + (int64_t)cur * dim + c0) = scale4(acc, out_scale);
+            else
+                *reinterpret_cast<float4*>((started ? tail : head) + c * dim + c0) = acc;
+        };
+        for (int j0 = 0; j0 < cnt; j0 += 8) {
+            int32_t sl[8];
+            float4 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {  // eight gathers before the dependent adds
+                const int j = j0 + q;
+                sl[q] = j < cnt ? s_slot[g][j] : -1;
+                const float* src = j < cnt ? s_src[g][j] : nullptr;
+                v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (sl[q] >= 0 && src) v[q] = scale4(*reinterpret_cast<const float4*>(src + c0), s_sc[g][j]);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (sl[q] < 0) break;
+                if (sl[q] != cur) {
+                    flush(true);
+                    cur = sl[q];
+                    started = true;
+                    acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                add4(acc, v[q]);
+            }
+        }
+        flush(seg_off[cur + 1] <= i1);
+    }
+}
+
+// Pass 2: slots whose list spans chunks: tail of the first chunk + heads of the following ones, in order.
+__global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restrict__ seg_off,
+                                                        const int32_t* __restrict__ count, int64_t cap, int dim,
+                                                        float out_scale, const float* __restrict__ head,
+                                                        const float* __restrict__ tail,
+                                                        float* __restrict__ grad_rows) {
+    const int lane = threadIdx.x & 31;
+    const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
+    if (s >= cap || s >= *count) return;
+    const int64_t cf = seg_off[s] / kChunk, cl = (seg_off[s + 1] - 1) / kChunk;
+    if (cf == cl) return;
+    for (int c0 = 4 * lane; c0 < dim; c0 += 128) {
+        float4 acc = *reinterpret_cast<const float4*>(tail + cf * dim + c0);
+        for (int64_t k = cf + 1; k <= cl; ++k) add4(acc, *reinterpret_cast<const float4*>(head + k * dim + c0));
+        *reinterpret_cast<float4*>(grad_rows + s * dim + c0) = scale4(acc, out_scale);
+    }
+}
+
+int end_bit_for(int64_t cap) {
+    int b = 1;
+    while (((int64_t)1 << b) < cap + 1 && b < 31) ++b;
+    return b;
+}
+
+}  // namespace
+
+ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
+    size_t temp = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 31);
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    return (int64_t)(2 * up((size_t)n * sizeof(int32_t)) + up(temp));
+}
+
+// inverse (n int64 slots < cap) -> order (n int32 occurrence indices grouped by slot, increasing within a
+// slot), sorted_slot (n int32: the slot of order[i]) and seg_off (cap + 1 int32; entries beyond the number
+// of slots + 1 are left untouched)
+ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap, void* workspace,
+                                 int64_t workspace_bytes, int32_t* order, int32_t* sorted_slot, int32_t* seg_off,
+                                 void* stream) {
+    ASME_CHECK_ARG(inverse && workspace && order && sorted_slot && seg_off, "asme_occurrence_csr: null pointer");
+    ASME_CHECK_ARG(n >= 1 && n < (int64_t)1 << 31 && cap < (int64_t)1 << 31, "asme_occurrence_csr: bad size");
+    ASME_CHECK_ARG(workspace_bytes >= asme_occurrence_csr_workspace(n), "asme_occurrence_csr: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    char* ws = (char*)workspace;
+    int32_t* keys = (int32_t*)ws;
+    int32_t* vals = (int32_t*)(ws + up((size_t)n * 4));
+    void* temp = ws + 2 * up((size_t)n * 4);
+    size_t temp_bytes = (size_t)workspace_bytes - 2 * up((size_t)n * 4);
+    hipLaunchKernelGGL(csr_prep_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, keys, vals);
+    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, sorted_slot, vals, order, (int)n, 0,
+                                           end_bit_for(cap), s) != hipSuccess)
+        return hip_status(hipErrorUnknown, "asme_occurrence_csr: sort");
+    hipLaunchKernelGGL(csr_bounds_kernel, dim3(nblk(n)), dim3(256), 0, s, sorted_slot, n, cap, seg_off);
+    ASME_LAUNCH_CHECK("asme_occurrence_csr");
+}
+
+ASME_API int64_t asme_table_grad_workspace(int64_t n, int64_t dim) {
+    return 2 * ((n + kChunk - 1) / kChunk) * dim * (int64_t)sizeof(float);
+}
+
+// grad_rows[s] = out_scale * sum over slot s's occurrences of their contribution rows, in a fixed order
+// (chunks of 32 sorted occurrences, then chunk partials in order: bit-reproducible).  Contribution k covers
+// flat occurrences [c_off[k], c_off[k] + c_n[k]): row t = c_rows[k][t] (* c_scale[k][t]).  Host arrays of at
+// most 4 contributions, sorted by c_off and disjoint; dim % 4 == 0.  Rows of slots >= *count are untouched.
+ASME_API int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, const int32_t* seg_off,
+                                    const int32_t* count, int64_t n, int64_t cap, int64_t dim, int n_contrib,
+                                    const int64_t* c_off, const int64_t* c_n, const float* const* c_rows,
+                                    const float* const* c_scale, float out_scale, void* workspace,
+                                    int64_t workspace_bytes, float* grad_rows, void* stream) {
+    ASME_CHECK_ARG(order && sorted_slot && seg_off && count && grad_rows && c_off && c_n && c_rows,
+                   "asme_table_grad_reduce: null");
+    ASME_CHECK_ARG(n_contrib >= 1 && n_contrib <= kMaxContrib, "asme_table_grad_reduce: 1..4 contributions");
+    ASME_CHECK_ARG(dim > 0 && dim % 4 == 0 && ((uintptr_t)grad_rows & 15) == 0,
+                   "asme_table_grad_reduce: dim % 4 == 0, 16-B aligned rows");
+    ASME_CHECK_ARG(workspace_bytes >= asme_table_grad_workspace(n, dim) && (workspace || n == 0),
+                   "asme_table_grad_reduce: workspace too small");
+    Contribs C{};
+    C.count = n_contrib;
+    for (int k = 0; k < n_contrib; ++k) {
+        C.off[k] = c_off[k];
+        C.n[k] = c_n[k];
+        C.rows[k] = c_rows[k];
+        C.scale[k] = c_scale ? c_scale[k] : nullptr;
+        ASME_CHECK_ARG(c_rows[k] && ((uintptr_t)c_rows[k] & 15) == 0, "asme_table_grad_reduce: rows 16-B aligned");
+        ASME_CHECK_ARG(k == 0 || c_off[k] >= c_off[k - 1] + c_n[k - 1], "asme_table_grad_reduce: sorted, disjoint");
+    }
+    if (n == 0 || cap == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t nchunks = (n + kChunk - 1) / kChunk;
+    float* head = (float*)workspace;
+    float* tail = head + nchunks * dim;
+    hipLaunchKernelGGL(grad_chunk_kernel, dim3((unsigned)((nchunks + kChunkGroups - 1) / kChunkGroups)), dim3(256), 0, s, order,
+                       sorted_slot, seg_off, n, cap, (int)dim, C, out_scale, grad_rows, head, tail);
+    hipLaunchKernelGGL(grad_span_kernel, dim3((unsigned)((cap * 32 + 255) / 256)), dim3(256), 0, s, seg_off, count,
+                       cap, (int)dim, out_scale, head, tail, grad_rows);
+    ASME_LAUNCH_CHECK("asme_table_grad_reduce");
+}

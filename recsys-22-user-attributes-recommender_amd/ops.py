@@ -9,6 +9,7 @@ kernels derive the mask from (seed, element index) with Philox, so the backward 
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -18,6 +19,7 @@ import torch
 from . import _lib
 from ._lib import call, ptr, stream
 
+ctypes_i64, ctypes_vp = ctypes.c_int64, ctypes.c_void_p
 _N_PARTIALS = 1024  # blocks (and partial rows) used by the grid-stride backward reductions
 
 
@@ -117,10 +119,15 @@ class SparseTablePlan:
         self.capacity = n
         self._grad_rows = None
         self._inverse = {}
+        self._flat_inverse = inverse
+        self._offset = {}
+        self._contrib = []  # (flat offset, n, rows (n, d), scale (n,) or None) -- see add_rows / add_scaled
         off = 0
         for x in id_sets:
             k = x.numel()
-            self._inverse[x.data_ptr(), tuple(x.shape)] = inverse[off:off + k].view(x.shape)
+            key = (x.data_ptr(), tuple(x.shape))
+            self._inverse[key] = inverse[off:off + k].view(x.shape)
+            self._offset[key] = off
             off += k
         self.consumed = False
         tg = getattr(table, "_asme_table_grad", None) if table is not None else None
@@ -133,11 +140,67 @@ class SparseTablePlan:
         """dedup only (no table attached): unique ids in first-occurrence order + inverse per id set"""
         return cls(None, id_sets, slot_map, vocab=vocab, dim=0)
 
+    def add_rows(self, ids: torch.Tensor, rows: torch.Tensor):
+        """register the gradient rows (one per occurrence of the registered id set `ids`) of this step;
+        summed per unique row, in occurrence order, when grad_rows is first read"""
+        self._add(ids, _f32(rows).reshape(ids.numel(), self.dim), None)
+
+    def add_scaled(self, ids: torch.Tensor, scale: torch.Tensor, rows: torch.Tensor):
+        """register scale[t] * rows[t] per occurrence t of `ids` (the sampled head: g_pos/g_neg * h)"""
+        self._add(ids, _f32(rows).reshape(ids.numel(), self.dim), _f32(scale).reshape(ids.numel()))
+
+    def _add(self, ids, rows, scale):
+        key = (ids.data_ptr(), tuple(ids.shape))
+        if key not in self._offset:
+            raise KeyError("ids were not registered with the sparse table plan of this step")
+        if self._grad_rows is not None:
+            raise RuntimeError("table gradient already materialised for this step")
+        self._contrib.append((self._offset[key], ids.numel(), rows, scale))
+
+    def _reduce_contributions(self) -> torch.Tensor:
+        """deterministic table gradient: occurrences grouped by row (stable radix sort), sums in a fixed
+        order (asme_occurrence_csr + asme_table_grad_reduce); no atomics, no zero fill"""
+        dev = self.unique.device
+        n, d = self.capacity, self.dim
+        if n == 0:
+            return torch.zeros(0, d, device=dev, dtype=torch.float32)
+        lib = _lib.load()
+        ws_bytes = int(lib.asme_occurrence_csr_workspace(n))
+        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+        order = torch.empty(n, device=dev, dtype=torch.int32)
+        slot = torch.empty(n, device=dev, dtype=torch.int32)
+        seg_off = torch.empty(n + 1, device=dev, dtype=torch.int32)
+        call("asme_occurrence_csr", ptr(self._flat_inverse), n, n, ptr(ws), ws_bytes, ptr(order), ptr(slot),
+             ptr(seg_off), stream())
+        part_bytes = int(lib.asme_table_grad_workspace(n, d))
+        parts = torch.empty(max(part_bytes, 4) // 4, device=dev, dtype=torch.float32)
+        out = torch.empty(n, d, device=dev, dtype=torch.float32)
+        contrib = sorted(self._contrib, key=lambda c: c[0])
+        for i in range(0, len(contrib), 4):
+            part = contrib[i:i + 4]
+            k = len(part)
+            offs = (ctypes_i64 * k)(*[c[0] for c in part])
+            ns = (ctypes_i64 * k)(*[c[1] for c in part])
+            rows = (ctypes_vp * k)(*[c[2].data_ptr() for c in part])
+            scales = (ctypes_vp * k)(*[(c[3].data_ptr() if c[3] is not None else None) for c in part])
+            dest = out if i == 0 else torch.empty_like(out)  # more than 4 contributions: add the rest
+            call("asme_table_grad_reduce", ptr(order), ptr(slot), ptr(seg_off), ptr(self.count), n, n, d, k, offs,
+                 ns, rows, scales, 1.0, ptr(parts), part_bytes, ptr(dest), stream())
+            if i:
+                out += dest
+        self._contrib = []
+        return out
+
     @property
     def grad_rows(self) -> torch.Tensor:
-        """compact (capacity, d) gradient rows, slot s <-> unique[s] (allocated on first use)"""
+        """compact (capacity, d) gradient rows, slot s <-> unique[s]: the ordered sums of the registered
+        contributions (add_rows / add_scaled), or a zeroed buffer for callers that scatter-add into it"""
         if self._grad_rows is None:
-            self._grad_rows = torch.zeros(self.capacity, self.dim, device=self.unique.device, dtype=torch.float32)
+            if self._contrib:
+                self._grad_rows = self._reduce_contributions()
+            else:
+                self._grad_rows = torch.zeros(self.capacity, self.dim, device=self.unique.device,
+                                              dtype=torch.float32)
         return self._grad_rows
 
     def n_unique(self) -> int:
@@ -207,9 +270,7 @@ class _EmbeddingFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             plan = spec.table_grad.plan if spec.table_grad is not None else None
             if plan is not None:
-                inv = plan.inverse_of(ids)
-                call("asme_scatter_add_rows", ptr(d_rows), ptr(inv), T, D, ptr(plan.grad_rows), plan.capacity, 1.0,
-                     stream())
+                plan.add_rows(ids, d_rows)
             else:
                 g_table = torch.zeros_like(table)
                 call("asme_scatter_add_rows", ptr(d_rows), ptr(ids), T, D, ptr(g_table), V, 1.0, stream())
@@ -524,9 +585,9 @@ class _SampledLogitsFn(torch.autograd.Function):
             # dH pass with the real table; the table contributions go to the compact rows
             call("asme_sampled_logits_bwd", ptr(h2), ptr(table), ptr(pos_ids), ptr(neg_ids), T, D, V, ptr(gp),
                  ptr(gn), ptr(dh), None, stream())
-            ip, ineg = plan.inverse_of(pos_ids), plan.inverse_of(neg_ids)
-            call("asme_sampled_logits_bwd", ptr(h2), ptr(plan.grad_rows), ptr(ip), ptr(ineg), T, D, plan.capacity,
-                 ptr(gp), ptr(gn), None, ptr(plan.grad_rows), stream())
+            # table rows: g_pos[t] * h[t] / g_neg[t] * h[t], summed per unique row by the plan (deterministic)
+            plan.add_scaled(pos_ids, gp, h2)
+            plan.add_scaled(neg_ids, gn, h2)
         else:
             if ctx.needs_input_grad[1]:
                 g_table = torch.zeros_like(table)

@@ -163,7 +163,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         recv = self.exchange.push_grads(st, g)
         shard = self.model.item_table()
         if len(st.recv_local):
-            ops.scatter_add_rows(recv, own.inverse_of(st.recv_local), own.grad_rows, 1.0 / W)
+            own.add_rows(st.recv_local, recv.mul_(1.0 / W))  # ordered per-row sums (deterministic)
         shard._asme_table_grad.plan = own
         dense = [p for p in self.model.parameters() if p is not shard and p.grad is not None]
         if dense and W > 1:

@@ -284,6 +284,46 @@ def test_sparse_table_plan_equals_dense(asme, dev):
     assert int((slot_map != -1).sum()) == 0  # map reset after the update
 
 
+@pytest.mark.parametrize("D", [32, 64, 128, 192])
+def test_deterministic_table_grad(asme, dev, D):
+    """Plan contributions (add_rows / add_scaled) -> ordered per-row sums: equal to the fp64 sum of every
+    occurrence's row, and bit-identical run to run.  A few hot ids (thousands of occurrences: lists spanning
+    many 32-occurrence chunks), a long tail, and out-of-range ids (no slot, no contribution)."""
+    torch.manual_seed(11 + D)
+    V, T = 5000, 3000
+    hot = torch.randint(0, 4, (T,), device=dev)
+    tail = torch.randint(0, V, (T,), device=dev)
+    pick = torch.rand(T, device=dev) < 0.6
+    ids = [torch.where(pick, hot, tail), torch.randint(0, V, (T,), device=dev), torch.randint(0, 50, (T,), device=dev)]
+    ids[1][::97] = V + 3  # invalid ids: inverse -1
+    rows = torch.randn(T, D, device=dev)
+    h = torch.randn(T, D, device=dev)
+    g1, g2 = torch.randn(T, device=dev), torch.randn(T, device=dev)
+
+    def run():
+        slot_map = torch.full((V,), -1, dtype=torch.int32, device=dev)
+        plan = asme.ops.SparseTablePlan(None, ids, slot_map, vocab=V, dim=D)
+        plan.add_rows(ids[0], rows)
+        plan.add_scaled(ids[1], g1, h)
+        plan.add_scaled(ids[2], g2, h)
+        U = plan.n_unique()
+        out = plan.grad_rows[:U].clone()
+        uniq = plan.unique[:U].clone()
+        plan.release()
+        return uniq, out
+
+    u0, a = run()
+    u1, b = run()
+    assert torch.equal(u0, u1)
+    assert torch.equal(a, b)  # bitwise reproducible
+    dense = torch.zeros(V + 8, D, device=dev, dtype=torch.float64)
+    dense.index_add_(0, ids[0], rows.double())
+    dense.index_add_(0, ids[1], (g1[:, None] * h).double())
+    dense.index_add_(0, ids[2], (g2[:, None] * h).double())
+    want = dense[u0]
+    assert (a.double() - want).abs().max().item() < 1e-4 * max(1.0, want.abs().max().item())
+
+
 def test_lazy_adam_bit_exact_vs_dense(asme, dev):
     """Exact catch-up: lazily replayed zero-gradient steps == the dense row update every step, bitwise."""
     torch.manual_seed(6)

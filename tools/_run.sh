@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python bench.py --cpu-baseline 0 > gpurun_out/b1.log 2>&1 && \
+timeout -k 10 300 python bench.py --cpu-baseline 0 --steps 30 > gpurun_out/b2.log 2>&1
