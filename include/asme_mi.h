@@ -255,6 +255,16 @@ int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, con
                            const float* const* c_scale, float out_scale, void* workspace, int64_t workspace_bytes,
                            float* grad_rows, void* stream);
 
+
+/* ---- Weight-stationary Linear GEMM (csrc/wsgemm.hip; transformer_layers.py:175-199, 212-220 nn.Linear and
+ * PositionwiseFeedForward).  One NB x K weight block resident in LDS per workgroup, X streamed from HBM into
+ * registers, deferred buffer-store epilogue.  epi: 0 store (+bias), 1 pre = C + bias -> pre_out and
+ * Y = dropout(GELU(pre)), 2 Y = C * keep * GELU'(pre_in); trans = 1: W is K x N (Y = X W).  Dropout as
+ * asme_gelu_dropout_fwd (salt 5, element m*N + n). */
+int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N);
+int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W, int64_t N, int trans, const float* bias,
+                   int epi, float* pre_out, const float* pre_in, float p, uint64_t seed, float* Y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

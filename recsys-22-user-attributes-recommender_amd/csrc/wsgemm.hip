@@ -1,0 +1,284 @@
+// Weight-stationary streaming GEMM for the token-major Linear layers, fp32 MFMA on gfx950.
+//
+// Reference semantics (paths relative to /root/reference/src/asme):
+//   nn.Linear projections         core/models/common/layers/transformer_layers.py:175-199 (Q,K,V,O)
+//   PositionwiseFeedForward       transformer_layers.py:212-220  W2(dropout(GELU_erf(W1 x)))
+// The shapes of the ASME transformer are tall and skinny: M = B*L tokens (2e5 at the bench shape) against
+// K, N <= 512.  So the kernel keeps one NB x K block of the weight in LDS for the workgroup's whole life
+// (loaded once; the hot loop has no barrier) and every wave streams its own 16-token tiles of X from HBM
+// straight into registers, kD k16 blocks in flight, while it multiplies the previous ones:
+//   C^T tile (NB features x 16 tokens) += W_blk (NB x 16 k) . X_tile^T (16 k x 16 tokens)
+// Lane (c16, g) of an MFMA supplies k = 4g..4g+3 of one 16-k block for its feature / token, so the X rows
+// are read as float4 (4 lanes = 64 contiguous bytes of a row) and the W block as conflict-free
+// ds_read_b128 (W image row r, 16-B slot s stored at slot s ^ (r & 15)).
+// Epilogue: a finished tile's accumulators (+ bias) move to a stash and are written by buffer stores
+// spread over the NEXT tile's k blocks, one 16-feature tile per block -- nothing overwrites a store's source
+// registers until a tile later (an LDS read or MFMA landing on them right after the store stalls the
+// wave until the store has left), and rows past M are dropped by the buffer range check.
+// Epilogues: WS_STORE       Y = C (+ bias)
+//            WS_GELU_DROP   pre = C + bias; Y = dropout(GELU(pre))            (FFN inner layer, forward)
+//            WS_GELU_BWD    Y = C * keep * GELU'(pre)                          (through the FFN activation)
+// Dropout decisions are exactly those of asme_gelu_dropout_fwd/bwd (norm.hip): element m*N + n, one
+// Philox block per 4 consecutive elements, salt 5.
+// Measured at M = 204800 (tools/probe/sgemm_probe.py, fp32 MFMA peak 157 TF/s): K=128 -> N=512 113 TF/s,
+// K=512 -> N=128 126 TF/s, vs hipBLASLt 93 / 96.
+#include "common.h"
+
+using namespace asme;
+
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32v4 __attribute__((ext_vector_type(4)));
+
+constexpr int kD = 8;               // k16 blocks of X in flight per wave
+constexpr int kWaves = 8;           // 512-thread workgroups, one per CU, two waves per SIMD
+constexpr uint32_t kDrop = 0x80000000u;  // >= every buffer's record count: the access is dropped / reads 0
+
+enum { WS_STORE = 0, WS_GELU_DROP = 1, WS_GELU_BWD = 2 };
+
+struct WsEpi {
+    const float* bias;   // [N] or null
+    float* pre_out;      // WS_GELU_DROP: pre-activation out
+    const float* pre_in; // WS_GELU_BWD: pre-activation in
+    float p;             // dropout probability (0: none)
+    uint64_t seed;
+};
+
+__device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s ^ (r & 15)); }
+__device__ __forceinline__ void bstore(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const u32v4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 0);
+}
+__device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const u32v4 u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// X: M x K row-major.  TRANS = false: W is N x K (nn.Linear.weight), Y = X W^T.  TRANS = true: W is K x N
+// (the input gradient dX = dY W of a layer whose weight is N_out x N_in = K x N).
+template <int K, int CT, bool TRANS, int EPI>
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ws_gemm_kernel(
+    const float* __restrict__ X, int64_t M, const float* __restrict__ W, int N, float* __restrict__ Y, WsEpi ep) {
+    constexpr int NB = 16 * CT;  // output features per workgroup
+    constexpr int K4 = K / 4;
+    constexpr int NKB = K / 16;
+    static_assert(NKB % kD == 0, "the ring depth must divide the k16 blocks of a tile");
+    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    const int nblk = N / NB;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
+    const int wg_per_nb = per_xcd / nblk;  // the workgroups of one XCD split over the feature blocks
+    if (slot >= wg_per_nb * nblk) return;
+    const int nb = slot % nblk;
+    const int n0 = nb * NB;
+    // ---- the W block, once
+    if (!TRANS) {
+        for (int i = threadIdx.x; i < NB * K4; i += kWaves * 64) {
+            const int r = i / K4, s = i % K4;
+            lds4[wslot(r, s, K4)] = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + 4 * s);
+        }
+    } else {  // block element (r, k) = W[k][n0 + r]: lanes read consecutive r (coalesced)
+        float* l = reinterpret_cast<float*>(lds4);
+        for (int i = threadIdx.x; i < NB * K; i += kWaves * 64) {
+            const int r = i % NB, k = i / NB;
+            l[wslot(r, k >> 2, K4) * 4 + (k & 3)] = W[(int64_t)k * N + n0 + r];
+        }
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+    // ---- 16-token tiles of this (XCD, feature block): contiguous per XCD, strided over its waves
+    const int64_t ntile = (M + 15) / 16;
+    const int64_t lo = ntile * xcd / 8, hi = ntile * (xcd + 1) / 8;
+    const int wcount = wg_per_nb * kWaves;
+    const int widx = (slot / nblk) * kWaves + wave;
+    const int64_t my_tiles = hi - lo > widx ? (hi - lo - widx + wcount - 1) / wcount : 0;
+    if (my_tiles == 0) return;
+    const int64_t t0 = lo + widx;
+    auto xrow = [&](int64_t j) -> const float* {  // clamped rows are computed and dropped at the store
+        int64_t m = (t0 + (j < my_tiles ? j : my_tiles - 1) * wcount) * 16 + c16;
+        return X + (m < M ? m : M - 1) * K + 4 * g;
+    };
+    const __amdgpu_buffer_rsrc_t yr = rsrc(Y, M * N * 4);
+    const __amdgpu_buffer_rsrc_t pr = rsrc(EPI == WS_GELU_DROP ? (const void*)ep.pre_out : (const void*)ep.pre_in,
+                                           EPI == WS_STORE ? 0 : M * N * 4);
+    float4 breg[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+        breg[ct] = ep.bias ? *reinterpret_cast<const float4*>(ep.bias + n0 + ct * 16 + 4 * g)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float keep_k = ep.p > 0.f ? 1.f / (1.f - ep.p) : 1.f;
+    const float* rc = xrow(0);
+    const float* rn = xrow(1);
+    float4 ring[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) {
+        ring[d] = *reinterpret_cast<const float4*>(rc + d * 16);
+        __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's vmcnt waits assume it
+    }
+    float4 stash[CT], pre[CT];
+    uint32_t soff = kDrop;  // byte offset of (row, n0 + 4g) of the stashed tile in Y
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) stash[ct] = pre[ct] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 wc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) wc[ct] = lds4[wslot(ct * 16 + c16, g, K4)];
+    // the stashed tile's epilogue for one 16-feature tile
+    auto epilogue = [&](int ct) {
+        const uint32_t off = soff + ct * 64;
+        float4 v = stash[ct];
+        if constexpr (EPI == WS_STORE) {
+            bstore(v, yr, off);
+        } else {
+            float u[4] = {1.f, 1.f, 1.f, 1.f};
+            if (ep.p > 0.f) {
+                philox_uniform4(ep.seed, 5u, off >> 4, u);  // element index (off / 4), 4 per Philox block
+#pragma unroll
+                for (int i = 0; i < 4; ++i) u[i] = u[i] >= ep.p ? keep_k : 0.f;
+            }
+            if constexpr (EPI == WS_GELU_DROP) {
+                bstore(v, pr, off);
+                v = make_float4(gelu_erf(v.x) * u[0], gelu_erf(v.y) * u[1], gelu_erf(v.z) * u[2],
+                                gelu_erf(v.w) * u[3]);
+            } else {
+                const float4 x = pre[ct];
+                v = make_float4(v.x * u[0] * gelu_erf_grad(x.x), v.y * u[1] * gelu_erf_grad(x.y),
+                                v.z * u[2] * gelu_erf_grad(x.z), v.w * u[3] * gelu_erf_grad(x.w));
+            }
+            bstore(v, yr, off);
+        }
+    };
+    floatx4 acc[CT];
+    for (int64_t j = 0; j < my_tiles; ++j) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            const int kbn = kb + 1 == NKB ? 0 : kb + 1;
+            float4 wn[CT];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) wn[ct] = lds4[wslot(ct * 16 + c16, kbn * 4 + g, K4)];
+            __builtin_amdgcn_sched_barrier(0);  // the next block's W reads go out ahead of this block's MFMAs
+            const int d = kb % kD;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].x, ring[d].x, acc[ct]);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].y, ring[d].y, acc[ct]);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].z, ring[d].z, acc[ct]);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].w, ring[d].w, acc[ct]);
+            // refill the slot just consumed: block kb + kD of this tile or of the next one (unconditional,
+            // so the vmcnt bookkeeping stays exact; past the last tile it re-reads the last one)
+            ring[d] = *reinterpret_cast<const float4*>((kb + kD < NKB ? rc : rn) + ((kb + kD) % NKB) * 16);
+            // the previous tile's epilogue, one 16-feature tile per block (late in the tile, so the
+            // pre-activation loads WS_GELU_BWD issued at the tile boundary have landed)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+                if ((ct + 1) * NKB / CT - 1 == kb) epilogue(ct);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) wc[ct] = wn[ct];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // tile done: to the stash (written during the next tile)
+        const int64_t m = (t0 + j * wcount) * 16 + c16;
+        soff = m < M ? (uint32_t)((m * N + n0 + 4 * g) * 4) : kDrop;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            stash[ct] = make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
+                                    acc[ct][3] + breg[ct].w);
+            if constexpr (EPI == WS_GELU_BWD) pre[ct] = bload(pr, soff + ct * 64);
+        }
+        rc = rn;
+        rn = xrow(j + 2);
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) epilogue(ct);  // the last tile
+}
+
+template <int K, int CT, bool TRANS, int EPI>
+int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
+    const size_t lds = (size_t)16 * CT * K * 4;
+    static bool attr = false;  // opt in above 64 KiB of dynamic LDS once per instantiation
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return hip_status(e, "asme_ws_linear: LDS opt-in");
+        attr = true;
+    }
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M, W,
+                       N, Y, ep);
+    return hip_status(hipGetLastError(), "asme_ws_linear");
+}
+
+// features per workgroup: 64, or 96 when N / 64 does not divide the 32 workgroups of an XCD (N = 384)
+int pick_ct(int N) {
+    if (N % 64 == 0 && 32 % (N / 64) == 0) return 4;
+    if (N % 96 == 0 && 32 % (N / 96) == 0) return 6;
+    return 0;
+}
+
+template <int K, bool TRANS, int EPI>
+int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
+    if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
+    return launch_ws<K, 6, TRANS, EPI>(X, M, W, N, Y, ep, s);
+}
+
+template <bool TRANS, int EPI>
+int dispatch_k(int K, int ct, const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep,
+               hipStream_t s) {
+    switch (K) {
+        case 128: return dispatch_ct<128, TRANS, EPI>(ct, X, M, W, N, Y, ep, s);
+        case 256: return dispatch_ct<256, TRANS, EPI>(ct, X, M, W, N, Y, ep, s);
+        case 384: return dispatch_ct<384, TRANS, EPI>(ct, X, M, W, N, Y, ep, s);
+        default: return dispatch_ct<512, TRANS, EPI>(ct, X, M, W, N, Y, ep, s);
+    }
+}
+
+}  // namespace
+
+// 1 when (M, K, N) is a shape the weight-stationary kernel takes: K in {128, 256, 384, 512}, N a multiple of
+// 64 (or 96) that splits the 32 workgroups of an XCD, the W block within 128 KiB of LDS, Y < 2 GiB.
+ASME_API int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N) {
+    if (M <= 0 || (K != 128 && K != 256 && K != 384 && K != 512)) return 0;
+    const int ct = pick_ct((int)N);
+    if (ct == 0 || N > 4096) return 0;
+    if ((int64_t)16 * ct * K * 4 > 128 * 1024) return 0;
+    if (M * N * 4 >= (int64_t)kDrop || M * K * 4 >= ((int64_t)1 << 40)) return 0;
+    return 1;
+}
+
+// Y (M x N) = X (M x K) . W^T (+ bias) with epilogue `epi` (0 store, 1 GELU + dropout with the
+// pre-activation in pre_out, 2 GELU backward with the pre-activation pre_in); trans = 1: W is K x N and
+// Y = X . W (the input gradient of a Linear with weight W).  Rows of X, Y, pre: contiguous, 16-B aligned.
+ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W, int64_t N, int trans,
+                            const float* bias, int epi, float* pre_out, const float* pre_in, float p, uint64_t seed,
+                            float* Y, void* stream) {
+    ASME_CHECK_ARG(X && W && Y, "asme_ws_linear: null pointer");
+    ASME_CHECK_ARG(asme_ws_linear_supported(M, K, N), "asme_ws_linear: unsupported shape");
+    ASME_CHECK_ARG(epi >= 0 && epi <= 2, "asme_ws_linear: bad epilogue");
+    ASME_CHECK_ARG(epi != 1 || pre_out, "asme_ws_linear: GELU forward needs pre_out");
+    ASME_CHECK_ARG(epi != 2 || pre_in, "asme_ws_linear: GELU backward needs pre_in");
+    ASME_CHECK_ARG(((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 15) == 0 && ((uintptr_t)W & 15) == 0,
+                   "asme_ws_linear: 16-B alignment");
+    ASME_CHECK_ARG(p >= 0.f && p < 1.f, "asme_ws_linear: dropout probability in [0, 1)");
+    const WsEpi ep{bias, pre_out, pre_in, p, seed};
+    const int ct = pick_ct((int)N);
+    hipStream_t s = (hipStream_t)stream;
+    if (trans) {
+        if (epi == 0) return dispatch_k<true, WS_STORE>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+        if (epi == 1) return dispatch_k<true, WS_GELU_DROP>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+        return dispatch_k<true, WS_GELU_BWD>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+    }
+    if (epi == 0) return dispatch_k<false, WS_STORE>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+    if (epi == 1) return dispatch_k<false, WS_GELU_DROP>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+    return dispatch_k<false, WS_GELU_BWD>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+}

@@ -260,9 +260,7 @@ class TransformerLayer(nn.Module):
             o = ops.attention(qkv, key_valid, att.heads, causal, _p(att.dropout, tr))
             a = ops.linear(o, att.output_linear.weight, att.output_linear.bias)
             h1, ln2 = ops.residual_ln(x, a, blk.output_sublayer.norm, _p(blk.input_sublayer.dropout, tr), 0.0)
-            f = ops.linear(ln2, ff.w_1.weight, ff.w_1.bias)
-            g = ops.gelu_dropout(f, _p(ff.dropout, tr))
-            f2 = ops.linear(g, ff.w_2.weight, ff.w_2.bias)
+            f2 = ops.ffn(ln2, ff.w_1.weight, ff.w_1.bias, ff.w_2.weight, ff.w_2.bias, _p(ff.dropout, tr))
             nxt = blocks[i + 1].input_sublayer.norm if i + 1 < len(blocks) else None
             x, ln = ops.residual_ln(h1, f2, nxt, _p(blk.output_sublayer.dropout, tr), _p(blk.dropout, tr))
         return x

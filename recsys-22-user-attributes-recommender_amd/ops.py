@@ -351,42 +351,127 @@ def gather_sum(ids, table, bias=None, skip_zero=False):
 
 
 # ------------------------------------------------------------------------------------ linear
+_WS_SUPPORTED = {}
+
+
+def _ws_ok(M: int, K: int, N: int) -> bool:
+    """(M, K, N) runs on the weight-stationary MFMA GEMM (csrc/wsgemm.hip)"""
+    key = (M, K, N)
+    if key not in _WS_SUPPORTED:
+        _WS_SUPPORTED[key] = bool(_lib.load().asme_ws_linear_supported(M, K, N))
+    return _WS_SUPPORTED[key]
+
+
+def _ws(x2, w, N: int, trans: int, bias=None, epi: int = 0, pre_out=None, pre_in=None, p: float = 0.0,
+        seed: int = 0):
+    """Y = x2 . w^T (+ bias) (trans = 0, w: N x K) or x2 . w (trans = 1, w: K x N) with epilogue epi"""
+    M, K = x2.shape
+    y = torch.empty(M, N, device=x2.device, dtype=torch.float32)
+    call("asme_ws_linear", ptr(x2), M, K, ptr(w), N, trans, ptr(bias), epi, ptr(pre_out), ptr(pre_in), p, seed,
+         ptr(y), stream())
+    return y
+
+
+def _weight_grad(dy2, x2, has_bias: bool):
+    """dW = dY^T X, db = sum_t dY on the split-token MFMA kernel (asme_linear_weight_grad)"""
+    dy2, x2 = _f32(dy2), _f32(x2)
+    T, N = dy2.shape
+    K = x2.shape[1]
+    if N % 4 or K % 4:  # shapes the kernel does not tile: library GEMM
+        return dy2.t() @ x2, (dy2.sum(0) if has_bias else None)
+    nbytes = int(_lib.load().asme_linear_weight_grad_workspace(T, N, K))
+    ws = torch.empty(max(4, nbytes // 4), device=dy2.device, dtype=torch.float32)
+    dw = torch.empty(N, K, device=dy2.device, dtype=torch.float32)
+    db = torch.empty(N, device=dy2.device, dtype=torch.float32) if has_bias else None
+    call("asme_linear_weight_grad", ptr(dy2), N, ptr(x2), K, T, N, K, ptr(ws), nbytes, ptr(dw), ptr(db), 0, stream())
+    return dw, db
+
+
+def _linear_fwd(x2, w, b):
+    M, K = x2.shape
+    N = w.shape[0]
+    if _ws_ok(M, K, N) and w.is_contiguous() and (b is None or b.is_contiguous()):
+        return _ws(x2, w, N, 0, bias=b)
+    return torch.nn.functional.linear(x2, w, b)
+
+
+def _linear_dx(dy2, w):
+    M, N = dy2.shape
+    K = w.shape[1]
+    if _ws_ok(M, N, K) and w.is_contiguous():
+        return _ws(dy2, w, K, 1)
+    return dy2 @ w
+
+
 class _LinearFn(torch.autograd.Function):
-    """nn.Linear with the weight/bias gradient on the split-token MFMA kernel (asme_linear_weight_grad);
-    the forward and the input gradient are plain library GEMMs (hipBLASLt)."""
+    """nn.Linear on the weight-stationary MFMA GEMM (forward and input gradient; library GEMM for shapes it
+    does not take) with the weight/bias gradient on the split-token MFMA kernel (asme_linear_weight_grad)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
+        N, K = w.shape
+        x2 = _f32(x).reshape(-1, K)
+        ctx.save_for_backward(x2, w)
         ctx.has_bias = b is not None
-        return torch.nn.functional.linear(x, w, b)
+        ctx.xshape = x.shape
+        return _linear_fwd(x2, w, b).view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x2, w = ctx.saved_tensors
         N, K = w.shape
-        dy2 = dy.reshape(-1, N)
-        x2 = x.reshape(-1, K)
-        dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dy2 = _f32(dy).reshape(-1, N)
+        dx = _linear_dx(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = db = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dy2, x2 = _f32(dy2), _f32(x2)
-            if N % 4 == 0 and K % 4 == 0:
-                T = x2.shape[0]
-                nbytes = int(_lib.load().asme_linear_weight_grad_workspace(T, N, K))
-                ws = torch.empty(max(4, nbytes // 4), device=x.device, dtype=torch.float32)
-                dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
-                db = torch.empty(N, device=x.device, dtype=torch.float32) if ctx.has_bias else None
-                call("asme_linear_weight_grad", ptr(dy2), N, ptr(x2), K, T, N, K, ptr(ws), nbytes, ptr(dw), ptr(db),
-                     0, stream())
-            else:  # shapes the kernel does not tile: library GEMM
-                dw = dy2.t() @ x2
-                db = dy2.sum(0) if ctx.has_bias else None
+            dw, db = _weight_grad(dy2, x2, ctx.has_bias)
         return dx, dw, db
 
 
 def linear(x, w, b=None):
     return _LinearFn.apply(x, w, b)
+
+
+class _FFNFn(torch.autograd.Function):
+    """PositionwiseFeedForward W2(dropout(GELU_erf(W1 x + b1))) + b2 (transformer_layers.py:212-220) with the
+    activation fused into the GEMMs: forward GEMM1 writes the pre-activation and dropout(GELU(.)); the backward
+    input-gradient GEMM of W2 applies keep * GELU'(pre) in its epilogue.  Same dropout decisions as
+    gelu_dropout (salt 5, element index over the (T, d_ff) activation)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, p: float):
+        F, D = w1.shape
+        x2 = _f32(x).reshape(-1, D)
+        M = x2.shape[0]
+        seed = new_seed(p)
+        pre = torch.empty(M, F, device=x.device, dtype=torch.float32)
+        g = _ws(x2, w1, F, 0, bias=b1, epi=1, pre_out=pre, p=p, seed=seed)
+        y = _linear_fwd(g, w2, b2)
+        ctx.save_for_backward(x2, pre, g, w1, w2)
+        ctx.meta = (p, seed, b1 is not None, b2 is not None, x.shape)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, pre, g, w1, w2 = ctx.saved_tensors
+        p, seed, hb1, hb2, xshape = ctx.meta
+        F, D = w1.shape
+        dy2 = _f32(dy).reshape(-1, D)
+        d_pre = _ws(dy2, w2, F, 1, epi=2, pre_in=pre, p=p, seed=seed)
+        dw2, db2 = _weight_grad(dy2, g, hb2)
+        dx = _linear_dx(d_pre, w1).view(xshape) if ctx.needs_input_grad[0] else None
+        dw1, db1 = _weight_grad(d_pre, x2, hb1)
+        return dx, dw1, db1, dw2, db2, None
+
+
+def ffn(x, w1, b1, w2, b2, p: float = 0.0):
+    """W2(dropout(GELU(W1 x + b1))) + b2; fused on the weight-stationary GEMM when the shapes allow"""
+    F, D = w1.shape
+    M = x.numel() // D
+    if (_ws_ok(M, D, F) and _ws_ok(M, F, D) and w1.is_contiguous() and w2.is_contiguous()
+            and b1 is not None and b1.is_contiguous()):
+        return _FFNFn.apply(x, w1, b1, w2, b2, p)
+    return linear(gelu_dropout(linear(x, w1, b1), p), w2, b2)
 
 
 # ------------------------------------------------------------------------------------ layer norm

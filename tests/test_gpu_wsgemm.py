@@ -1,0 +1,103 @@
+"""Weight-stationary Linear GEMM (csrc/wsgemm.hip) against fp64 references, its fused GELU/dropout
+epilogues against the standalone row kernels (bitwise), and the fused FFN autograd function against the
+per-op composition (transformer_layers.py:212-220)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _call(asme, x, w, N, trans, bias=None, epi=0, pre_out=None, pre_in=None, p=0.0, seed=0):
+    M, K = x.shape
+    y = torch.full((M, N), float("nan"), device=x.device)
+    L = asme._lib
+    L.call("asme_ws_linear", L.ptr(x), M, K, L.ptr(w), N, trans, L.ptr(bias), epi, L.ptr(pre_out), L.ptr(pre_in),
+           p, seed, L.ptr(y), L.stream())
+    return y
+
+
+@pytest.mark.parametrize("M", [1, 17, 1000, 4099, 65536 + 48])
+@pytest.mark.parametrize("K,N", [(128, 128), (128, 384), (128, 512), (512, 128), (384, 128), (256, 64)])
+def test_ws_linear_matches_fp64(asme, dev, M, K, N):
+    torch.manual_seed(M + K + N)
+    assert asme._lib.load().asme_ws_linear_supported(M, K, N) == 1
+    x = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) / K ** 0.5
+    b = torch.randn(N, device=dev)
+    y = _call(asme, x, w, N, 0, bias=b)
+    ref = x.double() @ w.double().t() + b.double()
+    assert torch.isfinite(y).all()
+    assert (y.double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+    # trans: W is K x N (the input gradient of a Linear with weight W)
+    wt = torch.randn(K, N, device=dev) / K ** 0.5
+    y = _call(asme, x, wt, N, 1)
+    ref = x.double() @ wt.double()
+    assert torch.isfinite(y).all()
+    assert (y.double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+
+
+def test_ws_linear_rejects_unsupported(asme):
+    lib = asme._lib.load()
+    assert lib.asme_ws_linear_supported(100, 100, 128) == 0      # K not tiled
+    assert lib.asme_ws_linear_supported(100, 128, 100) == 0      # N not a multiple of 64 / 96
+    assert lib.asme_ws_linear_supported(100, 512, 384) == 0      # W block over 128 KiB of LDS
+    assert lib.asme_ws_linear_supported(1 << 22, 128, 512) == 0  # Y over 2 GiB
+
+
+@pytest.mark.parametrize("p", [0.0, 0.2])
+@pytest.mark.parametrize("M", [333, 20000])
+def test_ws_gelu_epilogues_match_row_kernels(asme, dev, p, M):
+    torch.manual_seed(3)
+    D, Fd = 128, 512
+    L = asme._lib
+    x = torch.randn(M, D, device=dev)
+    w1 = torch.randn(Fd, D, device=dev) / D ** 0.5
+    b1 = torch.randn(Fd, device=dev)
+    seed = 987654321
+    pre = torch.empty(M, Fd, device=dev)
+    act = _call(asme, x, w1, Fd, 0, bias=b1, epi=1, pre_out=pre, p=p, seed=seed)
+    pre_ref = _call(asme, x, w1, Fd, 0, bias=b1)
+    assert torch.equal(pre, pre_ref)
+    act_ref = torch.empty_like(pre)
+    L.call("asme_gelu_dropout_fwd", L.ptr(pre), pre.numel(), p, seed, L.ptr(act_ref), L.stream())
+    assert torch.equal(act, act_ref)
+    # backward through the activation: (dY W2) * keep * GELU'(pre)
+    w2 = torch.randn(D, Fd, device=dev) / Fd ** 0.5
+    dy = torch.randn(M, D, device=dev)
+    d_pre = _call(asme, dy, w2, Fd, 1, epi=2, pre_in=pre, p=p, seed=seed)
+    dg = _call(asme, dy, w2, Fd, 1)
+    d_ref = torch.empty_like(pre)
+    L.call("asme_gelu_dropout_bwd", L.ptr(pre), L.ptr(dg), pre.numel(), p, seed, L.ptr(d_ref), L.stream())
+    assert torch.equal(d_pre, d_ref)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_fused_ffn_matches_composition(asme, dev, p):
+    torch.manual_seed(4)
+    B, L_, D, Fd = 3, 50, 128, 512
+    ff = torch.nn.ModuleDict({"w_1": torch.nn.Linear(D, Fd), "w_2": torch.nn.Linear(Fd, D)}).to(dev)
+    x = torch.randn(B, L_, D, device=dev)
+    outs = []
+    for fused in (True, False):
+        ff.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        torch.manual_seed(11)  # same dropout seed draw
+        if fused:
+            y = asme.ops.ffn(xx, ff["w_1"].weight, ff["w_1"].bias, ff["w_2"].weight, ff["w_2"].bias, p)
+        else:
+            h = asme.ops.gelu_dropout(asme.ops.linear(xx, ff["w_1"].weight, ff["w_1"].bias), p)
+            y = asme.ops.linear(h, ff["w_2"].weight, ff["w_2"].bias)
+        gy = torch.randn_like(y, generator=torch.Generator(device=dev).manual_seed(5))
+        (y * gy).sum().backward()
+        outs.append((y.detach(), xx.grad.clone(), [q.grad.clone() for q in ff.parameters()]))
+    (y1, dx1, g1), (y0, dx0, g0) = outs
+    assert torch.allclose(y1, y0, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(dx1, dx0, rtol=1e-5, atol=1e-5)
+    for a, b in zip(g1, g0):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-4)
+    if p == 0.0:  # against plain PyTorch fp32
+        ff.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        y = ff["w_2"](F.gelu(ff["w_1"](xx)))
+        assert torch.allclose(y1, y.detach(), rtol=1e-4, atol=1e-4)

@@ -1,5 +1,5 @@
 import ctypes, os, torch
-lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprobe.so"))
+lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("PROBE_LIB", "libprobe.so")))
 lib.run_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
 out = torch.empty(4096 * 256, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
