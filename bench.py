@@ -29,8 +29,8 @@ PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1024, help="sequences per GPU")
     ap.add_argument("--seq-len", type=int, default=200)
     ap.add_argument("--items", type=int, default=10_000_000)
@@ -143,7 +143,8 @@ def main():
     timer = asme._lib.KernelTimer(["asme_adam_rows_step", "asme_attention_fwd", "asme_attention_bwd",
                                    "asme_embedding_fwd", "asme_embedding_bwd", "asme_lazy_adam_catch_up",
                                    "asme_lazy_adam_apply", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
-                                   "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd"])
+                                   "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
+                                   "asme_ws_linear"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -193,6 +194,8 @@ def main():
         "asme_attention_fwd": ("mfma", 2 * 2.0 * pairs * dk),
         "asme_attention_bwd": ("mfma", 5 * 2.0 * pairs * dk),
         "asme_linear_weight_grad": ("mfma", wg_flops / 4),
+        # forward + input-gradient GEMMs: 8 per block, the same 4 shapes twice, averaged per launch
+        "asme_ws_linear": ("mfma", 2 * wg_flops / 8),
         "asme_gelu_dropout_fwd": ("hbm", 2 * T * ffn * 4),
         "asme_residual_ln_fwd": ("hbm", 4 * T * d * 4 + T * 8),
         "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),

@@ -10,6 +10,7 @@
 // representative flags assigns compact slots in first-occurrence order.  The map is then rewritten
 // to hold the slot (row_slot for the Adam kernel) and must be reset with asme_dedup_reset.
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "common.h"
 
@@ -296,10 +297,16 @@ int end_bit_for(int64_t cap) {
 
 }  // namespace
 
+// rocprim picks a block-sort + merge-sort path below 2^20 items (10 merge passes at 6e5 occurrences); the
+// limit 0 forces Onesweep LSD radix (one histogram pass + one pass per 8-bit digit of the slot range)
+using OccurrenceSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                         rocprim::default_config, 0>;
+
 ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
     size_t temp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 31);
+    (void)rocprim::radix_sort_pairs<OccurrenceSortConfig>(nullptr, temp, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                          (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0,
+                                                          31);
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     return (int64_t)(2 * up((size_t)n * sizeof(int32_t)) + up(temp));
 }
@@ -321,8 +328,8 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     void* temp = ws + 2 * up((size_t)n * 4);
     size_t temp_bytes = (size_t)workspace_bytes - 2 * up((size_t)n * 4);
     hipLaunchKernelGGL(csr_prep_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, keys, vals);
-    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, sorted_slot, vals, order, (int)n, 0,
-                                           end_bit_for(cap), s) != hipSuccess)
+    if (rocprim::radix_sort_pairs<OccurrenceSortConfig>(temp, temp_bytes, keys, sorted_slot, vals, order, (size_t)n,
+                                                         0, end_bit_for(cap), s) != hipSuccess)
         return hip_status(hipErrorUnknown, "asme_occurrence_csr: sort");
     hipLaunchKernelGGL(csr_bounds_kernel, dim3(nblk(n)), dim3(256), 0, s, sorted_slot, n, cap, seg_off);
     ASME_LAUNCH_CHECK("asme_occurrence_csr");
