@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--table-grad", choices=["sparse", "dense"], default="sparse")
     ap.add_argument("--ids", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--cpu-batch", type=int, default=256, help="sequences per CPU-baseline step")
     ap.add_argument("--cpu-steps", type=int, default=2)
     return ap.parse_args()
@@ -104,9 +106,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.backend == "gloo":
+        local = local % torch.cuda.device_count()  # rehearsal: several ranks may share one GPU
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     asme = __graft_entry__.load_package()
     V = args.items + 3
@@ -173,7 +180,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = 1000.0 * elapsed / args.steps

@@ -32,6 +32,49 @@ from .modules import (ITEM_SEQ_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME, POSITIVE
 from .sequence import InputSequence
 
 
+def _host_staged(group, t: torch.Tensor) -> bool:
+    """gloo has no device all_to_all: device tensors go through host memory (tests / 1-GPU rehearsals of the
+    multi-rank path; production runs use the nccl (= RCCL) backend and never stage)"""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, group=None):
+    if _host_staged(group, inp):
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def _all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
+    if _host_staged(group, t):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
+def _broadcast(t: torch.Tensor, src: int, group=None):
+    if _host_staged(group, t):
+        h = t.cpu()
+        dist.broadcast(h, src, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src, group=group)
+
+
+def _all_gather(outs, t: torch.Tensor, group=None):
+    if _host_staged(group, t):
+        hs = [torch.empty(o.shape, dtype=o.dtype) for o in outs]
+        dist.all_gather(hs, t.cpu(), group=group)
+        for o, h in zip(outs, hs):
+            o.copy_(h)
+    else:
+        dist.all_gather(outs, t, group=group)
+
+
 def shard_rows(vocab: int, world: int, rank: int) -> int:
     """number of global rows {rank, rank + W, ...} < vocab owned by `rank`"""
     return max(0, (vocab - rank + world - 1) // world)
@@ -60,19 +103,19 @@ class RowShardExchange:
         order = torch.argsort(owner, stable=True)
         send_counts_t = torch.bincount(owner, minlength=W).to(torch.int64)
         recv_counts_t = torch.empty_like(send_counts_t)
-        dist.all_to_all_single(recv_counts_t, send_counts_t, group=self.group)
+        _all_to_all(recv_counts_t, send_counts_t, group=self.group)
         counts = torch.stack([send_counts_t, recv_counts_t]).cpu()  # one host sync per step
         sc, rc = counts[0].tolist(), counts[1].tolist()
         send_local = (unique.index_select(0, order) // W).contiguous()
         recv_local = torch.empty(sum(rc), dtype=torch.int64, device=unique.device)
-        dist.all_to_all_single(recv_local, send_local, rc, sc, group=self.group)
+        _all_to_all(recv_local, send_local, rc, sc, group=self.group)
         return ExchangeState(order, sc, rc, recv_local)
 
     def reply_rows(self, st: ExchangeState, rows: torch.Tensor) -> torch.Tensor:
         """owners' rows (aligned with st.recv_local) -> the requester's rows aligned with its unique ids"""
         U = len(st.order)
         got = torch.empty(U, rows.shape[1], dtype=rows.dtype, device=rows.device)
-        dist.all_to_all_single(got, rows.contiguous(), st.send_counts, st.recv_counts, group=self.group)
+        _all_to_all(got, rows.contiguous(), st.send_counts, st.recv_counts, group=self.group)
         out = torch.empty_like(got)
         out.index_copy_(0, st.order, got)
         return out
@@ -82,7 +125,7 @@ class RowShardExchange:
         send = grad_unique.index_select(0, st.order).contiguous()
         recv = torch.empty(len(st.recv_local), grad_unique.shape[1], dtype=grad_unique.dtype,
                            device=grad_unique.device)
-        dist.all_to_all_single(recv, send, st.recv_counts, st.send_counts, group=self.group)
+        _all_to_all(recv, send, st.recv_counts, st.send_counts, group=self.group)
         return recv
 
 
@@ -113,7 +156,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         shard = self.model.item_table()
         for p in self.model.parameters():
             if p is not shard:
-                dist.broadcast(p.data, src, group=self.group)
+                _broadcast(p.data, src, group=self.group)
 
     def _maps(self, dev):
         if self._req_map is None:
@@ -168,7 +211,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         dense = [p for p in self.model.parameters() if p is not shard and p.grad is not None]
         if dense and W > 1:
             flat = torch.cat([p.grad.reshape(-1) for p in dense])
-            dist.all_reduce(flat, group=self.group)
+            _all_reduce(flat, group=self.group)
             flat.mul_(1.0 / W)
             off = 0
             for p in dense:
@@ -191,7 +234,7 @@ def train_step(module, optimizer, batch, batch_idx: int = 0):
 def _gather_queries(x: torch.Tensor, group) -> torch.Tensor:
     W = dist.get_world_size(group)
     out = [torch.empty_like(x) for _ in range(W)]
-    dist.all_gather(out, x.contiguous(), group=group)
+    _all_gather(out, x.contiguous(), group=group)
     return torch.cat(out, 0)
 
 
@@ -213,7 +256,7 @@ def catalog_ranks(exchange: RowShardExchange, hidden: torch.Tensor, targets: tor
     t_all = _gather_queries(targets.to(torch.int64), group)
     s_all = _gather_queries(tscore, group)
     counts = ops.catalog_count_above(h_all, table_shard, t_all, s_all, W, rank)
-    dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    _all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
     n = hidden.shape[0]
     return counts[rank * n:(rank + 1) * n].to(torch.int64) + 1
 
@@ -228,8 +271,8 @@ def catalog_topk(exchange: RowShardExchange, hidden: torch.Tensor, table_shard: 
     v, i = ops.catalog_topk(h_all, table_shard, k, id_stride=W, id_offset=rank)
     vs = [torch.empty_like(v) for _ in range(W)]
     is_ = [torch.empty_like(i) for _ in range(W)]
-    dist.all_gather(vs, v, group=group)
-    dist.all_gather(is_, i, group=group)
+    _all_gather(vs, v, group=group)
+    _all_gather(is_, i, group=group)
     cand_v = torch.cat([x[rank * n:(rank + 1) * n] for x in vs], 1)
     cand_i = torch.cat([x[rank * n:(rank + 1) * n] for x in is_], 1)
     # (score desc, id asc): sort by id, then stably by score
