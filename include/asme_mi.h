@@ -38,20 +38,22 @@ int asme_mi_abi_version(void);
  * out[t] = drop2( LN2( drop1( LN1( table[ids[t]] + pos_table[t % seq_len] ) ) + extra[t] ) )
  * Any of pos_table / LN1 (ln1_w,ln1_b) / extra / LN2 may be NULL (identity).  stats: (n_tokens, 4)
  * = mean1, rstd1, mean2, rstd2 for the backward.  err_flag (nullable) gets bit 0 set on an
- * out-of-range id (nn.Embedding would raise IndexError). */
+ * out-of-range id (nn.Embedding would raise IndexError).  keep_mask (nullable; dim % 4 == 0 only):
+ * (n_tokens, dim/4) bytes, byte c of token t = the dropout decisions of elements 4c..4c+3 (bit i: drop1
+ * keeps element 4c+i, bit 4+i: drop2), written when p1 > 0 or p2 > 0 and read back by the backward. */
 int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
                        int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float ln1_eps,
                        float p1, uint64_t seed1, const float* extra, const float* ln2_w, const float* ln2_b,
-                       float ln2_eps, float p2, uint64_t seed2, float* out, float* stats, int* err_flag,
-                       void* stream);
+                       float ln2_eps, float p2, uint64_t seed2, float* out, float* stats, uint8_t* keep_mask,
+                       int* err_flag, void* stream);
 /* Backward of asme_embedding_fwd: d_rows (n_tokens, dim) = grad wrt (table row + pos row);
  * d_extra (nullable) = grad wrt extra; partials (n_partials, 4*dim) = per-block sums of
  * dLN1.w, dLN1.b, dLN2.w, dLN2.b (reduce with asme_reduce_rows). */
 int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
                        int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float p1,
                        uint64_t seed1, const float* extra, const float* ln2_w, float p2, uint64_t seed2,
-                       const float* dout, const float* stats, float* d_rows, float* d_extra, float* partials,
-                       int64_t n_partials, void* stream);
+                       const uint8_t* keep_mask, const float* dout, const float* stats, float* d_rows,
+                       float* d_extra, float* partials, int64_t n_partials, void* stream);
 int asme_embedding_bwd_partials_count(void);
 /* nn.Embedding dense backward (autograd embedding_dense_backward): grad[ids[r]] += scale * rows[r]
  * (hardware fp32 atomics; ids outside [0, vocab) are skipped). */

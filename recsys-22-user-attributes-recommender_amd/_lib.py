@@ -21,8 +21,8 @@ p, i64, i32, f32, u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_
 SIGNATURES = {
     "asme_mi_last_error": [],
     "asme_mi_abi_version": [],
-    "asme_embedding_fwd": [p, i64, i64, p, i64, i64, p, p, p, f32, f32, u64, p, p, p, f32, f32, u64, p, p, p, p],
-    "asme_embedding_bwd": [p, i64, i64, p, i64, i64, p, p, p, f32, u64, p, p, f32, u64, p, p, p, p, p, i64, p],
+    "asme_embedding_fwd": [p, i64, i64, p, i64, i64, p, p, p, f32, f32, u64, p, p, p, f32, f32, u64, p, p, p, p, p],
+    "asme_embedding_bwd": [p, i64, i64, p, i64, i64, p, p, p, f32, u64, p, p, f32, u64, p, p, p, p, p, p, i64, p],
     "asme_embedding_bwd_partials_count": [],
     "asme_scatter_add_rows": [p, p, i64, i64, p, i64, f32, p],
     "asme_position_grad": [p, i64, i64, i64, p, i64, p, i32, p],

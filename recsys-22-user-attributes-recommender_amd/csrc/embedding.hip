@@ -172,6 +172,255 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(
     if (partials) write_row_partials<R, 4, kWavesPerBlock>(acc, lane, wave, D, partials);
 }
 
+// ---------------------------------------------------------------------------------------------
+// D % 4 == 0 (every transformer width): K tokens per LPR-lane group, so each wave has 2*K independent
+// 512-B row gathers (+ position rows) in flight before the first use -- the random item-row gather is
+// latency-bound, not bandwidth-bound, at one row per group.  Both dropouts of a 4-element chunk come
+// from ONE Philox4x32-10 block (8 16-bit uniforms: x,y -> drop1, z,w -> drop2; keep iff u16 >=
+// round(p * 65536)), and the forward stores the 8 decisions as one keep byte per chunk (bit i: drop1
+// of element i, bit 4+i: drop2), (T, D/4) bytes, so the backward never regenerates them.
+__device__ __forceinline__ uint32_t emb_thresh(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+
+__device__ __forceinline__ uint32_t emb_keep_bits(uint64_t seed, uint64_t chunk, uint32_t th1, uint32_t th2) {
+    u32x4 c{(uint32_t)chunk, (uint32_t)(chunk >> 32), 0xE3B0C442u, 0x5851F42Du};
+    const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint32_t m = 0;
+    m |= ((r.x & 0xFFFFu) >= th1 ? 1u : 0u) | ((r.x >> 16) >= th1 ? 2u : 0u);
+    m |= ((r.y & 0xFFFFu) >= th1 ? 4u : 0u) | ((r.y >> 16) >= th1 ? 8u : 0u);
+    m |= ((r.z & 0xFFFFu) >= th2 ? 16u : 0u) | ((r.z >> 16) >= th2 ? 32u : 0u);
+    m |= ((r.w & 0xFFFFu) >= th2 ? 64u : 0u) | ((r.w >> 16) >= th2 ? 128u : 0u);
+    return m;
+}
+
+__host__ __device__ inline uint64_t emb_seed(uint64_t s1, uint64_t s2) { return s1 ^ (s2 * 0x9E3779B97F4A7C15ull); }
+
+template <class R, int kEmbK>  // kEmbK: tokens per lane group
+__global__ __launch_bounds__(256) void emb_fwd4_kernel(
+    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
+    const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float eps1, float p1,
+    const float* __restrict__ extra, const float* __restrict__ w2, const float* __restrict__ b2, float eps2,
+    float p2, uint64_t seed, float* __restrict__ out, float* __restrict__ stats, uint8_t* __restrict__ keep,
+    int* __restrict__ err) {
+    static_assert(R::W == 4, "4-wide layout only");
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR;
+    const int64_t t0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * R::RPW * kEmbK + lane / R::LPR;
+    int64_t id[kEmbK];
+#pragma unroll
+    for (int k = 0; k < kEmbK; ++k) {
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        int64_t v = t < T ? ids[t] : 0;
+        if (v < 0 || v >= V) {
+            if (sub == 0 && t < T && err) atomicOr(err, 1);
+            v = 0;
+        }
+        id[k] = v;
+    }
+    RowVals<R> x[kEmbK], q[kEmbK];
+#pragma unroll
+    for (int k = 0; k < kEmbK; ++k) row_load<R>(table + id[k] * D, sub, D, x[k]);
+    if (pos) {
+#pragma unroll
+        for (int k = 0; k < kEmbK; ++k) {
+            const int64_t t = t0 + (int64_t)k * R::RPW;
+            row_load<R>(pos + ((t < T ? t : 0) % L) * D, sub, D, q[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kEmbK; ++k)
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
+    }
+    RowVals<R> w1v, b1v, w2v, b2v;
+    if (w1) {
+        row_load<R>(w1, sub, D, w1v);
+        row_load<R>(b1, sub, D, b1v);
+    }
+    if (w2) {
+        row_load<R>(w2, sub, D, w2v);
+        row_load<R>(b2, sub, D, b2v);
+    }
+    const bool drop = p1 > 0.f || p2 > 0.f;
+    const uint32_t th1 = emb_thresh(p1), th2 = emb_thresh(p2);
+    const float k1 = 1.f / (1.f - p1), k2 = 1.f / (1.f - p2);
+#pragma unroll
+    for (int k = 0; k < kEmbK; ++k) {
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        if (t >= T) break;
+        if (extra) row_load<R>(extra + t * D, sub, D, q[k]);
+        float m1 = 0.f, r1 = 1.f, m2 = 0.f, r2 = 1.f;
+        RowVals<R> tmp;
+        if (w1) {
+            row_ln_stats<R>(x[k], sub, D, eps1, m1, r1);
+            row_normalise<R>(x[k], sub, D, m1, r1, tmp);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[k][j][i] = tmp[j][i] * w1v[j][i] + b1v[j][i];
+        }
+        uint32_t bits[R::NV];
+        if (drop) {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j) {
+                const int c = R::col(sub, j);
+                bits[j] = c < D ? emb_keep_bits(seed, ((uint64_t)t * D + c) >> 2, th1, th2) : 0u;
+                if (p1 > 0.f)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
+            }
+        }
+        if (extra)
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
+        if (w2) {
+            row_ln_stats<R>(x[k], sub, D, eps2, m2, r2);
+            row_normalise<R>(x[k], sub, D, m2, r2, tmp);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[k][j][i] = tmp[j][i] * w2v[j][i] + b2v[j][i];
+        }
+        if (drop) {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j) {
+                if (p2 > 0.f)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
+                const int c = R::col(sub, j);
+                if (keep && c < D) keep[((uint64_t)t * D + c) >> 2] = (uint8_t)bits[j];
+            }
+        }
+        row_store<R>(out + t * D, sub, D, x[k]);
+        if (sub == 0 && stats) *reinterpret_cast<float4*>(stats + t * 4) = make_float4(m1, r1, m2, r2);
+    }
+}
+
+template <class R, int kPass>  // kPass: tokens per lane group per grid-stride pass
+__global__ __launch_bounds__(256) void emb_bwd4_kernel(
+    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
+    const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1,
+    const float* __restrict__ extra, const float* __restrict__ w2, float p2, uint64_t seed,
+    const uint8_t* __restrict__ keep, const float* __restrict__ dout, const float* __restrict__ stats,
+    float* __restrict__ d_rows, float* __restrict__ d_extra, float* __restrict__ partials) {
+    static_assert(R::W == 4, "4-wide layout only");
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR, wave = threadIdx.x >> 6;
+    float acc[4][R::NV][R::W];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) row_zero<R>(acc[k]);
+    const bool drop = p1 > 0.f || p2 > 0.f;
+    const uint32_t th1 = emb_thresh(p1), th2 = emb_thresh(p2);
+    const float k1 = 1.f / (1.f - p1), k2 = 1.f / (1.f - p2);
+    for (int64_t tb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * R::RPW * kPass + lane / R::LPR;
+         tb - lane / R::LPR < T; tb += (int64_t)gridDim.x * kWavesPerBlock * R::RPW * kPass) {
+        int64_t id[kPass];
+        float4 st[kPass];
+        RowVals<R> x[kPass], g[kPass], q[kPass];
+#pragma unroll
+        for (int k = 0; k < kPass; ++k) {
+            const int64_t t = tb + (int64_t)k * R::RPW;
+            int64_t v = t < T ? ids[t] : 0;
+            id[k] = (v < 0 || v >= V) ? 0 : v;
+        }
+#pragma unroll
+        for (int k = 0; k < kPass; ++k) {
+            const int64_t t = tb + (int64_t)k * R::RPW;
+            const int64_t tt = t < T ? t : 0;
+            row_load<R>(table + id[k] * D, sub, D, x[k]);
+            if (pos) row_load<R>(pos + (tt % L) * D, sub, D, q[k]);
+            row_load<R>(dout + tt * D, sub, D, g[k]);
+            st[k] = *reinterpret_cast<const float4*>(stats + tt * 4);
+        }
+#pragma unroll
+        for (int k = 0; k < kPass; ++k) {
+            const int64_t t = tb + (int64_t)k * R::RPW;
+            const bool live = t < T;
+            if (!live) {
+                row_zero<R>(x[k]);
+                row_zero<R>(g[k]);
+            } else if (pos) {
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
+            }
+            uint32_t bits[R::NV];
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j) {
+                const int c = R::col(sub, j);
+                bits[j] = 0xFFu;
+                if (drop && live && c < D)
+                    bits[j] = keep ? (uint32_t)keep[((uint64_t)t * D + c) >> 2]
+                                   : emb_keep_bits(seed, ((uint64_t)t * D + c) >> 2, th1, th2);
+            }
+            // recompute z = drop1(LN1(x)) + extra
+            RowVals<R> xh1, xh2;
+            if (w1) {
+                row_normalise<R>(x[k], sub, D, st[k].x, st[k].y, xh1);
+                row_affine<R>(xh1, sub, D, w1, b1, x[k]);
+            }
+            if (p1 > 0.f)
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
+            if (w2) {
+                if (extra && live) {
+                    row_load<R>(extra + t * D, sub, D, q[k]);
+#pragma unroll
+                    for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
+                }
+                row_normalise<R>(x[k], sub, D, st[k].z, st[k].w, xh2);
+            }
+            if (p2 > 0.f)
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) g[k][j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
+            RowVals<R> gz;
+            if (w2) {
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc[2][j][i] += g[k][j][i] * xh2[j][i];
+                        acc[3][j][i] += g[k][j][i];
+                    }
+                row_ln_bwd<R>(g[k], xh2, w2, st[k].w, sub, D, gz);
+            } else {
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) gz[j][i] = g[k][j][i];
+            }
+            if (d_extra && live) row_store<R>(d_extra + t * D, sub, D, gz);
+            if (p1 > 0.f)
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) gz[j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
+            if (w1) {
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc[0][j][i] += gz[j][i] * xh1[j][i];
+                        acc[1][j][i] += gz[j][i];
+                    }
+                RowVals<R> gx;
+                row_ln_bwd<R>(gz, xh1, w1, st[k].y, sub, D, gx);
+                if (live) row_store<R>(d_rows + t * D, sub, D, gx);
+            } else if (live) {
+                row_store<R>(d_rows + t * D, sub, D, gz);
+            }
+        }
+    }
+    if (partials) write_row_partials<R, 4, kWavesPerBlock>(acc, lane, wave, D, partials);
+}
+
 template <int VPL>
 __global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float* __restrict__ rows,
                                                                const int64_t* __restrict__ ids, int64_t n, int D,
@@ -291,18 +540,27 @@ ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t se
                                 int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
                                 const float* ln1_b, float ln1_eps, float p1, uint64_t seed1, const float* extra,
                                 const float* ln2_w, const float* ln2_b, float ln2_eps, float p2, uint64_t seed2,
-                                float* out, float* stats, int* err_flag, void* stream) {
+                                float* out, float* stats, uint8_t* keep_mask, int* err_flag, void* stream) {
     ASME_CHECK_ARG(ids && table && out && stats, "asme_embedding_fwd: null pointer");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && seq_len >= 1 && n_tokens >= 0, "asme_embedding_fwd: bad shape");
     ASME_CHECK_ARG(p1 >= 0.f && p1 < 1.f && p2 >= 0.f && p2 < 1.f, "asme_embedding_fwd: dropout p must be in [0,1)");
     if (n_tokens == 0) return 0;
     if (with_row_layout(dim, [&](auto layout) {
             using R = decltype(layout);
-            const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
-            hipLaunchKernelGGL(emb_fwd_kernel<R>, dim3((unsigned)((n_tokens + rows - 1) / rows)), dim3(256), 0,
-                               (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w,
-                               ln1_b, ln1_eps, p1, seed1, extra, ln2_w, ln2_b, ln2_eps, p2, seed2, out, stats,
-                               err_flag);
+            if constexpr (R::W == 4) {
+                constexpr int K = 2;  // measured at the bench shape: K = 1/2/4/8 -> 75/68/72/88 us (p = 0.2)
+                const int64_t rows = (int64_t)kWavesPerBlock * R::RPW * K;
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K>), dim3((unsigned)((n_tokens + rows - 1) / rows)),
+                                   dim3(256), 0, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim,
+                                   pos_table, ln1_w, ln1_b, ln1_eps, p1, extra, ln2_w, ln2_b, ln2_eps, p2,
+                                   emb_seed(seed1, seed2), out, stats, keep_mask, err_flag);
+            } else {
+                const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
+                hipLaunchKernelGGL(emb_fwd_kernel<R>, dim3((unsigned)((n_tokens + rows - 1) / rows)), dim3(256), 0,
+                                   (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table,
+                                   ln1_w, ln1_b, ln1_eps, p1, seed1, extra, ln2_w, ln2_b, ln2_eps, p2, seed2, out,
+                                   stats, err_flag);
+            }
         }))
         return -1;
     ASME_LAUNCH_CHECK("asme_embedding_fwd");
@@ -313,8 +571,9 @@ ASME_API int asme_embedding_bwd_partials_count(void) { return 1024; }
 ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
                                 int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
                                 const float* ln1_b, float p1, uint64_t seed1, const float* extra, const float* ln2_w,
-                                float p2, uint64_t seed2, const float* dout, const float* stats, float* d_rows,
-                                float* d_extra, float* partials, int64_t n_partials, void* stream) {
+                                float p2, uint64_t seed2, const uint8_t* keep_mask, const float* dout,
+                                const float* stats, float* d_rows, float* d_extra, float* partials,
+                                int64_t n_partials, void* stream) {
     ASME_CHECK_ARG(ids && table && dout && stats && d_rows, "asme_embedding_bwd: null pointer");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512, "asme_embedding_bwd: bad shape");
     ASME_CHECK_ARG(!partials || n_partials >= 1, "asme_embedding_bwd: n_partials must be >= 1");
@@ -325,9 +584,18 @@ ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t se
             const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
             // grid-stride with one partial row per block when the LN parameter grads are wanted
             const int64_t nb = partials ? n_partials : (n_tokens + rows - 1) / rows;
-            hipLaunchKernelGGL(emb_bwd_kernel<R>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, ids,
-                               n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1, seed1, extra,
-                               ln2_w, p2, seed2, dout, stats, d_rows, d_extra, partials);
+            if constexpr (R::W == 4) {
+                constexpr int kPass = 1;  // 2 tokens per pass: 160 VGPRs, 3 waves/SIMD, slower (169 vs 121 us)
+                const int64_t nb4 = partials ? n_partials : (n_tokens + rows - 1) / rows;
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass>), dim3((unsigned)nb4), dim3(256), lds,
+                                   (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w,
+                                   ln1_b, p1, extra, ln2_w, p2, emb_seed(seed1, seed2), keep_mask, dout, stats, d_rows,
+                                   d_extra, partials);
+            } else {
+                hipLaunchKernelGGL(emb_bwd_kernel<R>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, ids,
+                                   n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1, seed1,
+                                   extra, ln2_w, p2, seed2, dout, stats, d_rows, d_extra, partials);
+            }
         }))
         return -1;
     ASME_LAUNCH_CHECK("asme_embedding_bwd");

@@ -243,17 +243,20 @@ class _EmbeddingFn(torch.autograd.Function):
         stats = torch.empty(T, 4, device=table.device, dtype=torch.float32)
         s1, s2 = new_seed(spec.p1), new_seed(spec.p2)
         extra_c = None if extra is None else _f32(extra).reshape(T, D)
+        keep = None
+        if (spec.p1 > 0 or spec.p2 > 0) and D % 4 == 0:  # dropout decisions, one byte per 4 elements
+            keep = torch.empty(T, D // 4, device=table.device, dtype=torch.uint8)
         call("asme_embedding_fwd", ptr(ids), T, spec.seq_len, ptr(table), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
              spec.ln1_eps, spec.p1, s1, ptr(extra_c), ptr(ln2_w), ptr(ln2_b), spec.ln2_eps, spec.p2, s2, ptr(out),
-             ptr(stats), None, stream())
-        ctx.save_for_backward(ids, table, pos, ln1_w, ln1_b, extra_c, ln2_w, stats)
+             ptr(stats), ptr(keep), None, stream())
+        ctx.save_for_backward(ids, table, pos, ln1_w, ln1_b, extra_c, ln2_w, stats, keep)
         ctx.spec, ctx.seeds = spec, (s1, s2)
         ctx.has = (pos is not None, ln1_w is not None, extra is not None, ln2_w is not None)
         return out.view(*ids.shape, D)
 
     @staticmethod
     def backward(ctx, dout):
-        ids, table, pos, ln1_w, ln1_b, extra, ln2_w, stats = ctx.saved_tensors
+        ids, table, pos, ln1_w, ln1_b, extra, ln2_w, stats, keep = ctx.saved_tensors
         spec = ctx.spec
         s1, s2 = ctx.seeds
         T = ids.numel()
@@ -264,8 +267,8 @@ class _EmbeddingFn(torch.autograd.Function):
         has_ln = ctx.has[1] or ctx.has[3]
         part = torch.empty(_N_PARTIALS, 4 * D, device=table.device, dtype=torch.float32) if has_ln else None
         call("asme_embedding_bwd", ptr(ids), T, spec.seq_len, ptr(table), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
-             spec.p1, s1, ptr(extra), ptr(ln2_w), spec.p2, s2, ptr(dout), ptr(stats), ptr(d_rows), ptr(d_extra),
-             ptr(part), _N_PARTIALS, stream())
+             spec.p1, s1, ptr(extra), ptr(ln2_w), spec.p2, s2, ptr(keep), ptr(dout), ptr(stats), ptr(d_rows),
+             ptr(d_extra), ptr(part), _N_PARTIALS, stream())
         g_table = None
         if ctx.needs_input_grad[1]:
             plan = spec.table_grad.plan if spec.table_grad is not None else None

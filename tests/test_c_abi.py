@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(asme):
 def test_argument_validation_is_loud(asme):
     lib = asme._lib.load()
     rc = lib.asme_embedding_fwd(None, 4, 2, None, 10, 8, None, None, None, 1e-5, 0.0, 0, None, None, None, 1e-5,
-                                0.0, 0, None, None, None, None)
+                                0.0, 0, None, None, None, None, None)
     assert rc == -1
     assert b"null pointer" in lib.asme_mi_last_error()
     with pytest.raises(asme._lib.ASMEKernelError):

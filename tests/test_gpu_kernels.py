@@ -146,6 +146,43 @@ def test_embedding_fused_double_ln(asme, dev, D):
         assert _rel(a.grad, b.grad) < 1e-4
 
 
+@pytest.mark.parametrize("D,L", [(128, 200), (64, 9), (32, 7)])
+@pytest.mark.parametrize("p1,p2", [(0.2, 0.2), (0.0, 0.3), (0.25, 0.0)])
+def test_embedding_dropout_keep_mask(asme, dev, D, L, p1, p2):
+    """Embedding with both dropouts: the forward's stored keep bytes (bit i: drop1 of element 4c+i, bit 4+i:
+    drop2) are decoded and used by a CPU fp32 reference for output and every gradient; keep rates ~ 1-p."""
+    torch.manual_seed(D + L)
+    B, V = 6, 53
+    ids = torch.randint(0, V, (B, L))
+    E, P = torch.randn(V, D), torch.randn(L, D)
+    w1, b1, w2, b2 = torch.randn(D), torch.randn(D), torch.randn(D), torch.randn(D)
+    gpu = [t.to(dev).clone().requires_grad_(True) for t in (E, P, w1, b1, w2, b2)]
+    spec = asme.ops.EmbeddingSpec(seq_len=L, p1=p1, p2=p2)
+    yd = asme.ops.embedding(ids.to(dev), gpu[0], gpu[1], (gpu[2], gpu[3]), None, (gpu[4], gpu[5]), spec)
+    keep = yd.grad_fn.saved_tensors[-1].cpu().to(torch.int64)          # (T, D/4) bytes
+    bits = (keep.unsqueeze(-1) >> torch.arange(8)) & 1                  # (T, D/4, 8)
+    k1 = bits[..., :4].reshape(B, L, D).float()
+    k2 = bits[..., 4:].reshape(B, L, D).float()
+    if p1 == 0:
+        assert bool((k1 == 1).all())
+    else:
+        assert abs(1 - k1.mean().item() - p1) < 0.03
+    if p2 == 0:
+        assert bool((k2 == 1).all())
+    else:
+        assert abs(1 - k2.mean().item() - p2) < 0.03
+    cpu = [t.clone().requires_grad_(True) for t in (E, P, w1, b1, w2, b2)]
+    x = F.embedding(ids, cpu[0]) + cpu[1].unsqueeze(0)
+    z = F.layer_norm(x, (D,), cpu[2], cpu[3]) * k1 / (1 - p1)
+    y = F.layer_norm(z, (D,), cpu[4], cpu[5]) * k2 / (1 - p2)
+    go = torch.randn(B, L, D)
+    y.backward(go)
+    yd.backward(go.to(dev))
+    assert _rel(yd, y) < 1e-5
+    for a, b in zip(gpu, cpu):
+        assert _rel(a.grad, b.grad) < 1e-4
+
+
 def test_residual_ln_and_gelu_dropout(asme, dev):
     torch.manual_seed(1)
     n, D = 300, 128
