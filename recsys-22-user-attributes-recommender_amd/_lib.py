@@ -41,6 +41,10 @@ SIGNATURES = {
     "asme_table_grad_workspace": [i64, i64],
     "asme_table_grad_reduce": [p, p, p, p, i64, i64, i64, i32, p, p, p, p, f32, p, i64, p, p],
     "asme_catalog_rank": [p, i64, i64, i64, p, i64, i64, p, p, p, p, p],
+    "asme_linear_xent_fwd_workspace": [i64, i64, i64],
+    "asme_linear_xent_fwd": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, p, i64, p, p],
+    "asme_linear_xent_bwd_workspace": [i64, i64, i64],
+    "asme_linear_xent_bwd": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, p, p, p, p, p, p, i64, p],
     "asme_catalog_topk_workspace": [i64, i64, i64],
     "asme_catalog_topk": [p, i64, i64, i64, p, i64, i64, p, i64, i64, i64, p, i64, p, p, p],
     "asme_catalog_target_scores": [p, i64, i64, i64, p, i64, p, p, p],
@@ -80,7 +84,8 @@ SIGNATURES = {
 _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64,
              "asme_linear_weight_grad_workspace": ctypes.c_int64,
              "asme_attention_dropout_mask_bytes": ctypes.c_int64, "asme_linear_partials_rows": ctypes.c_int64,
-             "asme_catalog_topk_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
+             "asme_catalog_topk_workspace": ctypes.c_int64, "asme_linear_xent_fwd_workspace": ctypes.c_int64,
+             "asme_linear_xent_bwd_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
              "asme_table_grad_workspace": ctypes.c_int64}
 
 _lib: Optional[ctypes.CDLL] = None

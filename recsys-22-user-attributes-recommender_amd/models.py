@@ -97,12 +97,21 @@ class TransformerEncoderModel(SequenceRecommenderModel):
         if is_linear and module.bias is not None:
             module.bias.data.zero_()
 
+    def encode_rows(self, sequence, rows: torch.Tensor) -> torch.Tensor:
+        """representations of the flattened positions `rows` only, (M, d)"""
+        rep = self.encode(sequence)
+        return rep.reshape(-1, rep.shape[-1]).index_select(0, rows)
+
     def forward_rows(self, sequence, rows: torch.Tensor) -> torch.Tensor:
         """Full-catalogue logits for the flattened positions `rows` only, (M, |V|).  Identical to
         forward(sequence).view(-1, |V|)[rows] without the (B, L, |V|) tensor."""
-        rep = self.encode(sequence)
-        h = rep.reshape(-1, rep.shape[-1]).index_select(0, rows)
-        return self._projection_layer(h, sequence)
+        return self._projection_layer(self.encode_rows(sequence, rows), sequence)
+
+    def head_weight_bias(self):
+        """(W (|V|, d), b or None) when the projection is the linear / tied full-catalogue head h W^T + b
+        (layers.py:105-109,138-143) -- the fused logits + cross-entropy kernels then apply; else None."""
+        wb = getattr(self._projection_layer, "weight_bias", None)
+        return wb() if wb is not None else None
 
 
 def normal_initialize_weights(module: nn.Module, initializer_range: float = 0.2) -> None:

@@ -20,6 +20,7 @@ import inspect
 from typing import Dict, Optional
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 from torch.optim.lr_scheduler import LambdaLR
 
@@ -205,6 +206,28 @@ def _instantiate_loss(loss_function, item_tokenizer):
     return loss_function
 
 
+# Full-catalogue CE heads: True = asme_linear_xent_* (logits never stored; 10 n|V|d MFMA FLOP), False = library
+# GEMM logits (n, |V|) + CE kernels (6 n|V|d FLOP, 2 x 4 n|V| bytes of logits and their gradient), None = fused
+# only when those logits would exceed XENT_MATERIALISE_MAX_BYTES (at BERT4Rec C3, 37k x 27k, the materialised
+# path is faster: 10.9 vs 14.4 ms, tools/xent_bench.py).
+FUSED_XENT: Optional[bool] = None
+XENT_MATERIALISE_MAX_BYTES = 16 << 30
+
+
+def _rows_cross_entropy(model, sequence, rows, targets, pad: int) -> torch.Tensor:
+    """CrossEntropyLoss(ignore_index=pad) of the full-catalogue logits at the flattened positions `rows`
+    (masked_training_module.py:93-111 / losses.py:77-115).  With a linear or tied head the logits are never
+    materialised (ops.linear_cross_entropy); otherwise they are, for the selected rows only."""
+    wb = model.head_weight_bias() if FUSED_XENT is not False and hasattr(model, "head_weight_bias") else None
+    if wb is not None:
+        h = model.encode_rows(sequence, rows)
+        big = 8 * h.shape[0] * wb[0].shape[0] > XENT_MATERIALISE_MAX_BYTES
+        if (FUSED_XENT or big) and ops.linear_xent_ok(h, wb[0]):
+            return ops.linear_cross_entropy(h, wb[0], wb[1], targets, pad)
+        return ops.cross_entropy(F.linear(h, wb[0], wb[1]), targets, pad)
+    return ops.cross_entropy(model.forward_rows(sequence, rows), targets, pad)
+
+
 class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
     def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
                  beta_2: float = 0.998, weight_decay: float = 0, loss_function=None, table_grad: str = "dense"):
@@ -227,8 +250,8 @@ class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
         if ce_loss and target.dim() == 2 and hasattr(self.model, "forward_rows"):
             # per-step targets: only the non-pad positions contribute to the CE
             rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)
-            logits = self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
-            loss = ops.cross_entropy(logits, target.reshape(-1).index_select(0, rows), pad)
+            loss = _rows_cross_entropy(self.model, build_model_input(self.model, self.item_tokenizer, batch), rows,
+                                       target.reshape(-1).index_select(0, rows), pad)
         else:
             loss = self.loss_function(target, self(batch, batch_idx))
         self.log(LOG_KEY_TRAINING_LOSS, loss)
@@ -292,8 +315,8 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         pad = self.item_tokenizer.pad_token_id
         self._plan_table([batch[ITEM_SEQ_ENTRY_NAME]])
         rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)
-        logits = self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
-        loss = ops.cross_entropy(logits, target.reshape(-1).index_select(0, rows), pad)
+        loss = _rows_cross_entropy(self.model, build_model_input(self.model, self.item_tokenizer, batch), rows,
+                                   target.reshape(-1).index_select(0, rows), pad)
         self.log(LOG_KEY_TRAINING_LOSS, loss, prog_bar=False)
         return {"loss": loss}
 

@@ -755,6 +755,61 @@ def cross_entropy(logits, targets, ignore_index: int):
     return _CrossEntropyFn.apply(logits, targets, ignore_index)
 
 
+_XENT_DIMS = (32, 64, 128)
+
+
+def linear_xent_ok(hidden: torch.Tensor, weight: torch.Tensor) -> bool:
+    """shapes the fused logits + cross-entropy kernels take (asme_linear_xent_*)"""
+    return (hidden.shape[-1] in _XENT_DIMS and weight.dim() == 2 and weight.shape[1] == hidden.shape[-1]
+            and weight.stride(1) == 1 and weight.stride(0) % 4 == 0 and weight.data_ptr() % 16 == 0)
+
+
+class _LinearXentFn(torch.autograd.Function):
+    """CrossEntropyLoss(ignore_index)(H W^T + b, targets), mean over non-ignored rows, without the (n, |V|)
+    logits (csrc/xent.hip; layers.py:105-109,138-143 + losses.py:77-115)."""
+
+    @staticmethod
+    def forward(ctx, hidden, weight, bias, targets, ignore_index: int):
+        h = _f32(hidden).reshape(-1, hidden.shape[-1])
+        t = _i64(targets).reshape(-1)
+        n, d = h.shape
+        V = weight.shape[0]
+        if t.numel() != n:
+            raise ValueError(f"hidden rows ({n}) and targets ({t.numel()}) differ")
+        lib = _lib.load()
+        ws = torch.empty(max(4, int(lib.asme_linear_xent_fwd_workspace(n, V, d)) // 4 + 1), device=h.device,
+                         dtype=torch.float32)
+        lse = torch.empty(n, device=h.device, dtype=torch.float32)
+        out = torch.empty(2, device=h.device, dtype=torch.float32)
+        call("asme_linear_xent_fwd", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
+             ignore_index, ptr(lse), ptr(ws), ws.numel() * 4, ptr(out), stream())
+        ctx.save_for_backward(h, weight, bias, t, lse, out)
+        ctx.meta = (ignore_index, hidden.shape)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        h, weight, bias, t, lse, out = ctx.saved_tensors
+        ignore_index, shape = ctx.meta
+        n, d = h.shape
+        V = weight.shape[0]
+        lib = _lib.load()
+        ws = torch.empty(max(4, int(lib.asme_linear_xent_bwd_workspace(n, V, d)) // 4 + 1), device=h.device,
+                         dtype=torch.float32)
+        dh = torch.empty_like(h)
+        dw = torch.empty(V, d, device=h.device, dtype=torch.float32)
+        db = torch.empty(V, device=h.device, dtype=torch.float32) if bias is not None else None
+        dl = _f32(dloss.reshape(1))
+        call("asme_linear_xent_bwd", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
+             ignore_index, ptr(lse), ptr(out), ptr(dl), ptr(dh), ptr(dw), ptr(db), ptr(ws), ws.numel() * 4, stream())
+        return dh.view(shape), dw, db, None, None
+
+
+def linear_cross_entropy(hidden, weight, bias, targets, ignore_index: int):
+    """loss of CrossEntropyLoss(ignore_index)(F.linear(hidden, weight, bias), targets) on the fused kernels"""
+    return _LinearXentFn.apply(hidden, weight, bias, targets, ignore_index)
+
+
 def target_rank(scores: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
     """1-based rank of each target in its row (descending; ties -> lower id first)."""
     s = _f32(scores)

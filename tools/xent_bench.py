@@ -1,0 +1,65 @@
+"""Fused logits head + cross-entropy (asme_linear_xent_*) at the BERT4Rec C3 shape vs the materialised path.
+
+Usage: python tools/xent_bench.py [--rows M] [--items V] [--dim d]
+M defaults to the expected non-ignored rows of a B=1024, L=200 cloze batch (0.9*0.2*T + 0.1*B = 36,966).
+Prints kernel times (HIP events) and MFMA rates: executed FLOP (fwd 2MVd, bwd 8MVd: dH and dW each
+recompute the logits) and algorithmic FLOP (the logits GEMM and its two gradient GEMMs: 2MVd + 4MVd).
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+import __graft_entry__  # noqa: E402
+
+PEAK = 157.3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=36966)
+    ap.add_argument("--items", type=int, default=27003)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    asme = __graft_entry__.load_package()
+    dev = torch.device("cuda", 0)
+    M, V, d = a.rows, a.items, a.dim
+    torch.manual_seed(0)
+    h = (torch.randn(M, d, device=dev) * 0.3).requires_grad_(True)
+    W = (torch.randn(V, d, device=dev) * 0.3).requires_grad_(True)
+    b = (torch.randn(V, device=dev) * 0.1).requires_grad_(True)
+    t = torch.randint(3, V, (M,), device=dev)
+    mvd = float(M) * V * d
+    with asme._lib.KernelTimer(["asme_linear_xent_fwd", "asme_linear_xent_bwd"]) as kt:
+        for _ in range(a.iters + 1):
+            loss = asme.ops.linear_cross_entropy(h, W, b, t, 0)
+            loss.backward()
+    st = kt.summary()
+    f = st["asme_linear_xent_fwd"]["avg_ms"]
+    bw = st["asme_linear_xent_bwd"]["avg_ms"]
+    print(f"fused fwd {f:.3f} ms: {2 * mvd / f / 1e9:.1f} TF/s ({2 * mvd / f / 1e9 / PEAK:.2f} of fp32 MFMA peak)")
+    print(f"fused bwd {bw:.3f} ms: executed {8 * mvd / bw / 1e9:.1f} TF/s ({8 * mvd / bw / 1e9 / PEAK:.2f}), "
+          f"algorithmic {4 * mvd / bw / 1e9:.1f} TF/s")
+    print(f"fused step {f + bw:.3f} ms: algorithmic {6 * mvd / (f + bw) / 1e9:.1f} TF/s "
+          f"({6 * mvd / (f + bw) / 1e9 / PEAK:.2f} of peak), executed {10 * mvd / (f + bw) / 1e9:.1f} TF/s")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for i in range(a.iters + 1):
+        if i == 1:
+            ev[0].record()
+        logits = F.linear(h, W, b)
+        loss = asme.ops.cross_entropy(logits, t, 0)
+        loss.backward()
+        del logits, loss
+    ev[1].record()
+    torch.cuda.synchronize()
+    m = ev[0].elapsed_time(ev[1]) / a.iters
+    print(f"materialised (library GEMM {M * V * 4 / 1e9:.1f} GB logits + CE kernels + 2 GEMMs): {m:.3f} ms/step "
+          f"({6 * mvd / m / 1e9:.1f} TF/s algorithmic)")
+
+
+if __name__ == "__main__":
+    main()
