@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the row-sharded path even at N=1 (1-rank RCCL group): its overhead without the fabric")
     ap.add_argument("--cpu-batch", type=int, default=256, help="sequences per CPU-baseline step")
     ap.add_argument("--cpu-steps", type=int, default=2)
     return ap.parse_args()
@@ -108,8 +110,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.backend == "gloo":
         local = local % torch.cuda.device_count()  # rehearsal: several ranks may share one GPU
-    if world > 1:
+    if world > 1 or args.sharded:
         torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -120,7 +126,7 @@ def main():
     B, L, d = args.batch, args.seq_len, args.dim
 
     torch.manual_seed(rank)
-    sharded = world > 1
+    sharded = world > 1 or args.sharded
     # N > 1: the item table is row-sharded over the ranks (RCCL all-to-all of ids / rows / row grads,
     # one all_reduce of the replicated dense gradients); N = 1: the whole table on the one GPU
     rows = asme.sharded.shard_rows(V, world, rank) if sharded else V
@@ -260,7 +266,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args, V)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -199,6 +199,15 @@ int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_t* map, v
 int asme_dedup_reset(const int64_t* unique, const int32_t* count, int64_t cap, int32_t* map, void* stream);
 int asme_owner_histogram(const int64_t* unique, const int32_t* count, int64_t cap, int world, int32_t* owner,
                          int32_t* counts, void* stream);
+/* stable grouping of n unique ids by owner (id % world, world <= 64): order[j] = index of the j-th id sent,
+ * send_local[j] = ids[order[j]] / world, counts[w] (int64) = ids sent to rank w, pos (nullable) = the inverse
+ * permutation (pos[order[j]] = j).  Workspace: asme_bucket_by_owner_workspace bytes. */
+int64_t asme_bucket_by_owner_workspace(int64_t n, int world);
+int asme_bucket_by_owner(const int64_t* ids, int64_t n, int world, void* workspace, int64_t ws_bytes, int64_t* order,
+                         int64_t* send_local, int64_t* counts, int64_t* pos, void* stream);
+/* out[r] = table[ids[r]] (zero row for ids outside [0, vocab)): the owner side of the sharded lookup */
+int asme_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t vocab, int64_t dim, float* out,
+                     void* stream);
 
 
 /* ---- Fused Linear layers (csrc/linear.hip): fp32 MFMA GEMMs with the block's elementwise passes as
@@ -275,9 +284,9 @@ int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, con
 
 /* ---- Weight-stationary Linear GEMM (csrc/wsgemm.hip; transformer_layers.py:175-199, 212-220 nn.Linear and
  * PositionwiseFeedForward).  One NB x K weight block resident in LDS per workgroup, X streamed from HBM into
- * registers, deferred buffer-store epilogue.  epi: 0 store (+bias), 1 pre = C + bias -> pre_out and
- * Y = dropout(GELU(pre)), 2 Y = C * keep * GELU'(pre_in); trans = 1: W is K x N (Y = X W).  Dropout as
- * asme_gelu_dropout_fwd (salt 5, element m*N + n). */
+ * registers, deferred buffer-store epilogue.  epi: 0 store (+bias), 1 pre = C + bias, Y = dropout(GELU(pre))
+ * and the activation factor keep * GELU'(pre) -> pre_out, 2 Y = C * pre_in (pre_in = that factor); trans = 1:
+ * W is K x N (Y = X W).  Dropout as asme_gelu_dropout_fwd (salt 5, element m*N + n). */
 int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N);
 int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W, int64_t N, int trans, const float* bias,
                    int epi, float* pre_out, const float* pre_in, float p, uint64_t seed, float* Y, void* stream);

@@ -80,12 +80,15 @@ SIGNATURES = {
     "asme_dedup_ids": [p, i64, i64, p, p, i64, p, p, p, p],
     "asme_dedup_reset": [p, p, i64, p, p],
     "asme_owner_histogram": [p, p, i64, i32, p, p, p],
+    "asme_bucket_by_owner_workspace": [i64, i32],
+    "asme_bucket_by_owner": [p, i64, i32, p, i64, p, p, p, p, p],
+    "asme_gather_rows": [p, i64, p, i64, i64, p, p],
 }
 _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64,
              "asme_linear_weight_grad_workspace": ctypes.c_int64,
              "asme_attention_dropout_mask_bytes": ctypes.c_int64, "asme_linear_partials_rows": ctypes.c_int64,
              "asme_catalog_topk_workspace": ctypes.c_int64, "asme_linear_xent_fwd_workspace": ctypes.c_int64,
-             "asme_linear_xent_bwd_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
+             "asme_linear_xent_bwd_workspace": ctypes.c_int64, "asme_bucket_by_owner_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
              "asme_table_grad_workspace": ctypes.c_int64}
 
 _lib: Optional[ctypes.CDLL] = None

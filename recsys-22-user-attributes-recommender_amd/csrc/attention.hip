@@ -162,12 +162,21 @@ template <int DK, int NS = kNS>
 __device__ __forceinline__ void rows_times_slice(const float* __restrict__ tile, int g, int c16,
                                                  const float (&f)[DK / 4], floatx4 (&acc)[NS]) {
     constexpr int S = DK + 4, DQ = DK / 4;
+    // the b128 row reads of step s4+1 are issued before step s4's MFMAs (LDS latency off the MFMA stream)
+    float4 ab[2][NS];
+    const float* base = tile + c16 * S + g * DQ;
+#pragma unroll
+    for (int sub = 0; sub < NS; ++sub) ab[0][sub] = *reinterpret_cast<const float4*>(base + sub * 16 * S);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s4 = 0; s4 < DQ / 4; ++s4) {
-        float4 a[NS];
+        if (s4 + 1 < DQ / 4) {
 #pragma unroll
-        for (int sub = 0; sub < NS; ++sub)
-            a[sub] = *reinterpret_cast<const float4*>(tile + (sub * 16 + c16) * S + g * DQ + 4 * s4);
+            for (int sub = 0; sub < NS; ++sub)
+                ab[(s4 + 1) & 1][sub] = *reinterpret_cast<const float4*>(base + sub * 16 * S + 4 * (s4 + 1));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float4(&a)[NS] = ab[s4 & 1];
 #pragma unroll
         for (int sub = 0; sub < NS; ++sub) acc[sub] = mfma16(a[sub].x, f[4 * s4], acc[sub]);
 #pragma unroll
@@ -184,13 +193,29 @@ template <int DK, int NS = kNS>
 __device__ __forceinline__ void cols_times_weights(const float* __restrict__ tile, int g, int c16,
                                                    const float (&w)[NS][4], floatx4 (&out)[DK / 16]) {
     constexpr int S = DK + 4, NCT = DK / 16;
+    // the operands of sub-tile sub+1 are read while sub's MFMAs run: the b32 column reads would otherwise
+    // expose their LDS latency before every pair of MFMAs
+    float vb[2][4][NCT];
+    const float* base = tile + 4 * g * S + c16;
 #pragma unroll
-    for (int sub = 0; sub < NS; ++sub)
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) vb[0][s][ct] = base[s * S + ct * 16];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sub = 0; sub < NS; ++sub) {
+        if (sub + 1 < NS) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) vb[(sub + 1) & 1][s][ct] = base[((sub + 1) * 16 + s) * S + ct * 16];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this sub-tile's MFMAs
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int ct = 0; ct < NCT; ++ct)
-                out[ct] = mfma16(tile[(sub * 16 + 4 * g + s) * S + ct * 16 + c16], w[sub][s], out[ct]);
+            for (int ct = 0; ct < NCT; ++ct) out[ct] = mfma16(vb[sub & 1][s][ct], w[sub][s], out[ct]);
+    }
 }
 
 template <int DK>

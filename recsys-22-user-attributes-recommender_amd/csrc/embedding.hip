@@ -519,6 +519,33 @@ __global__ __launch_bounds__(256) void gather_sum_bwd_kernel(const float* __rest
     }
 }
 
+// out[r] = table[ids[r]] (zero row for ids outside [0, V)); D % 4 == 0: float4 lanes, K rows in flight per
+// lane group (the owner side of the row-sharded lookup)
+template <class R, int K>
+__global__ __launch_bounds__(256) void gather_rows4_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                           const float* __restrict__ table, int64_t V, int D,
+                                                           float* __restrict__ out) {
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR;
+    const int64_t r0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * R::RPW * K + lane / R::LPR;
+    int64_t id[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t r = r0 + (int64_t)k * R::RPW;
+        id[k] = r < n ? ids[r] : -1;
+    }
+    RowVals<R> x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (id[k] >= 0 && id[k] < V) row_load<R>(table + id[k] * D, sub, D, x[k]);
+        else row_zero<R>(x[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t r = r0 + (int64_t)k * R::RPW;
+        if (r < n) row_store<R>(out + r * D, sub, D, x[k]);
+    }
+}
+
 inline int vpl_of(int64_t D) { return (int)((D + 63) / 64); }
 
 #define ASME_VPL_DISPATCH(VPLV, ...)                              \
@@ -644,6 +671,26 @@ ASME_API int asme_gather_sum_fwd(const int64_t* ids, int64_t n, int64_t k, int s
                                                       (hipStream_t)stream, ids, n, (int)k, skip_zero, table, vocab,
                                                       (int)dim, bias, out, accumulate));
     ASME_LAUNCH_CHECK("asme_gather_sum_fwd");
+}
+
+ASME_API int asme_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t vocab, int64_t dim,
+                              float* out, void* stream) {
+    ASME_CHECK_ARG(ids && table && out, "asme_gather_rows: null pointer");
+    ASME_CHECK_ARG(dim >= 1 && dim <= 512, "asme_gather_rows: bad shape");
+    if (n == 0) return 0;
+    if (dim % 4 != 0 || ((uintptr_t)table & 15) || ((uintptr_t)out & 15))
+        return asme_gather_sum_fwd(ids, n, 1, 0, table, vocab, dim, nullptr, out, 0, stream);
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            if constexpr (R::W == 4) {
+                constexpr int K = 4;
+                const int64_t rows = (int64_t)kWavesPerBlock * R::RPW * K;
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(gather_rows4_kernel<R, K>), dim3((unsigned)((n + rows - 1) / rows)),
+                                   dim3(256), 0, (hipStream_t)stream, ids, n, table, vocab, (int)dim, out);
+            }
+        }))
+        return -1;
+    ASME_LAUNCH_CHECK("asme_gather_rows");
 }
 
 ASME_API int asme_gather_sum_bwd(const float* dout, const int64_t* ids, int64_t n, int64_t k, int skip_zero,

@@ -78,6 +78,105 @@ __global__ void owner_hist_kernel(const int64_t* __restrict__ ids, const int32_t
 
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+// ---- stable bucketing of the requester's unique ids by owner (counting sort over W <= 64 buckets):
+// block b of kBk ids -> bcount[w * nb + b]; one block scans (w-major) into offsets; the scatter pass ranks
+// each id among the same-owner ids of its block (wave ballots + LDS wave prefixes, four rounds in order),
+// so positions are stable: bucket w holds its ids in increasing unique-index order.
+constexpr int kBk = 1024, kBkThreads = 256, kMaxW = 64;
+
+__global__ __launch_bounds__(kBkThreads) void bucket_count_kernel(const int64_t* __restrict__ ids, int64_t n, int W,
+                                                                  int32_t* __restrict__ bcount, int64_t nb) {
+    __shared__ int32_t h[kMaxW];
+    for (int w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * kBk;
+    for (int r = 0; r < kBk / kBkThreads; ++r) {
+        const int64_t i = b0 + r * kBkThreads + threadIdx.x;
+        if (i < n) atomicAdd(h + (int)(ids[i] % W), 1);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < W; w += blockDim.x) bcount[(int64_t)w * nb + blockIdx.x] = h[w];
+}
+
+// exclusive scan of bcount (W * nb, w-major) in place; counts[w] = ids owned by w
+__global__ __launch_bounds__(1024) void bucket_scan_kernel(int32_t* __restrict__ bcount, int64_t nb, int W, int64_t n,
+                                                           int64_t* __restrict__ counts) {
+    __shared__ int32_t part[1024];
+    const int64_t total = nb * W;
+    const int64_t per = (total + blockDim.x - 1) / blockDim.x;
+    const int64_t lo = min(total, (int64_t)threadIdx.x * per), hi = min(total, lo + per);
+    int32_t s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += bcount[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t run = 0;
+        for (int t = 0; t < (int)blockDim.x; ++t) {
+            const int32_t v = part[t];
+            part[t] = run;
+            run += v;
+        }
+    }
+    __syncthreads();
+    int32_t run = part[threadIdx.x];
+    for (int64_t i = lo; i < hi; ++i) {
+        const int32_t v = bcount[i];
+        bcount[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < W; w += blockDim.x) {
+        const int64_t beg = bcount[(int64_t)w * nb];
+        const int64_t end = w + 1 < W ? (int64_t)bcount[(int64_t)(w + 1) * nb] : n;
+        counts[w] = end - beg;
+    }
+}
+
+__global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_t* __restrict__ ids, int64_t n, int W,
+                                                                    const int32_t* __restrict__ boff, int64_t nb,
+                                                                    int64_t* __restrict__ order,
+                                                                    int64_t* __restrict__ send_local) {
+    constexpr int kWv = kBkThreads / 64;
+    __shared__ int32_t base[kMaxW];
+    __shared__ int32_t wcnt[kWv][kMaxW];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int w = threadIdx.x; w < W; w += blockDim.x) base[w] = boff[(int64_t)w * nb + blockIdx.x];
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int64_t b0 = (int64_t)blockIdx.x * kBk;
+    for (int r = 0; r < kBk / kBkThreads; ++r) {
+        const int64_t i = b0 + r * kBkThreads + threadIdx.x;
+        const bool live = i < n;
+        const int64_t id = live ? ids[i] : 0;
+        const int mine = live ? (int)(id % W) : -1;
+        int rank = 0;
+        for (int w = 0; w < W; ++w) {
+            const uint64_t m = __ballot(mine == w);
+            if (mine == w) rank = __popcll(m & lt);
+            if (lane == 0) wcnt[wave][w] = __popcll(m);
+        }
+        __syncthreads();
+        if (live) {
+            int pre = 0;
+            for (int v = 0; v < wave; ++v) pre += wcnt[v][mine];
+            const int64_t pos = (int64_t)base[mine] + pre + rank;
+            order[pos] = i;
+            send_local[pos] = id / W;
+        }
+        __syncthreads();
+        for (int w = threadIdx.x; w < W; w += blockDim.x) {
+            int t = 0;
+            for (int v = 0; v < kWv; ++v) t += wcnt[v][w];
+            base[w] += t;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void invert_perm_kernel(const int64_t* __restrict__ order, int64_t n, int64_t* __restrict__ pos) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) pos[order[j]] = j;
+}
+
 }  // namespace
 
 ASME_API int64_t asme_dedup_workspace_bytes(int64_t n) {
@@ -128,6 +227,36 @@ ASME_API int asme_owner_histogram(const int64_t* unique, const int32_t* count, i
     hipLaunchKernelGGL(owner_hist_kernel, dim3(nblk(cap)), dim3(256), 0, (hipStream_t)stream, unique, count, cap,
                        world, owner, counts);
     ASME_LAUNCH_CHECK("asme_owner_histogram");
+}
+
+ASME_API int64_t asme_bucket_by_owner_workspace(int64_t n, int world) {
+    const int64_t nb = (n + kBk - 1) / kBk;
+    return (nb * world + 1) * (int64_t)sizeof(int32_t);
+}
+
+// Row-shard request routing: the n unique ids, grouped by owner (id % world) in a stable order.
+// order[j] = index into ids of the j-th id sent; send_local[j] = ids[order[j]] / world (the owner's row);
+// counts[w] = ids sent to rank w (int64, world entries); pos[order[j]] = j (nullable: the inverse permutation).
+ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, int world, void* workspace, int64_t ws_bytes,
+                                  int64_t* order, int64_t* send_local, int64_t* counts, int64_t* pos, void* stream) {
+    ASME_CHECK_ARG(ids && workspace && order && send_local && counts, "asme_bucket_by_owner: null pointer");
+    ASME_CHECK_ARG(world >= 1 && world <= kMaxW, "asme_bucket_by_owner: world must be in [1, 64]");
+    ASME_CHECK_ARG(n >= 0 && n < ((int64_t)1 << 31), "asme_bucket_by_owner: bad n");
+    ASME_CHECK_ARG(ws_bytes >= asme_bucket_by_owner_workspace(n, world), "asme_bucket_by_owner: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (hipMemsetAsync(counts, 0, world * sizeof(int64_t), s) != hipSuccess)
+            return hip_status(hipGetLastError(), "asme_bucket_by_owner");
+        return 0;
+    }
+    const int64_t nb = (n + kBk - 1) / kBk;
+    int32_t* bcount = (int32_t*)workspace;
+    hipLaunchKernelGGL(bucket_count_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, world, bcount, nb);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, bcount, nb, world, n, counts);
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, world, bcount, nb,
+                       order, send_local);
+    if (pos) hipLaunchKernelGGL(invert_perm_kernel, dim3(nblk(n)), dim3(256), 0, s, order, n, pos);
+    ASME_LAUNCH_CHECK("asme_bucket_by_owner");
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -16,8 +16,10 @@
 // registers until a tile later (an LDS read or MFMA landing on them right after the store stalls the
 // wave until the store has left), and rows past M are dropped by the buffer range check.
 // Epilogues: WS_STORE       Y = C (+ bias)
-//            WS_GELU_DROP   pre = C + bias; Y = dropout(GELU(pre))            (FFN inner layer, forward)
-//            WS_GELU_BWD    Y = C * keep * GELU'(pre)                          (through the FFN activation)
+//            WS_GELU_DROP   pre = C + bias; Y = dropout(GELU(pre)); A = keep * GELU'(pre)   (FFN inner, forward)
+//            WS_GELU_BWD    Y = C * A                                                   (through the activation)
+// A (the activation factor, written by the forward in place of the pre-activation, same bytes) makes the
+// backward epilogue a single multiply: no Philox, erf or exp in the input-gradient GEMM.
 // Dropout decisions are exactly those of asme_gelu_dropout_fwd/bwd (norm.hip): element m*N + n, one
 // Philox block per 4 consecutive elements, salt 5.
 // Measured at M = 204800 (tools/probe/sgemm_probe.py, fp32 MFMA peak 157 TF/s): K=128 -> N=512 113 TF/s,
@@ -39,8 +41,8 @@ enum { WS_STORE = 0, WS_GELU_DROP = 1, WS_GELU_BWD = 2 };
 
 struct WsEpi {
     const float* bias;   // [N] or null
-    float* pre_out;      // WS_GELU_DROP: pre-activation out
-    const float* pre_in; // WS_GELU_BWD: pre-activation in
+    float* pre_out;      // WS_GELU_DROP: activation factor keep * GELU'(pre) out
+    const float* pre_in; // WS_GELU_BWD: activation factor in
     float p;             // dropout probability (0: none)
     uint64_t seed;
 };
@@ -134,23 +136,22 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         float4 v = stash[ct];
         if constexpr (EPI == WS_STORE) {
             bstore(v, yr, off);
-        } else {
+        } else if constexpr (EPI == WS_GELU_DROP) {
             float u[4] = {1.f, 1.f, 1.f, 1.f};
             if (ep.p > 0.f) {
                 philox_uniform4(ep.seed, 5u, off >> 4, u);  // element index (off / 4), 4 per Philox block
 #pragma unroll
                 for (int i = 0; i < 4; ++i) u[i] = u[i] >= ep.p ? keep_k : 0.f;
             }
-            if constexpr (EPI == WS_GELU_DROP) {
-                bstore(v, pr, off);
-                v = make_float4(gelu_erf(v.x) * u[0], gelu_erf(v.y) * u[1], gelu_erf(v.z) * u[2],
-                                gelu_erf(v.w) * u[3]);
-            } else {
-                const float4 x = pre[ct];
-                v = make_float4(v.x * u[0] * gelu_erf_grad(x.x), v.y * u[1] * gelu_erf_grad(x.y),
-                                v.z * u[2] * gelu_erf_grad(x.z), v.w * u[3] * gelu_erf_grad(x.w));
-            }
+            // the backward's whole activation factor keep * GELU'(pre), so its epilogue is one multiply
+            bstore(make_float4(u[0] * gelu_erf_grad(v.x), u[1] * gelu_erf_grad(v.y), u[2] * gelu_erf_grad(v.z),
+                               u[3] * gelu_erf_grad(v.w)),
+                   pr, off);
+            v = make_float4(gelu_erf(v.x) * u[0], gelu_erf(v.y) * u[1], gelu_erf(v.z) * u[2], gelu_erf(v.w) * u[3]);
             bstore(v, yr, off);
+        } else {
+            const float4 f = pre[ct];
+            bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off);
         }
     };
     floatx4 acc[CT];

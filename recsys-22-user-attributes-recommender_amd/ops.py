@@ -117,6 +117,7 @@ class SparseTablePlan:
             call("asme_dedup_ids", ptr(flat), n, self.vocab, ptr(slot_map), ptr(ws), ws_bytes, ptr(self.unique),
                  ptr(inverse), ptr(self.count), stream())
         self.capacity = n
+        self.grad_scale = 1.0  # factor on every reduced gradient row (the sharded owner: 1/W, DDP averaging)
         self._grad_rows = None
         self._inverse = {}
         self._flat_inverse = inverse
@@ -134,6 +135,35 @@ class SparseTablePlan:
         if tg is not None and tg.lazy is not None:
             # rows gathered by this step's forward must carry every earlier (zero-gradient) update
             tg.lazy.catch_up(self.unique, self.count, self.capacity)
+
+    @classmethod
+    def identity(cls, n_rows: int, id_sets: Sequence[torch.Tensor], dim: int) -> "SparseTablePlan":
+        """plan over ids that already are row indices of a compact (n_rows, dim) table in which every row
+        occurs (the sharded step's table of fetched rows): no dedup, slot s == row s, so grad_rows[:n_rows]
+        is the table's gradient in row order, from the same ordered (deterministic) reduction"""
+        self = cls.__new__(cls)
+        flat = torch.cat([_i64(x).reshape(-1) for x in id_sets])
+        n = flat.numel()
+        if n_rows > n:
+            raise ValueError("identity plan: every row must occur at least once")
+        dev = flat.device
+        self.vocab, self.dim = n_rows, dim
+        self.slot_map = None
+        self.unique = torch.arange(n_rows, device=dev, dtype=torch.int64)
+        self.count = torch.full((1,), n_rows, device=dev, dtype=torch.int32)
+        self.capacity = n
+        self.grad_scale = 1.0
+        self._grad_rows = None
+        self._inverse, self._offset, self._contrib = {}, {}, []
+        self._flat_inverse = flat
+        off = 0
+        for x in id_sets:
+            key = (x.data_ptr(), tuple(x.shape))
+            self._inverse[key] = x
+            self._offset[key] = off
+            off += x.numel()
+        self.consumed = False
+        return self
 
     @classmethod
     def for_ids(cls, vocab: int, id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor) -> "SparseTablePlan":
@@ -185,7 +215,7 @@ class SparseTablePlan:
             scales = (ctypes_vp * k)(*[(c[3].data_ptr() if c[3] is not None else None) for c in part])
             dest = out if i == 0 else torch.empty_like(out)  # more than 4 contributions: add the rest
             call("asme_table_grad_reduce", ptr(order), ptr(slot), ptr(seg_off), ptr(self.count), n, n, d, k, offs,
-                 ns, rows, scales, 1.0, ptr(parts), part_bytes, ptr(dest), stream())
+                 ns, rows, scales, self.grad_scale, ptr(parts), part_bytes, ptr(dest), stream())
             if i:
                 out += dest
         self._contrib = []
@@ -214,7 +244,8 @@ class SparseTablePlan:
         return self._inverse[key]
 
     def release(self):
-        call("asme_dedup_reset", ptr(self.unique), ptr(self.count), self.capacity, ptr(self.slot_map), stream())
+        if self.slot_map is not None:
+            call("asme_dedup_reset", ptr(self.unique), ptr(self.count), self.capacity, ptr(self.slot_map), stream())
         self.consumed = True
 
 
@@ -349,6 +380,31 @@ def _reduce_rows(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def gather_rows(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """table[ids] (no autograd; zero rows for ids outside the table) on asme_gather_rows"""
+    ids = _i64(ids).reshape(-1)
+    V, D = table.shape
+    out = torch.empty(ids.numel(), D, device=table.device, dtype=torch.float32)
+    call("asme_gather_rows", ptr(ids), ids.numel(), ptr(_f32(table)), V, D, ptr(out), stream())
+    return out
+
+
+def bucket_by_owner(unique: torch.Tensor, world: int):
+    """stable grouping of unique ids by owner (id % world): (order, send_local, counts (int64, world), pos) with
+    unique[order[j]] the j-th id sent, send_local[j] its owner-local row, pos[order[j]] = j"""
+    u = _i64(unique).reshape(-1)
+    n = u.numel()
+    dev = u.device
+    ws = torch.empty(max(8, int(_lib.load().asme_bucket_by_owner_workspace(n, world))), device=dev, dtype=torch.uint8)
+    order = torch.empty(n, device=dev, dtype=torch.int64)
+    send_local = torch.empty(n, device=dev, dtype=torch.int64)
+    counts = torch.empty(world, device=dev, dtype=torch.int64)
+    pos = torch.empty(n, device=dev, dtype=torch.int64)
+    call("asme_bucket_by_owner", ptr(u), n, world, ptr(ws), ws.numel(), ptr(order), ptr(send_local), ptr(counts),
+         ptr(pos), stream())
+    return order, send_local, counts, pos
+
+
 def gather_sum(ids, table, bias=None, skip_zero=False):
     return _GatherSumFn.apply(ids, table, bias, skip_zero)
 
@@ -437,9 +493,9 @@ def linear(x, w, b=None):
 
 class _FFNFn(torch.autograd.Function):
     """PositionwiseFeedForward W2(dropout(GELU_erf(W1 x + b1))) + b2 (transformer_layers.py:212-220) with the
-    activation fused into the GEMMs: forward GEMM1 writes the pre-activation and dropout(GELU(.)); the backward
-    input-gradient GEMM of W2 applies keep * GELU'(pre) in its epilogue.  Same dropout decisions as
-    gelu_dropout (salt 5, element index over the (T, d_ff) activation)."""
+    activation fused into the GEMMs: forward GEMM1 writes dropout(GELU(pre)) and the activation factor
+    A = keep * GELU'(pre); the backward input-gradient GEMM of W2 multiplies by A in its epilogue.  Same dropout
+    decisions as gelu_dropout (salt 5, element index over the (T, d_ff) activation)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, p: float):
@@ -447,20 +503,20 @@ class _FFNFn(torch.autograd.Function):
         x2 = _f32(x).reshape(-1, D)
         M = x2.shape[0]
         seed = new_seed(p)
-        pre = torch.empty(M, F, device=x.device, dtype=torch.float32)
-        g = _ws(x2, w1, F, 0, bias=b1, epi=1, pre_out=pre, p=p, seed=seed)
+        fac = torch.empty(M, F, device=x.device, dtype=torch.float32)
+        g = _ws(x2, w1, F, 0, bias=b1, epi=1, pre_out=fac, p=p, seed=seed)
         y = _linear_fwd(g, w2, b2)
-        ctx.save_for_backward(x2, pre, g, w1, w2)
+        ctx.save_for_backward(x2, fac, g, w1, w2)
         ctx.meta = (p, seed, b1 is not None, b2 is not None, x.shape)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, pre, g, w1, w2 = ctx.saved_tensors
+        x2, fac, g, w1, w2 = ctx.saved_tensors
         p, seed, hb1, hb2, xshape = ctx.meta
         F, D = w1.shape
         dy2 = _f32(dy).reshape(-1, D)
-        d_pre = _ws(dy2, w2, F, 1, epi=2, pre_in=pre, p=p, seed=seed)
+        d_pre = _ws(dy2, w2, F, 1, epi=2, pre_in=fac, p=p, seed=seed)
         dw2, db2 = _weight_grad(dy2, g, hb2)
         dx = _linear_dx(d_pre, w1).view(xshape) if ctx.needs_input_grad[0] else None
         dw1, db1 = _weight_grad(d_pre, x2, hb1)

@@ -82,10 +82,11 @@ def shard_rows(vocab: int, world: int, rank: int) -> int:
 
 @dataclass
 class ExchangeState:
-    order: torch.Tensor          # permutation sorting the requester's unique ids by owner
+    order: torch.Tensor          # send order: the j-th id sent is unique[order[j]] (grouped by owner)
     send_counts: List[int]       # ids sent to each owner
     recv_counts: List[int]       # ids received from each requester
     recv_local: torch.Tensor     # local row ids requested from this rank, grouped by requester
+    pos: torch.Tensor            # inverse of order: unique[i] is sent at position pos[i]
 
 
 class RowShardExchange:
@@ -99,33 +100,35 @@ class RowShardExchange:
     def request(self, unique: torch.Tensor) -> ExchangeState:
         """route the requester's unique global ids to their owners"""
         W = self.world
-        owner = unique % W
-        order = torch.argsort(owner, stable=True)
-        send_counts_t = torch.bincount(owner, minlength=W).to(torch.int64)
+        if unique.is_cuda:  # stable owner bucketing in one counting-sort pass (asme_bucket_by_owner)
+            order, send_local, send_counts_t, pos = ops.bucket_by_owner(unique, W)
+        else:
+            owner = unique % W
+            order = torch.argsort(owner, stable=True)
+            send_counts_t = torch.bincount(owner, minlength=W).to(torch.int64)
+            send_local = (unique.index_select(0, order) // W).contiguous()
+            pos = torch.empty_like(order)
+            pos[order] = torch.arange(len(order), dtype=order.dtype)
         recv_counts_t = torch.empty_like(send_counts_t)
         _all_to_all(recv_counts_t, send_counts_t, group=self.group)
         counts = torch.stack([send_counts_t, recv_counts_t]).cpu()  # one host sync per step
         sc, rc = counts[0].tolist(), counts[1].tolist()
-        send_local = (unique.index_select(0, order) // W).contiguous()
         recv_local = torch.empty(sum(rc), dtype=torch.int64, device=unique.device)
         _all_to_all(recv_local, send_local, rc, sc, group=self.group)
-        return ExchangeState(order, sc, rc, recv_local)
+        return ExchangeState(order, sc, rc, recv_local, pos)
 
     def reply_rows(self, st: ExchangeState, rows: torch.Tensor) -> torch.Tensor:
-        """owners' rows (aligned with st.recv_local) -> the requester's rows aligned with its unique ids"""
+        """owners' rows (aligned with st.recv_local) -> the requester's rows in SEND order: row j belongs to
+        unique[st.order[j]] (unique id i is row st.pos[i]; callers remap ids instead of permuting rows)"""
         U = len(st.order)
         got = torch.empty(U, rows.shape[1], dtype=rows.dtype, device=rows.device)
         _all_to_all(got, rows.contiguous(), st.send_counts, st.recv_counts, group=self.group)
-        out = torch.empty_like(got)
-        out.index_copy_(0, st.order, got)
-        return out
+        return got
 
-    def push_grads(self, st: ExchangeState, grad_unique: torch.Tensor) -> torch.Tensor:
-        """requester's gradient rows (aligned with its unique ids) -> owners, aligned with st.recv_local"""
-        send = grad_unique.index_select(0, st.order).contiguous()
-        recv = torch.empty(len(st.recv_local), grad_unique.shape[1], dtype=grad_unique.dtype,
-                           device=grad_unique.device)
-        _all_to_all(recv, send, st.recv_counts, st.send_counts, group=self.group)
+    def push_grads(self, st: ExchangeState, grad_send: torch.Tensor) -> torch.Tensor:
+        """requester's gradient rows in send order (aligned with reply_rows) -> owners, aligned with recv_local"""
+        recv = torch.empty(len(st.recv_local), grad_send.shape[1], dtype=grad_send.dtype, device=grad_send.device)
+        _all_to_all(recv, grad_send.contiguous(), st.recv_counts, st.send_counts, group=self.group)
         return recv
 
 
@@ -175,13 +178,19 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         # 2. route ids to owners; owners catch their rows up (lazy Adam) and gather them
         st = self.exchange.request(unique)
         own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
+        own.grad_scale = 1.0 / self.exchange.world  # DDP gradient averaging, applied in the ordered row sums
         with torch.no_grad():
-            rows = ops.gather_sum(st.recv_local, shard.detach(), None, skip_zero=False) if len(st.recv_local) \
+            rows = ops.gather_rows(st.recv_local, shard.detach()) if len(st.recv_local) \
                 else shard.new_empty(0, shard.shape[1])
+        # the compact table stays in send order; the ids are remapped to it (no row permutation)
         compact = self.exchange.reply_rows(st, rows).requires_grad_(True)
-        compact._asme_table_grad = ops.TableGrad()
-        inv_seq, inv_pos, inv_neg = (req.inverse_of(x) for x in (input_seq, pos, neg))
+        inv_seq, inv_pos, inv_neg = (st.pos.index_select(0, req.inverse_of(x).reshape(-1)).view(x.shape)
+                                     for x in (input_seq, pos, neg))
         req.release()
+        # its gradient: the heads' contributions summed per compact row in a fixed order (no atomics, no zero fill)
+        cplan = ops.SparseTablePlan.identity(U, [inv_seq, inv_pos, inv_neg], compact.shape[1])
+        compact._asme_table_grad = ops.TableGrad()
+        compact._asme_table_grad.plan = cplan
         # 3. the model runs on the compact table
         emb = self.model._sequence_embedding_layer.item_embedding_layer
         meta = get_additional_meta_data(self.model, batch)
@@ -193,20 +202,23 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         finally:
             emb._table_override = None
         loss = self.loss_function(pos_logits, neg_logits, mask=input_seq.ne(self.item_tokenizer.pad_token_id))
-        self._pending = (st, own, compact)
+        self._pending = (st, own, compact, cplan)
         return {"loss": loss}
 
     @torch.no_grad()
     def after_backward(self):
         """route the compact table gradient to the owners and average the replicated gradients"""
-        st, own, compact = self._pending
+        st, own, compact, cplan = self._pending
         self._pending = None
         W = self.exchange.world
-        g = compact.grad if compact.grad is not None else torch.zeros_like(compact)
+        g = cplan.grad_rows[:compact.shape[0]]
+        if compact.grad is not None:  # a head without the plan path returned a dense gradient
+            g = g + compact.grad
         recv = self.exchange.push_grads(st, g)
+        cplan.release()
         shard = self.model.item_table()
         if len(st.recv_local):
-            own.add_rows(st.recv_local, recv.mul_(1.0 / W))  # ordered per-row sums (deterministic)
+            own.add_rows(st.recv_local, recv)  # ordered per-row sums x 1/W (deterministic)
         shard._asme_table_grad.plan = own
         dense = [p for p in self.model.parameters() if p is not shard and p.grad is not None]
         if dense and W > 1:
@@ -250,8 +262,8 @@ def catalog_ranks(exchange: RowShardExchange, hidden: torch.Tensor, targets: tor
     group, W, rank = exchange.group, exchange.world, exchange.rank
     uniq, inv = torch.unique(targets, return_inverse=True)
     st = exchange.request(uniq)
-    got = exchange.reply_rows(st, table_shard.index_select(0, st.recv_local))
-    tscore = ops.catalog_target_scores(hidden, got.index_select(0, inv))
+    got = exchange.reply_rows(st, table_shard.index_select(0, st.recv_local))  # send order
+    tscore = ops.catalog_target_scores(hidden, got.index_select(0, st.pos.index_select(0, inv)))
     h_all = _gather_queries(hidden, group)
     t_all = _gather_queries(targets.to(torch.int64), group)
     s_all = _gather_queries(tscore, group)

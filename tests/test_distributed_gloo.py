@@ -36,11 +36,12 @@ def _worker(rank, world, port, V, D, q):
         unique = torch.randperm(V, generator=gr)[: 17 + 5 * rank]     # this rank's distinct ids
         st = ex.request(unique)
         assert int((st.recv_local >= shard.shape[0]).sum()) == 0
-        rows = ex.reply_rows(st, shard[st.recv_local])
-        ok_rows = torch.equal(rows, table[unique])
+        rows = ex.reply_rows(st, shard[st.recv_local])                # send order: row j <-> unique[order[j]]
+        ok_rows = torch.equal(rows, table[unique[st.order]]) and torch.equal(rows[st.pos], table[unique])
+        ok_rows = ok_rows and bool((unique[st.order] % world == torch.sort(unique[st.order] % world).values).all())
         # gradient push: owners receive every requester's rows, averaged over ranks
         grad = torch.randn(len(unique), D, generator=gr)
-        recv = ex.push_grads(st, grad)
+        recv = ex.push_grads(st, grad[st.order])
         acc = torch.zeros_like(shard)
         acc.index_add_(0, st.recv_local, recv / world)
         # reference: every rank's (unique, grad) scattered into the full table, then sliced

@@ -505,3 +505,32 @@ def test_catalog_rank_and_topk(asme, dev, d, nq, V, with_bias):
     assert (idx == ref_i).float().mean() > 0.97
     # the returned scores are the fused scores of the returned items
     assert torch.allclose(vals, logits.gather(1, idx), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+@pytest.mark.parametrize("n", [1, 1023, 1025, 300001])
+def test_bucket_by_owner_matches_stable_argsort(asme, dev, world, n):
+    """asme_bucket_by_owner == torch's stable argsort by owner (bit-exact order, counts, owner-local rows)"""
+    g = torch.Generator(device="cpu").manual_seed(n + world)
+    unique = torch.randperm(10_000_003, generator=g)[:n].to(dev)
+    order, send_local, counts, pos = asme.ops.bucket_by_owner(unique, world)
+    owner = unique % world
+    ref = torch.argsort(owner, stable=True)
+    assert torch.equal(order, ref)
+    assert torch.equal(counts, torch.bincount(owner, minlength=world))
+    assert torch.equal(send_local, unique[ref] // world)
+    assert torch.equal(pos[order], torch.arange(n, device=dev))
+
+
+@pytest.mark.parametrize("D", [128, 64, 36])
+def test_gather_rows(asme, dev, D):
+    torch.manual_seed(D)
+    V = 5000
+    table = torch.randn(V, D, device=dev)
+    ids = torch.randint(0, V, (7777,), device=dev)
+    ids[5] = V + 3   # out of range -> zero row
+    ids[9] = -1
+    out = asme.ops.gather_rows(ids, table)
+    ok = (ids >= 0) & (ids < V)
+    assert torch.equal(out[ok], table[ids[ok]])
+    assert bool((out[~ok] == 0).all())

@@ -55,21 +55,26 @@ def test_ws_gelu_epilogues_match_row_kernels(asme, dev, p, M):
     w1 = torch.randn(Fd, D, device=dev) / D ** 0.5
     b1 = torch.randn(Fd, device=dev)
     seed = 987654321
-    pre = torch.empty(M, Fd, device=dev)
-    act = _call(asme, x, w1, Fd, 0, bias=b1, epi=1, pre_out=pre, p=p, seed=seed)
-    pre_ref = _call(asme, x, w1, Fd, 0, bias=b1)
-    assert torch.equal(pre, pre_ref)
+    fac = torch.empty(M, Fd, device=dev)
+    act = _call(asme, x, w1, Fd, 0, bias=b1, epi=1, pre_out=fac, p=p, seed=seed)
+    pre = _call(asme, x, w1, Fd, 0, bias=b1)
     act_ref = torch.empty_like(pre)
     L.call("asme_gelu_dropout_fwd", L.ptr(pre), pre.numel(), p, seed, L.ptr(act_ref), L.stream())
     assert torch.equal(act, act_ref)
-    # backward through the activation: (dY W2) * keep * GELU'(pre)
+    # the stored activation factor keep * GELU'(pre) == the row kernel's backward of a unit gradient (bitwise)
+    ones = torch.ones_like(pre)
+    fac_ref = torch.empty_like(pre)
+    L.call("asme_gelu_dropout_bwd", L.ptr(pre), L.ptr(ones), pre.numel(), p, seed, L.ptr(fac_ref), L.stream())
+    assert torch.equal(fac, fac_ref)
+    # backward through the activation: (dY W2) * factor; the row kernel rounds (g * keep) * GELU' instead
     w2 = torch.randn(D, Fd, device=dev) / Fd ** 0.5
     dy = torch.randn(M, D, device=dev)
-    d_pre = _call(asme, dy, w2, Fd, 1, epi=2, pre_in=pre, p=p, seed=seed)
+    d_pre = _call(asme, dy, w2, Fd, 1, epi=2, pre_in=fac, p=p, seed=seed)
     dg = _call(asme, dy, w2, Fd, 1)
     d_ref = torch.empty_like(pre)
     L.call("asme_gelu_dropout_bwd", L.ptr(pre), L.ptr(dg), pre.numel(), p, seed, L.ptr(d_ref), L.stream())
-    assert torch.equal(d_pre, d_ref)
+    assert torch.allclose(d_pre, d_ref, rtol=1e-6, atol=1e-30)
+    assert torch.equal(d_pre == 0, d_ref == 0)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.3])
