@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--table-grad", choices=["sparse", "dense"], default="sparse")
     ap.add_argument("--ids", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--producer", choices=["resident", "gpu"], default="resident",
+                    help="resident: two pre-built device batches; gpu: every step samples its batch from sessions "
+                         "in HBM with the GPU pos/neg sampler (asme_posneg_sample) inside the timed step")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -147,9 +150,26 @@ def main():
     module.train()
     opt = module.configure_optimizers()
     batches = [synthetic_batch(B, L, V, 1234 + 7 * (rank * 2 + i), dev, args.ids) for i in range(2)]
+    if args.producer == "gpu":
+        # sessions of L + 1 items in HBM; each step's batch (x, pos, sampled negatives) is built on the GPU
+        # inside the step (asme_posneg_sample), as the reference's DataLoader would produce it
+        n_sess = max(4 * B, 8192)
+        g = torch.Generator(device=dev).manual_seed(4321 + rank)
+        flat = torch.randint(3, V, (n_sess * (L + 1),), device=dev, generator=g)
+        store = asme.batches.SessionStore(flat, torch.arange(n_sess + 1, device=dev) * (L + 1))
+        sampler = asme.batches.PositiveNegativeSamplerProcessor(tok)
+        order = torch.randperm(n_sess, device=dev, generator=g)
+
+        def get_batch(i):
+            idx = order[(i * B) % (n_sess - B + 1):][:B]
+            b = sampler.process_batch(store, idx, L, seed=1000 + i)
+            return {k: b[k] for k in ("item", "positive_samples", "negative_samples")}
+    else:
+        def get_batch(i):
+            return batches[i % 2]
 
     for i in range(args.warmup):
-        step_fn(batches[i % 2], i)
+        step_fn(get_batch(i), i)
     torch.cuda.synchronize()
 
     # per-kernel device time of the dominant kernel (HIP events on the launching stream)
@@ -157,7 +177,7 @@ def main():
                                    "asme_embedding_fwd", "asme_embedding_bwd", "asme_lazy_adam_catch_up",
                                    "asme_lazy_adam_apply", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
-                                   "asme_ws_linear"])
+                                   "asme_ws_linear", "asme_posneg_sample"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -173,7 +193,7 @@ def main():
     asme.ops.SparseTablePlan.release = _release
     with timer:
         for i in range(args.steps):
-            step_fn(batches[i % 2], i)
+            step_fn(get_batch(args.warmup + i), i)
     # lazily deferred zero-gradient Adam updates of the item table are part of the work: apply them all
     # (exact dense-Adam state) inside the timed region, timed on its own
     f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -218,6 +238,8 @@ def main():
         "asme_lazy_adam_catch_up": ("hbm", U * 8 + 6 * U * d * 4 + 2 * U * 4),
         "asme_gelu_dropout_bwd": ("hbm", 3 * T * ffn * 4),
         "asme_adam_rows_step": ("hbm", 6 * V * d * 4 + V * 4 + U * d * 4),
+        # session items read once + x / pos / neg written (the in-session membership scans hit the cache)
+        "asme_posneg_sample": ("hbm", B * (L + 1) * 8 + 3 * B * L * 8 + B * 8),
     }
     # HBM traffic per launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE, gfx950
     # corrections of MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py) for this exact configuration
@@ -253,7 +275,7 @@ def main():
         "config": {"workload": "sasrec-neg train step", "model": "SASRec", "global_batch": B * world,
                    "batch_per_gpu": B, "seq_len": L, "items": args.items, "dim": d, "heads": args.heads,
                    "layers": args.layers, "dropout": args.dropout, "table_grad": args.table_grad,
-                   "ids": args.ids,
+                   "ids": args.ids, "producer": args.producer,
                    "parallelism": f"dp{world}+rowshard{world}" if sharded else "single"},
         "roofline": roof,
         "rooflines": rooflines,

@@ -192,6 +192,25 @@ int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap,
                          int32_t* last_step, float* param, float* exp_avg, float* exp_avg_sq, int64_t dim,
                          const float* hist, int64_t step, void* stream);
 
+/* ---- input producers: sessions in HBM as flat item ids + offsets (n_sessions + 1) ---------
+ * asme_session_batch: collate (data/collate.py:42-111): out (batch, seq_len) = the last min(len - drop_last,
+ *   seq_len) items of session batch_idx[b] (left truncation), pad after; out_len (nullable) = that count.
+ * asme_posneg_sample: PositiveNegativeSamplerProcessor (pos_neg_sampler.py:41-63,89-106) + collate: x = s[:-1],
+ *   pos = s[1:], neg uniform over ids in [0, vocab) that are neither special (<= 8 ids) nor in the session,
+ *   with replacement (Philox, seed); err_flag bit 0: no admissible id, bit 1: a session shorter than 2.
+ * asme_cloze_mask: ClozeMaskProcessor (cloze_mask.py:50-92) on a collated batch (items, lengths); draws_u
+ *   (batch, seq_len + 1) / draws_r (batch, seq_len) replay given draws (nullable: Philox, seed). */
+int asme_session_batch(const int64_t* flat, const int64_t* offsets, int64_t n_sessions, const int64_t* batch_idx,
+                       int64_t batch, int64_t seq_len, int64_t drop_last, int64_t pad, int64_t* out, int64_t* out_len,
+                       void* stream);
+int asme_posneg_sample(const int64_t* flat, const int64_t* offsets, int64_t n_sessions, const int64_t* batch_idx,
+                       int64_t batch, int64_t seq_len, int64_t vocab, const int64_t* special_ids, int n_special,
+                       int64_t pad, uint64_t seed, int64_t* x, int64_t* pos, int64_t* neg, int64_t* out_len,
+                       int* err_flag, void* stream);
+int asme_cloze_mask(const int64_t* items, const int64_t* lengths, int64_t batch, int64_t seq_len, int64_t vocab,
+                    int64_t pad, int64_t mask_id, double mask_prob, double last_prob, const float* draws_u,
+                    const int64_t* draws_r, uint64_t seed, int64_t* out, int64_t* target, void* stream);
+
 /* ---- id dedup & shard bucketing (row-sharded item table) ------------------------ */
 int64_t asme_dedup_workspace_bytes(int64_t n);
 int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_t* map, void* workspace,

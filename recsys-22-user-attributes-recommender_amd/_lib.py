@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASME_MI_LIB", os.path.join(_HERE, "libasme_mi.so"))
 
 p, i64, i32, f32, u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
+f64 = ctypes.c_double
 
 # name -> argument types (every function returns int status unless listed in _RESTYPES)
 SIGNATURES = {
@@ -83,6 +84,9 @@ SIGNATURES = {
     "asme_bucket_by_owner_workspace": [i64, i32],
     "asme_bucket_by_owner": [p, i64, i32, p, i64, p, p, p, p, p],
     "asme_gather_rows": [p, i64, p, i64, i64, p, p],
+    "asme_session_batch": [p, p, i64, p, i64, i64, i64, i64, p, p, p],
+    "asme_posneg_sample": [p, p, i64, p, i64, i64, i64, p, i32, i64, u64, p, p, p, p, p, p],
+    "asme_cloze_mask": [p, p, i64, i64, i64, i64, i64, f64, f64, p, p, u64, p, p, p],
 }
 _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64,
              "asme_linear_weight_grad_workspace": ctypes.c_int64,

@@ -56,3 +56,53 @@ def test_recall_and_mrr_host_path(asme):
     mrr = asme.metrics.MRRMetric(k=3)
     mrr.update(p, m)
     assert abs(float(mrr.compute()) - (1 / 3 + 1 / 2) / 2) < EPS
+
+
+# ---- input producers: the reference's own processor KATs (tests/test_cloze_mask.py,
+# tests/test_pos_neg.py, seed_everything(42) -> torch's CPU generator; the example vocabulary has 13 ids,
+# specials PAD=0 MASK=1 UNK=2), reproduced by the oracle's restatement of the processors
+def test_oracle_cloze_mask_reference_kats():
+    import torch
+    from oracle import asme_oracle as O
+    torch.manual_seed(42)
+    seq, tgt = O.cloze_mask([5, 8, 9, 7, 3, 4], 1.0, 1.0, 13)
+    assert seq == [5, 8, 9, 7, 3, 1] and tgt == [0] * 5 + [4]
+    torch.manual_seed(42)
+    seq, tgt = O.cloze_mask([5, 8, 9, 7, 3, 4, 12, 10, 11, 3], 0.5, 0.1, 13)
+    assert seq == [5, 1, 9, 1, 3, 1, 12, 10, 1, 3]
+    assert tgt == [0, 8, 0, 7, 0, 4, 0, 0, 11, 0]
+
+
+def test_oracle_pos_neg_reference_kat():
+    import torch
+    from oracle import asme_oracle as O
+    torch.manual_seed(42)
+    x, pos, neg = O.pos_neg([5, 8, 9, 7, 3, 4], 13, [0, 1, 2])
+    assert x == [5, 8, 9, 7, 3] and pos == [8, 9, 7, 3, 4] and neg == [6, 6, 6, 6, 11]
+
+
+def test_oracle_cloze_draws_replay():
+    """cloze_draws lays the generator's draws out per (session, position): applying the processor's decision
+    rule to that layout reproduces cloze_mask run on the generator itself (what asme_cloze_mask's replay mode
+    relies on)"""
+    import numpy as np
+    import torch
+    from oracle import asme_oracle as O
+    g = np.random.default_rng(0)
+    sessions = [[int(v) for v in g.integers(3, 50, size=int(n))] for n in g.integers(1, 30, size=60)]
+    torch.manual_seed(7)
+    ref = [O.cloze_mask(s, 0.3, 0.1, 50) for s in sessions]
+    torch.manual_seed(7)
+    u, r = O.cloze_draws([len(s) for s in sessions], 30, 0.3, 0.1, 50)
+    for b, s in enumerate(sessions):
+        out, tgt = list(s), [0] * len(s)
+        if float(u[b, 0]) <= 0.1:
+            out[-1], tgt[-1] = 1, s[-1]
+        else:
+            for i in range(len(s)):
+                p = float(u[b, 1 + i])
+                if p < 0.3:
+                    q = p / 0.3
+                    out[i] = 1 if q < 0.8 else (int(r[b, i]) if q < 0.9 else s[i])
+                    tgt[i] = s[i]
+        assert (out, tgt) == ref[b], b
