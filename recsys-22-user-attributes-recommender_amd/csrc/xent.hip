@@ -97,12 +97,23 @@ __device__ __forceinline__ void tile_times_rows(const float* __restrict__ tile, 
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int sub = 0; sub < kNS; ++sub) acc[t][sub] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // two-stage register ring for the LDS row reads (step s4+1 issued before step s4's MFMAs): bounded
+    // register use (the fully unrolled loop otherwise keeps every step's reads live) and the LDS latency
+    // off the MFMA stream
+    float4 ab[2][kNS];
+    const float* base = tile + c16 * S + g * DQ;
+#pragma unroll
+    for (int sub = 0; sub < kNS; ++sub) ab[0][sub] = *reinterpret_cast<const float4*>(base + sub * 16 * S);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s4 = 0; s4 < DQ / 4; ++s4) {
-        float4 a[kNS];
+        if (s4 + 1 < DQ / 4) {
 #pragma unroll
-        for (int sub = 0; sub < kNS; ++sub)
-            a[sub] = *reinterpret_cast<const float4*>(tile + (sub * 16 + c16) * S + g * DQ + 4 * s4);
+            for (int sub = 0; sub < kNS; ++sub)
+                ab[(s4 + 1) & 1][sub] = *reinterpret_cast<const float4*>(base + sub * 16 * S + 4 * (s4 + 1));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float4(&a)[kNS] = ab[s4 & 1];
         // consecutive MFMAs write different accumulators (dependent latency 40 > issue 32 cycles)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
