@@ -101,5 +101,13 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
     const float pdf = 0.3989422804014327f * expf(-0.5f * x * x);
     return cdf + x * pdf;
 }
+// both of the above from one erf evaluation (bitwise equal to calling them separately)
+__device__ __forceinline__ void gelu_erf_and_grad(float x, float& gelu, float& grad) {
+    const float e = erff(x * 0.70710678118654752f);
+    gelu = 0.5f * x * (1.0f + e);
+    const float cdf = 0.5f * (1.0f + e);
+    const float pdf = 0.3989422804014327f * expf(-0.5f * x * x);
+    grad = cdf + x * pdf;
+}
 
 }  // namespace asme

@@ -144,11 +144,13 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                 for (int i = 0; i < 4; ++i) u[i] = u[i] >= ep.p ? keep_k : 0.f;
             }
             // the backward's whole activation factor keep * GELU'(pre), so its epilogue is one multiply
-            bstore(make_float4(u[0] * gelu_erf_grad(v.x), u[1] * gelu_erf_grad(v.y), u[2] * gelu_erf_grad(v.z),
-                               u[3] * gelu_erf_grad(v.w)),
-                   pr, off);
-            v = make_float4(gelu_erf(v.x) * u[0], gelu_erf(v.y) * u[1], gelu_erf(v.z) * u[2], gelu_erf(v.w) * u[3]);
-            bstore(v, yr, off);
+            float gl[4], gd[4];
+            gelu_erf_and_grad(v.x, gl[0], gd[0]);
+            gelu_erf_and_grad(v.y, gl[1], gd[1]);
+            gelu_erf_and_grad(v.z, gl[2], gd[2]);
+            gelu_erf_and_grad(v.w, gl[3], gd[3]);
+            bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off);
+            bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off);
         } else {
             const float4 f = pre[ct];
             bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off);
