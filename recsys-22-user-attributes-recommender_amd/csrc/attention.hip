@@ -583,7 +583,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
 // per-tile barriers, each K/V row is read from HBM once per head (not once per 64-query block), and
 // fully-masked 16-key sub-tiles are skipped.  Used when 2 * ceil(L/16)*16 * (dk+4) * 4 B fits the
 // 160 KiB LDS (L <= 300 at dk = 64); the streaming kernels above cover the rest.
-constexpr int kResThreads = 512;
+#ifndef ASME_RES_THREADS
+#define ASME_RES_THREADS 768  // 12 waves: 3 per SIMD (512: 245/605 us fwd/bwd, 768: 231/588)
+#endif
+constexpr int kResThreads = ASME_RES_THREADS;  // forward and dQ passes
+constexpr int kResThreadsKV = 512;             // dK/dV pass: 168+ VGPRs, 12 waves would spill
 
 __host__ __device__ inline int res_rows(int L) { return (L + 15) & ~15; }
 inline size_t res_lds_bytes(int L, int DK, bool with_stats) {
@@ -592,25 +596,25 @@ inline size_t res_lds_bytes(int L, int DK, bool with_stats) {
 }
 
 // rows [0, Lp) of two (L x DK) operands into padded LDS images (rows >= L zeroed); 8 float4 in flight
-template <int DK>
+template <int DK, int NT = kResThreads>
 __device__ __forceinline__ void load_pair_resident(const float* __restrict__ a, int64_t lda,
                                                    const float* __restrict__ b, int64_t ldb, int L, int Lp,
                                                    float* __restrict__ As, float* __restrict__ Bs) {
     constexpr int C4 = DK / 4, S = DK + 4;
     const int n4 = Lp * C4;
     // all loads of a batch are issued before the first store: at L = 200, dk = 64 one batch covers the head
-    for (int base = threadIdx.x; base < n4; base += kResThreads * 8) {
+    for (int base = threadIdx.x; base < n4; base += NT * 8) {
         float4 ra[8], rb[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int idx = base + u * kResThreads, row = idx / C4, c = (idx % C4) * 4;
+            const int idx = base + u * NT, row = idx / C4, c = (idx % C4) * 4;
             const bool ok = idx < n4 && row < L;
             ra[u] = ok ? *reinterpret_cast<const float4*>(a + (int64_t)row * lda + c) : make_float4(0.f, 0.f, 0.f, 0.f);
             rb[u] = ok ? *reinterpret_cast<const float4*>(b + (int64_t)row * ldb + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int idx = base + u * kResThreads, row = idx / C4, c = (idx % C4) * 4;
+            const int idx = base + u * NT, row = idx / C4, c = (idx % C4) * 4;
             if (idx < n4) {
                 *reinterpret_cast<float4*>(As + row * S + c) = ra[u];
                 *reinterpret_cast<float4*>(Bs + row * S + c) = rb[u];
@@ -842,6 +846,14 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dq_res_kernel(
         auto chunk = [&](auto ns_tag, int k0) {
             constexpr int NS = decltype(ns_tag)::value;
             floatx4 st[NS], dpt[NS];
+            // the chunk's stored dropout decisions are requested before its MFMAs (their latency hides there)
+            uint32_t mb[NS];
+#pragma unroll
+            for (int sub = 0; sub < NS; ++sub) {
+                const int key4 = k0 + sub * 16 + 4 * g;
+                mb[sub] = (p_drop > 0.f && drop_mask && key4 < L) ? drop_mask[drow * L4 + key4 / 4] : 0u;
+            }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int sub = 0; sub < NS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
             rows_times_slice<DK, NS>(Ks + k0 * S, g, c16, qf, st);
@@ -852,8 +864,7 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dq_res_kernel(
                 float4 f = make_float4(1.f, 1.f, 1.f, 1.f);
                 const int key4 = k0 + sub * 16 + 4 * g;
                 if (p_drop > 0.f)
-                    f = drop_mask ? bits_keep(key4 < L ? drop_mask[drow * L4 + key4 / 4] : (uint8_t)0, p_drop)
-                                  : attn_keep4(seed, drow, key4, p_drop);
+                    f = drop_mask ? bits_keep((uint8_t)mb[sub], p_drop) : attn_keep4(seed, drow, key4, p_drop);
                 const uint32_t vb = valid_bits4(kvw, k0 + sub * 16, g);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -884,7 +895,7 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dq_res_kernel(
 }
 
 template <int DK>
-__global__ __launch_bounds__(kResThreads) void attn_bwd_dkdv_res_kernel(
+__global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
     int64_t ldv, const float* __restrict__ dout, int64_t lddo, const float* __restrict__ stats,
     const float* __restrict__ dsum, float* __restrict__ dk, int64_t lddk, float* __restrict__ dv, int64_t lddv,
@@ -906,8 +917,9 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dkdv_res_kernel(
     const int64_t tok0 = (int64_t)b * L;
 
     stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
-    load_pair_resident<DK>(q + tok0 * ldq + h * DK, ldq, dout + tok0 * lddo + h * DK, lddo, L, Lp, Qs, Ds);
-    for (int i = threadIdx.x; i < Lp; i += kResThreads) {
+    load_pair_resident<DK, kResThreadsKV>(q + tok0 * ldq + h * DK, ldq, dout + tok0 * lddo + h * DK, lddo, L, Lp, Qs,
+                                          Ds);
+    for (int i = threadIdx.x; i < Lp; i += kResThreadsKV) {
         const bool ok = i < L;
         mx_s[i] = ok ? stats[((int64_t)bh * L + i) * 2] : 0.f;
         il_s[i] = ok ? stats[((int64_t)bh * L + i) * 2 + 1] : 0.f;
@@ -943,6 +955,12 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dkdv_res_kernel(
             auto chunk = [&](auto ns_tag, int qb) {
                 constexpr int NS = decltype(ns_tag)::value;
                 floatx4 st[NS], dpt[NS];
+                // the chunk's key-major dropout words are requested before its MFMAs
+                uint32_t mwv[NS];
+#pragma unroll
+                for (int sub = 0; sub < NS; ++sub)
+                    mwv[sub] = (p_drop > 0.f && drop_mask) ? keyw_key[((qb >> 4) + sub) * kstride] : 0u;
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int sub = 0; sub < NS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
                 rows_times_slice<DK, NS>(Qs + qb * S, g, c16, kf, st);
@@ -954,7 +972,7 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dkdv_res_kernel(
                     const float4 mx4 = *reinterpret_cast<const float4*>(mx_s + q4);
                     const float4 il4 = *reinterpret_cast<const float4*>(il_s + q4);
                     const float4 ds4 = *reinterpret_cast<const float4*>(dsum_s + q4);
-                    const uint32_t mw = (p_drop > 0.f && drop_mask) ? keyw_key[((qb >> 4) + sub) * kstride] >> (4 * g) : 0u;
+                    const uint32_t mw = mwv[sub] >> (4 * g);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int qq = q4 + r;
@@ -1067,7 +1085,7 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
             hipLaunchKernelGGL(attn_bwd_dq_res_kernel<DK>, rgrid, dim3(kResThreads), lds_dq, s, q, k, v, ld_q, ld_k,
                                ld_v, out, ld_out, dout, ld_dout, lse, dsum_ws, dq, ld_dq, key_valid, (int)heads,
                                (int)seq_len, causal, scale, p_drop, seed, drop_mask);
-            hipLaunchKernelGGL(attn_bwd_dkdv_res_kernel<DK>, rgrid, dim3(kResThreads), lds_kv, s, q, k, v, ld_q, ld_k,
+            hipLaunchKernelGGL(attn_bwd_dkdv_res_kernel<DK>, rgrid, dim3(kResThreadsKV), lds_kv, s, q, k, v, ld_q, ld_k,
                                ld_v, dout, ld_dout, lse, dsum_ws, dk, ld_dk, dv, ld_dv, key_valid, (int)heads,
                                (int)seq_len, causal, scale, p_drop, seed, drop_mask);
         } else {
