@@ -29,6 +29,9 @@ PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=["sasrec-neg", "bert4rec"], default="sasrec-neg",
+                    help="sasrec-neg: the headline (BASELINE C4 at N=1); bert4rec: BASELINE C3, cloze-masked BERT4Rec "
+                         "with the full-catalogue softmax (--items 27000), batches built by the GPU cloze producer")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1024, help="sequences per GPU")
@@ -106,6 +109,102 @@ def cpu_baseline(args, V):
                       f"{cpu_name}"}
 
 
+def bench_bert4rec(args, asme, dev, world, rank):
+    """BASELINE config C3: BERT4Rec (tied head), cloze masking p = 0.2 / last-item-only 0.1, B per GPU, full
+    catalogue CE over |V| = items + 3.  Every step builds its batch on the GPU (collate + asme_cloze_mask) from
+    sessions in HBM inside the timed region; data parallel over ranks (flat all_reduce of the gradients)."""
+    V = args.items + 3
+    B, L, d = args.batch, args.seq_len, args.dim
+    with torch.device(dev):
+        model = asme.BERT4RecModel(transformer_hidden_size=d, num_transformer_heads=args.heads,
+                                   num_transformer_layers=args.layers, item_vocab_size=V, max_seq_length=L,
+                                   transformer_dropout=args.dropout)
+    tok = asme.tokenization.Tokenizer(args.items)
+    module = asme.MaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None)
+    module.train()
+    opt, sched = asme.modules.split_optimizers(module.configure_optimizers())
+    n_sess = max(4 * B, 8192)
+    g = torch.Generator(device=dev).manual_seed(4321 + rank)
+    flat = torch.randint(3, V, (n_sess * L,), device=dev, generator=g)
+    store = asme.batches.SessionStore(flat, torch.arange(n_sess + 1, device=dev) * L)
+    cloze = asme.batches.ClozeMaskProcessor(tok, 0.2, 0.1)
+    order = torch.randperm(n_sess, device=dev, generator=g)
+    params = [p for p in model.parameters() if p.requires_grad]
+
+    def step(i):
+        idx = order[(i * B) % (n_sess - B + 1):][:B]
+        items, lengths = asme.batches.padded_session_batch(store, idx, L)
+        batch = cloze.process_batch(items, lengths, seed=1000 + i)
+        loss = module.training_step(batch, i)["loss"]
+        loss.backward()
+        if world > 1:
+            flat_g = torch.cat([p.grad.reshape(-1) for p in params])
+            dist.all_reduce(flat_g)
+            flat_g.mul_(1.0 / world)
+            off = 0
+            for p in params:
+                p.grad.copy_(flat_g[off:off + p.numel()].view_as(p.grad))
+                off += p.numel()
+        opt.step()
+        sched.step()
+        opt.zero_grad(set_to_none=True)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    timer = asme._lib.KernelTimer(["asme_attention_fwd", "asme_attention_bwd", "asme_ws_linear",
+                                   "asme_linear_weight_grad", "asme_cross_entropy_fwd", "asme_cross_entropy_bwd",
+                                   "asme_linear_xent_fwd", "asme_linear_xent_bwd", "asme_cloze_mask",
+                                   "asme_residual_ln_fwd", "asme_residual_ln_bwd"])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with timer:
+        for i in range(args.steps):
+            step(args.warmup + i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    T, H, dk = B * L, args.heads, d // args.heads
+    pairs = B * H * L * L  # bidirectional
+    wg_flops = 2.0 * T * (3 * d * d + d * d + 4 * d * d + 4 * d * d)
+    M = 0.9 * 0.2 * T + 0.1 * B  # expected non-ignored rows of a cloze batch (SURVEY §8d)
+    work = {"asme_attention_fwd": ("mfma", 4.0 * pairs * dk), "asme_attention_bwd": ("mfma", 10.0 * pairs * dk),
+            "asme_ws_linear": ("mfma", 2 * wg_flops / 8), "asme_linear_weight_grad": ("mfma", wg_flops / 4),
+            "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
+            "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0)}
+    rooflines = []
+    for name, st in timer.summary().items():
+        if not st["count"] or name not in work:
+            continue
+        bound, amount = work[name]
+        secs = st["avg_ms"] / 1e3
+        ach, peak, unit = ((amount / secs / 1e12, PEAK_FP32_MFMA_TFS, "TFLOP/s") if bound == "mfma"
+                           else (amount / secs / 1e9, PEAK_HBM_GBS, "GB/s"))
+        rooflines.append({"kernel": name, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                          "frac": round(ach / peak, 4), "traffic": None, "avg_ms": round(st["avg_ms"], 4),
+                          "launches": st["count"], "total_ms": round(st["total_ms"], 3)})
+    rooflines.sort(key=lambda r: -r["total_ms"])
+    result = {"metric": f"training sequences/sec (BERT4Rec cloze, B={B} L={L} |V|={V}, fwd+bwd+Adam)",
+              "value": round(B * world * args.steps / elapsed, 2), "unit": "sequences/s", "n_gpus": world,
+              "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
+              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+              "data": "synthetic sessions, GPU cloze masking inside the step, random-init weights",
+              "config": {"workload": "bert4rec cloze train step (BASELINE C3)", "model": "BERT4Rec",
+                         "global_batch": B * world, "batch_per_gpu": B, "seq_len": L, "items": args.items,
+                         "dim": d, "heads": H, "layers": args.layers, "dropout": args.dropout,
+                         "fused_xent": asme.modules.FUSED_XENT, "parallelism": f"dp{world}"},
+              "roofline": rooflines[0] if rooflines else None, "rooflines": rooflines, "cpu_baseline": None}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,6 +228,8 @@ def main():
     B, L, d = args.batch, args.seq_len, args.dim
 
     torch.manual_seed(rank)
+    if args.workload == "bert4rec":
+        return bench_bert4rec(args, asme, dev, world, rank)
     sharded = world > 1 or args.sharded
     # N > 1: the item table is row-sharded over the ranks (RCCL all-to-all of ids / rows / row grads,
     # one all_reduce of the replicated dense gradients); N = 1: the whole table on the one GPU

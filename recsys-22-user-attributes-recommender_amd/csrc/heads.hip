@@ -171,15 +171,35 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ l
     const float* x = logits + r * ld;
     const int64_t tg = targets[r];
     float m = -INFINITY, s = 0.f;
-    for (int64_t j = threadIdx.x; j < V; j += blockDim.x) {
-        const float v = x[j];
+    auto add1 = [&](float v) {
         if (v > m) {
             s = s * __expf(m - v) + 1.f;
             m = v;
         } else {
             s += __expf(v - m);
         }
+    };
+    // rows of an odd-length catalogue are not 16-B aligned: a scalar head, float4 body (two in flight), tail
+    const int64_t head = min(V, (int64_t)(((16 - ((uintptr_t)x & 15)) & 15) >> 2));
+    if (threadIdx.x < head) add1(x[threadIdx.x]);
+    const float4* x4 = reinterpret_cast<const float4*>(x + head);
+    const int64_t n4 = (V - head) >> 2;
+    auto add4 = [&](const float4& v) {
+        const float mx = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
+        if (mx > m) {
+            s *= __expf(m - mx);
+            m = mx;
+        }
+        s += (__expf(v.x - m) + __expf(v.y - m)) + (__expf(v.z - m) + __expf(v.w - m));
+    };
+    int64_t j = threadIdx.x;
+    for (; j + blockDim.x < n4; j += 2 * blockDim.x) {
+        const float4 a = x4[j], b = x4[j + blockDim.x];
+        add4(a);
+        add4(b);
     }
+    if (j < n4) add4(x4[j]);
+    for (int64_t k = head + 4 * n4 + threadIdx.x; k < V; k += blockDim.x) add1(x[k]);
     // wave-level merge
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -242,7 +262,26 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ l
     const float l = lse[r];
     const float* x = logits + r * ld;
     float* y = dlogits + r * ldg;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < V; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((((uintptr_t)x ^ (uintptr_t)y) & 15) == 0) {  // same alignment: scalar head, float4 body, scalar tail
+        const int64_t head = min(V, (int64_t)(((16 - ((uintptr_t)x & 15)) & 15) >> 2));
+        for (int64_t j = t0; j < head; j += stride) y[j] = scale * (__expf(x[j] - l) - (j == tg ? 1.f : 0.f));
+        const float4* x4 = reinterpret_cast<const float4*>(x + head);
+        float4* y4 = reinterpret_cast<float4*>(y + head);
+        const int64_t n4 = (V - head) >> 2;
+        for (int64_t j = t0; j < n4; j += stride) {
+            const float4 v = x4[j];
+            const int64_t c = head + 4 * j;
+            y4[j] = make_float4(scale * (__expf(v.x - l) - (c == tg ? 1.f : 0.f)),
+                                scale * (__expf(v.y - l) - (c + 1 == tg ? 1.f : 0.f)),
+                                scale * (__expf(v.z - l) - (c + 2 == tg ? 1.f : 0.f)),
+                                scale * (__expf(v.w - l) - (c + 3 == tg ? 1.f : 0.f)));
+        }
+        for (int64_t j = head + 4 * n4 + t0; j < V; j += stride)
+            y[j] = scale * (__expf(x[j] - l) - (j == tg ? 1.f : 0.f));
+        return;
+    }
+    for (int64_t j = t0; j < V; j += stride) {
         const float pj = __expf(x[j] - l);
         y[j] = scale * (pj - (j == tg ? 1.f : 0.f));
     }
@@ -350,7 +389,7 @@ ASME_API int asme_cross_entropy_bwd(const float* logits, int64_t ld, const float
                                     const float* stats, float* dlogits, int64_t ld_dlogits, void* stream) {
     ASME_CHECK_ARG(logits && lse && targets && dloss && stats && dlogits, "asme_cross_entropy_bwd: null pointer");
     if (n_rows == 0) return 0;
-    const int64_t bx = std::min<int64_t>((n_classes + 1023) / 1024, 64);
+    const int64_t bx = std::min<int64_t>((n_classes + 4095) / 4096, 64);  // ~4 float4 per thread
     hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)bx, (unsigned)n_rows), dim3(256), 0, (hipStream_t)stream,
                        logits, ld, lse, targets, ignore_index, n_classes, dloss, stats, dlogits, ld_dlogits);
     ASME_LAUNCH_CHECK("asme_cross_entropy_bwd");
