@@ -29,9 +29,10 @@ PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=["sasrec-neg", "bert4rec"], default="sasrec-neg",
+    ap.add_argument("--workload", choices=["sasrec-neg", "bert4rec", "kebert4rec"], default="sasrec-neg",
                     help="sasrec-neg: the headline (BASELINE C4 at N=1); bert4rec: BASELINE C3, cloze-masked BERT4Rec "
-                         "with the full-catalogue softmax (--items 27000), batches built by the GPU cloze producer")
+                         "with the full-catalogue softmax (--items 27000), batches built by the GPU cloze producer; "
+                         "kebert4rec: BASELINE C5 (--items 13000), a synthetic per-item category side attribute")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1024, help="sequences per GPU")
@@ -115,10 +116,20 @@ def bench_bert4rec(args, asme, dev, world, rank):
     sessions in HBM inside the timed region; data parallel over ranks (flat all_reduce of the gradients)."""
     V = args.items + 3
     B, L, d = args.batch, args.seq_len, args.dim
+    kebert = args.workload == "kebert4rec"
+    n_genre = 64  # synthetic side attribute: category of the item, content_embedding (SURVEY §8 C5)
     with torch.device(dev):
-        model = asme.BERT4RecModel(transformer_hidden_size=d, num_transformer_heads=args.heads,
-                                   num_transformer_layers=args.layers, item_vocab_size=V, max_seq_length=L,
-                                   transformer_dropout=args.dropout)
+        if kebert:
+            model = asme.KeBERT4RecModel(transformer_hidden_size=d, num_transformer_heads=args.heads,
+                                         num_transformer_layers=args.layers, item_vocab_size=V, max_seq_length=L,
+                                         transformer_dropout=args.dropout,
+                                         prefusion_attributes={"genre": {"embedding_type": "content_embedding"}},
+                                         additional_attributes_tokenizer={
+                                             "tokenizers.genre": asme.tokenization.Tokenizer(n_genre - 3)})
+        else:
+            model = asme.BERT4RecModel(transformer_hidden_size=d, num_transformer_heads=args.heads,
+                                       num_transformer_layers=args.layers, item_vocab_size=V, max_seq_length=L,
+                                       transformer_dropout=args.dropout)
     tok = asme.tokenization.Tokenizer(args.items)
     module = asme.MaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None)
     module.train()
@@ -135,6 +146,8 @@ def bench_bert4rec(args, asme, dev, world, rank):
         idx = order[(i * B) % (n_sess - B + 1):][:B]
         items, lengths = asme.batches.padded_session_batch(store, idx, L)
         batch = cloze.process_batch(items, lengths, seed=1000 + i)
+        if kebert:
+            batch["genre"] = torch.where(items > 0, items % (n_genre - 1) + 1, 0)
         loss = module.training_step(batch, i)["loss"]
         loss.backward()
         if world > 1:
@@ -189,12 +202,14 @@ def bench_bert4rec(args, asme, dev, world, rank):
                           "frac": round(ach / peak, 4), "traffic": None, "avg_ms": round(st["avg_ms"], 4),
                           "launches": st["count"], "total_ms": round(st["total_ms"], 3)})
     rooflines.sort(key=lambda r: -r["total_ms"])
-    result = {"metric": f"training sequences/sec (BERT4Rec cloze, B={B} L={L} |V|={V}, fwd+bwd+Adam)",
+    name = "KeBERT4Rec" if kebert else "BERT4Rec"
+    result = {"metric": f"training sequences/sec ({name} cloze, B={B} L={L} |V|={V}, fwd+bwd+Adam)",
               "value": round(B * world * args.steps / elapsed, 2), "unit": "sequences/s", "n_gpus": world,
               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
               "data": "synthetic sessions, GPU cloze masking inside the step, random-init weights",
-              "config": {"workload": "bert4rec cloze train step (BASELINE C3)", "model": "BERT4Rec",
+              "config": {"workload": ("kebert4rec cloze train step (BASELINE C5)" if kebert
+                                      else "bert4rec cloze train step (BASELINE C3)"), "model": name,
                          "global_batch": B * world, "batch_per_gpu": B, "seq_len": L, "items": args.items,
                          "dim": d, "heads": H, "layers": args.layers, "dropout": args.dropout,
                          "fused_xent": asme.modules.FUSED_XENT, "parallelism": f"dp{world}"},
@@ -228,7 +243,7 @@ def main():
     B, L, d = args.batch, args.seq_len, args.dim
 
     torch.manual_seed(rank)
-    if args.workload == "bert4rec":
+    if args.workload in ("bert4rec", "kebert4rec"):
         return bench_bert4rec(args, asme, dev, world, rank)
     sharded = world > 1 or args.sharded
     # N > 1: the item table is row-sharded over the ranks (RCCL all-to-all of ids / rows / row grads,
