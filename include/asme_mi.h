@@ -203,6 +203,11 @@ int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap,
 int asme_session_batch(const int64_t* flat, const int64_t* offsets, int64_t n_sessions, const int64_t* batch_idx,
                        int64_t batch, int64_t seq_len, int64_t drop_last, int64_t pad, int64_t* out, int64_t* out_len,
                        void* stream);
+/* asme_position_batch: (session, target_pos) pairs of a position index (data/datasets/index.py): out = the last
+ *   min(pos, seq_len) items before pos (right-padded), target = s[pos]; err_flag bit 0: a pair outside its session */
+int asme_position_batch(const int64_t* flat, const int64_t* offsets, int64_t n_sessions, const int64_t* pairs,
+                        int64_t batch, int64_t seq_len, int64_t pad, int64_t* out, int64_t* out_len, int64_t* target,
+                        int* err_flag, void* stream);
 int asme_posneg_sample(const int64_t* flat, const int64_t* offsets, int64_t n_sessions, const int64_t* batch_idx,
                        int64_t batch, int64_t seq_len, int64_t vocab, const int64_t* special_ids, int n_special,
                        int64_t pad, uint64_t seed, int64_t* x, int64_t* pos, int64_t* neg, int64_t* out_len,

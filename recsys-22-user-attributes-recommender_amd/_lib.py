@@ -85,6 +85,7 @@ SIGNATURES = {
     "asme_bucket_by_owner": [p, i64, i32, p, i64, p, p, p, p, p],
     "asme_gather_rows": [p, i64, p, i64, i64, p, p],
     "asme_session_batch": [p, p, i64, p, i64, i64, i64, i64, p, p, p],
+    "asme_position_batch": [p, p, i64, p, i64, i64, i64, p, p, p, p, p],
     "asme_posneg_sample": [p, p, i64, p, i64, i64, i64, p, i32, i64, u64, p, p, p, p, p, p],
     "asme_cloze_mask": [p, p, i64, i64, i64, i64, i64, f64, f64, p, p, u64, p, p, p],
 }

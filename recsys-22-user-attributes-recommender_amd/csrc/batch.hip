@@ -46,6 +46,30 @@ __global__ __launch_bounds__(256) void session_batch_kernel(const int64_t* __res
     if (threadIdx.x == 0 && out_len) out_len[b] = n;
 }
 
+// (session, target position) pairs of ASME's position indices (data/datasets/index.py; LOO / next-item splits):
+// SequencePositionDataset truncates the session to [:pos + 1] (sequence_position.py:50-58) and the target extractor
+// splits off the last item (target_extractor.py:41-70): out = the last min(pos, L) items before pos, target = s[pos]
+__global__ __launch_bounds__(256) void position_batch_kernel(const int64_t* __restrict__ flat,
+                                                             const int64_t* __restrict__ offsets, int64_t n_sessions,
+                                                             const int64_t* __restrict__ pairs, int64_t B, int64_t L,
+                                                             int64_t pad, int64_t* __restrict__ out,
+                                                             int64_t* __restrict__ out_len,
+                                                             int64_t* __restrict__ target, int* __restrict__ err) {
+    const int64_t b = blockIdx.x;
+    if (b >= B) return;
+    const int64_t s = pairs[2 * b], p = pairs[2 * b + 1];
+    const bool ok = s >= 0 && s < n_sessions && p >= 0 && p < offsets[s + 1] - offsets[s];
+    if (!ok && threadIdx.x == 0 && err) atomicOr(err, 1);
+    const int64_t beg = ok ? offsets[s] : 0;
+    const int64_t n = ok ? (p < L ? p : L) : 0;
+    const int64_t first = beg + p - n;
+    for (int64_t i = threadIdx.x; i < L; i += blockDim.x) out[b * L + i] = i < n ? flat[first + i] : pad;
+    if (threadIdx.x == 0) {
+        if (out_len) out_len[b] = n;
+        if (target) target[b] = ok ? flat[beg + p] : pad;
+    }
+}
+
 // ------------------------------------------------------------------------------------- pos / neg sampler
 // One wave per session.  x, pos: the collated s[:-1], s[1:]; neg: for each kept position one id drawn uniformly
 // from [0, V) and redrawn (next Philox counter) while it is special or occurs ANYWHERE in the full session (the
@@ -178,6 +202,17 @@ ASME_API int asme_session_batch(const int64_t* flat, const int64_t* offsets, int
     hipLaunchKernelGGL(session_batch_kernel, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, flat, offsets,
                        n_sessions, batch_idx, batch, seq_len, drop_last, pad, out, out_len);
     ASME_LAUNCH_CHECK("asme_session_batch");
+}
+
+ASME_API int asme_position_batch(const int64_t* flat, const int64_t* offsets, int64_t n_sessions,
+                                 const int64_t* pairs, int64_t batch, int64_t seq_len, int64_t pad, int64_t* out,
+                                 int64_t* out_len, int64_t* target, int* err_flag, void* stream) {
+    ASME_CHECK_ARG(flat && offsets && pairs && out, "asme_position_batch: null pointer");
+    ASME_CHECK_ARG(seq_len >= 1 && batch >= 0, "asme_position_batch: bad shape");
+    if (batch == 0) return 0;
+    hipLaunchKernelGGL(position_batch_kernel, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, flat, offsets,
+                       n_sessions, pairs, batch, seq_len, pad, out, out_len, target, err_flag);
+    ASME_LAUNCH_CHECK("asme_position_batch");
 }
 
 ASME_API int asme_posneg_sample(const int64_t* flat, const int64_t* offsets, int64_t n_sessions,
