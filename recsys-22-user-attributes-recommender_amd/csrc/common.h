@@ -95,19 +95,40 @@ __device__ __forceinline__ float dropout_factor(uint64_t seed, uint32_t salt, ui
     return v >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-    const float pdf = 0.3989422804014327f * expf(-0.5f * x * x);
-    return cdf + x * pdf;
-}
-// both of the above from one erf evaluation (bitwise equal to calling them separately)
+// GELU(x) = x * Phi(x), Phi(x) = 0.5 * (1 + erf(x / sqrt 2)) (nn.GELU(), the exact-erf form the reference uses) and
+// its derivative Phi(x) + x * phi(x).  Phi from erfc: erfc(a) = t * exp(-a^2 + P(t)), t = 1 / (1 + a / 2) (the
+// Chebyshev fit of Numerical Recipes, fractional error < 1.2e-7 everywhere, so the negative tail keeps its
+// RELATIVE accuracy), 1 + erf(z) = 2 - erfc(z) for z >= 0 and erfc(-z) below: one reciprocal, two exponentials
+// and ten FMAs per element for both values -- the FFN epilogues evaluate it for all T x 4d activations and are
+// VALU-bound on libm's erff (56 instructions for the pair, 22 here).
 __device__ __forceinline__ void gelu_erf_and_grad(float x, float& gelu, float& grad) {
-    const float e = erff(x * 0.70710678118654752f);
-    gelu = 0.5f * x * (1.0f + e);
-    const float cdf = 0.5f * (1.0f + e);
-    const float pdf = 0.3989422804014327f * expf(-0.5f * x * x);
-    grad = cdf + x * pdf;
+    const float z = x * 0.70710678118654752f;
+    const float a = fabsf(z);
+    const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * a);
+    float p = 0.17087277f;
+    p = fmaf(p, t, -0.82215223f);
+    p = fmaf(p, t, 1.48851587f);
+    p = fmaf(p, t, -1.13520398f);
+    p = fmaf(p, t, 0.27886807f);
+    p = fmaf(p, t, -0.18628806f);
+    p = fmaf(p, t, 0.09678418f);
+    p = fmaf(p, t, 0.37409196f);
+    p = fmaf(p, t, 1.00002368f);
+    p = fmaf(p, t, -1.26551223f);
+    const float erfc_a = t * __expf(fmaf(-a, a, p));
+    const float cdf = 0.5f * (z >= 0.f ? 2.0f - erfc_a : erfc_a);
+    gelu = x * cdf;
+    grad = fmaf(x * 0.3989422804014327f, __expf(-0.5f * x * x), cdf);
+}
+__device__ __forceinline__ float gelu_erf(float x) {
+    float g, d;
+    gelu_erf_and_grad(x, g, d);
+    return g;
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+    float g, d;
+    gelu_erf_and_grad(x, g, d);
+    return d;
 }
 
 }  // namespace asme

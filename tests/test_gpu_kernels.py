@@ -534,3 +534,29 @@ def test_gather_rows(asme, dev, D):
     ok = (ids >= 0) & (ids < V)
     assert torch.equal(out[ok], table[ids[ok]])
     assert bool((out[~ok] == 0).all())
+
+
+def test_gelu_pair_precision(asme, dev):
+    """GELU and GELU' (common.h gelu_erf_and_grad, erfc-based) vs float64 exact erf over [-12, 12]: elementwise
+    relative error, the negative tail included (where a naive 1 + erf would lose every digit)"""
+    x = torch.linspace(-12.0, 12.0, 200001, device=dev)
+    x = torch.cat([x, torch.randn(100000, device=dev) * 3])
+    g = torch.empty_like(x)
+    L = asme._lib
+    L.call("asme_gelu_dropout_fwd", L.ptr(x), x.numel(), 0.0, 0, L.ptr(g), L.stream())
+    d = torch.empty_like(x)
+    ones = torch.ones_like(x)
+    L.call("asme_gelu_dropout_bwd", L.ptr(x), L.ptr(ones), x.numel(), 0.0, 0, L.ptr(d), L.stream())
+    xd = x.double().cpu()
+    cdf = 0.5 * torch.special.erfc(-xd / math.sqrt(2.0))  # 1 + erf(z) cancels below z ~ -6 even in float64
+    ref_g = xd * cdf
+    ref_d = cdf + xd * torch.exp(-0.5 * xd * xd) / math.sqrt(2 * math.pi)
+    rel_g = ((g.double().cpu() - ref_g).abs() / ref_g.abs().clamp_min(1e-30))
+    rel_d = ((d.double().cpu() - ref_d).abs() / ref_d.abs().clamp_min(1e-30))
+    mask = ref_g.abs() > 1e-35  # below that GELU underflows float32
+    core = mask & (xd.abs() < 4)
+    # fp32 exp of an argument y carries ~|y| * 2e-7 relative error: 3e-5 at the far tail (|GELU| ~ 1e-30)
+    # -> 3e-6 where GELU matters (|x| < 4); fp32 GEMM accumulation noise on the same activations is ~1e-6
+    assert float(rel_g[mask].max()) < 3e-5, float(rel_g[mask].max())
+    assert float(rel_g[core].max()) < 3e-6, float(rel_g[core].max())
+    assert float((d.double().cpu() - ref_d).abs().max()) < 2e-6  # GELU' crosses 0 near x = -0.75: absolute
