@@ -86,6 +86,35 @@ __device__ __forceinline__ void philox_uniform4(uint64_t seed, uint32_t salt, ui
     u[2] = (float)(r.z >> 8) * s;
     u[3] = (float)(r.w >> 8) * s;
 }
+// GELU-dropout decisions (salt 5, the FFN activation): one Philox4x32-10 block serves the PAIR of 4-element chunks
+// (c & ~4, c | 4) -- 8 16-bit uniforms, x and y for the even chunk, z and w for the odd one; element kept iff
+// u16 >= round(p * 65536).  A fused-GEMM lane holds two such chunks (16 features apart), so it runs one block for
+// both; the row kernels run it per chunk and take their half.  Returns bit i = keep element i of the even chunk,
+// bit 4 + i = of the odd chunk.
+__device__ __forceinline__ uint32_t gelu_thresh(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+__device__ __forceinline__ uint32_t gelu_keep_bits8(uint64_t seed, uint64_t chunk, uint32_t thr) {
+    const uint64_t key = chunk & ~(uint64_t)4;
+    u32x4 c{(uint32_t)key, (uint32_t)(key >> 32), 5u, 0x5851F42Du};
+    const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint32_t m = 0;
+    m |= ((r.x & 0xFFFFu) >= thr ? 1u : 0u) | ((r.x >> 16) >= thr ? 2u : 0u);
+    m |= ((r.y & 0xFFFFu) >= thr ? 4u : 0u) | ((r.y >> 16) >= thr ? 8u : 0u);
+    m |= ((r.z & 0xFFFFu) >= thr ? 16u : 0u) | ((r.z >> 16) >= thr ? 32u : 0u);
+    m |= ((r.w & 0xFFFFu) >= thr ? 64u : 0u) | ((r.w >> 16) >= thr ? 128u : 0u);
+    return m;
+}
+// this chunk's 4 decisions
+__device__ __forceinline__ uint32_t gelu_keep_bits4(uint64_t seed, uint64_t chunk, uint32_t thr) {
+    return (gelu_keep_bits8(seed, chunk, thr) >> (((uint32_t)(chunk >> 2) & 1u) * 4u)) & 0xFu;
+}
+__device__ __forceinline__ void gelu_keep_factors(uint32_t bits4, float k, float (&u)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = (bits4 >> i) & 1u ? k : 0.f;
+}
+__device__ __forceinline__ float gelu_keep_factor(uint64_t seed, uint64_t idx, float p) {
+    return (gelu_keep_bits4(seed, idx >> 2, gelu_thresh(p)) >> (idx & 3)) & 1u ? 1.0f / (1.0f - p) : 0.0f;
+}
+
 // dropout keep-factor for element `idx`: 0 (dropped) or 1/(1-p)
 __device__ __forceinline__ float dropout_factor(uint64_t seed, uint32_t salt, uint64_t idx, float p) {
     float u[4];

@@ -251,9 +251,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                     if constexpr (EPI == EPI_GELU_DROP || EPI == EPI_GELU_BWD) {
                         float u[4] = {1.f, 1.f, 1.f, 1.f};
                         if (ep.p_gelu > 0.f) {
-                            philox_uniform4(ep.s_gelu, 5u, ((uint64_t)m * N + n) >> 2, u);
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) u[i] = u[i] >= ep.p_gelu ? keep_k : 0.f;
+                            gelu_keep_factors(gelu_keep_bits4(ep.s_gelu, ((uint64_t)m * N + n) >> 2,
+                                                              gelu_thresh(ep.p_gelu)),
+                                              keep_k, u);
                         }
                         if constexpr (EPI == EPI_GELU_DROP) {
                             *reinterpret_cast<float4*>(ep.pre + m * ldy + n) = v;

@@ -199,9 +199,7 @@ __global__ __launch_bounds__(256) void gelu_dropout_fwd_kernel(const float* __re
         float4 v = *reinterpret_cast<const float4*>(x + i);
         float u[4] = {1.f, 1.f, 1.f, 1.f};
         if (p > 0.f) {
-            philox_uniform4(seed, 5u, (uint64_t)i >> 2, u);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) u[k] = u[k] >= p ? 1.f / (1.f - p) : 0.f;
+            gelu_keep_factors(gelu_keep_bits4(seed, (uint64_t)i >> 2, gelu_thresh(p)), 1.f / (1.f - p), u);
         }
         float4 o;
         o.x = gelu_erf(v.x) * u[0];
@@ -210,7 +208,7 @@ __global__ __launch_bounds__(256) void gelu_dropout_fwd_kernel(const float* __re
         o.w = gelu_erf(v.w) * u[3];
         *reinterpret_cast<float4*>(y + i) = o;
     } else {
-        for (int64_t k = i; k < n; ++k) y[k] = gelu_erf(x[k]) * (p > 0.f ? dropout_factor(seed, 5u, k, p) : 1.f);
+        for (int64_t k = i; k < n; ++k) y[k] = gelu_erf(x[k]) * (p > 0.f ? gelu_keep_factor(seed, (uint64_t)k, p) : 1.f);
     }
 }
 
@@ -225,9 +223,7 @@ __global__ __launch_bounds__(256) void gelu_dropout_bwd_kernel(const float* __re
         float4 g = *reinterpret_cast<const float4*>(dy + i);
         float u[4] = {1.f, 1.f, 1.f, 1.f};
         if (p > 0.f) {
-            philox_uniform4(seed, 5u, (uint64_t)i >> 2, u);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) u[k] = u[k] >= p ? 1.f / (1.f - p) : 0.f;
+            gelu_keep_factors(gelu_keep_bits4(seed, (uint64_t)i >> 2, gelu_thresh(p)), 1.f / (1.f - p), u);
         }
         float4 o;
         o.x = g.x * u[0] * gelu_erf_grad(v.x);
@@ -237,7 +233,7 @@ __global__ __launch_bounds__(256) void gelu_dropout_bwd_kernel(const float* __re
         *reinterpret_cast<float4*>(dx + i) = o;
     } else {
         for (int64_t k = i; k < n; ++k)
-            dx[k] = dy[k] * (p > 0.f ? dropout_factor(seed, 5u, k, p) : 1.f) * gelu_erf_grad(x[k]);
+            dx[k] = dy[k] * (p > 0.f ? gelu_keep_factor(seed, (uint64_t)k, p) : 1.f) * gelu_erf_grad(x[k]);
     }
 }
 

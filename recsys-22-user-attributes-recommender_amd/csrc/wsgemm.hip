@@ -72,6 +72,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     constexpr int K4 = K / 4;
     constexpr int NKB = K / 16;
     static_assert(NKB % kD == 0, "the ring depth must divide the k16 blocks of a tile");
+    static_assert(CT % 2 == 0, "GELU-dropout Philox blocks serve feature-tile pairs");
     extern __shared__ __attribute__((aligned(16))) float4 lds4[];
     const int nblk = N / NB;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
@@ -115,6 +116,8 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         breg[ct] = ep.bias ? *reinterpret_cast<const float4*>(ep.bias + n0 + ct * 16 + 4 * g)
                            : make_float4(0.f, 0.f, 0.f, 0.f);
     const float keep_k = ep.p > 0.f ? 1.f / (1.f - ep.p) : 1.f;
+    const uint32_t thr = gelu_thresh(ep.p);
+    uint32_t pend = 0;  // GELU-dropout bits of the odd feature tile of the current pair
     const float* rc = xrow(0);
     const float* rn = xrow(1);
     float4 ring[kD];
@@ -139,9 +142,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         } else if constexpr (EPI == WS_GELU_DROP) {
             float u[4] = {1.f, 1.f, 1.f, 1.f};
             if (ep.p > 0.f) {
-                philox_uniform4(ep.seed, 5u, off >> 4, u);  // element index (off / 4), 4 per Philox block
-#pragma unroll
-                for (int i = 0; i < 4; ++i) u[i] = u[i] >= ep.p ? keep_k : 0.f;
+                // feature tiles ct and ct + 1 are the chunk pair (c, c | 4) of one Philox block: generated at the
+                // even tile, the odd tile's half kept in `pend` (chunk = element index off / 4 over 4)
+                if ((ct & 1) == 0) pend = gelu_keep_bits8(ep.seed, (uint64_t)(off >> 4), thr);
+                gelu_keep_factors((ct & 1) ? (pend >> 4) : (pend & 0xFu), keep_k, u);
             }
             // the backward's whole activation factor keep * GELU'(pre), so its epilogue is one multiply
             float gl[4], gd[4];
