@@ -81,6 +81,45 @@ __device__ __forceinline__ void adam_elem4(float4& P, const float4& G, float4& M
     V = make_float4(v0.x, v0.y, v1.x, v1.y);
 }
 
+// adam_elem with g == 0 and no weight decay (the lazy replay's step), with the same IEEE result op for op:
+// 0 - m == -m exactly and c * (-m) == -(c * m), so m + c * (0 - m) == m - c * m; (1 - b2) * 0 * 0 == +0 and
+// v * b2 >= +0 (v never goes negative), so v * b2 + 0 == v * b2.  4 of the 14 operations disappear.
+__device__ __forceinline__ void adam_decay(float& p, float& m, float& v, const AdamHyper& hp) {
+#pragma clang fp contract(off)
+    m = m - hp.one_minus_b1 * m;
+    v = v * hp.b2;
+    const float denom = __builtin_amdgcn_sqrtf(v) * hp.inv_bc2_sqrt + hp.eps;
+    p = p + hp.neg_step_size * (m * __builtin_amdgcn_rcpf(denom));
+}
+__device__ __forceinline__ void adam_decay2(float2v& p, float2v& m, float2v& v, const AdamHyper& hp) {
+#pragma clang fp contract(off)
+    m = m - hp.one_minus_b1 * m;
+    v = v * hp.b2;
+    const float2v s = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+    const float2v d = s * hp.inv_bc2_sqrt + hp.eps;
+    const float2v r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    p = p + hp.neg_step_size * (m * r);
+}
+// one zero-gradient step (weight decay keeps the general form: its gradient wd * p is not zero)
+__device__ __forceinline__ void adam_zero_grad_step(float& p, float& m, float& v, const AdamHyper& hp) {
+    if (hp.wd != 0.f)
+        adam_elem(p, 0.f, m, v, hp);
+    else
+        adam_decay(p, m, v, hp);
+}
+__device__ __forceinline__ void adam_zero_grad_step4(float4& P, float4& M, float4& V, const AdamHyper& hp) {
+    if (hp.wd != 0.f) {
+        adam_elem4(P, make_float4(0.f, 0.f, 0.f, 0.f), M, V, hp);
+        return;
+    }
+    float2v p0 = {P.x, P.y}, p1 = {P.z, P.w}, m0 = {M.x, M.y}, m1 = {M.z, M.w}, v0 = {V.x, V.y}, v1 = {V.z, V.w};
+    adam_decay2(p0, m0, v0, hp);
+    adam_decay2(p1, m1, v1, hp);
+    P = make_float4(p0.x, p0.y, p1.x, p1.y);
+    M = make_float4(m0.x, m0.y, m1.x, m1.y);
+    V = make_float4(v0.x, v0.y, v1.x, v1.y);
+}
+
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamList L, AdamHyper hp) {
     const int64_t blk = blockIdx.x;
     int ti = 0;
@@ -242,7 +281,7 @@ __global__ __launch_bounds__(256) void lazy_catch_up_kernel(const int64_t* __res
         const AdamHyper hp = hist[t];
 #pragma unroll
         for (int j = 0; j < VPL; ++j)
-            if (lane + 64 * j < D) adam_elem(P[j], 0.f, M[j], Vv[j], hp);
+            if (lane + 64 * j < D) adam_zero_grad_step(P[j], M[j], Vv[j], hp);
     }
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
@@ -288,15 +327,13 @@ __global__ __launch_bounds__(256) void lazy_catch_up_v4_kernel(const int64_t* __
         M = *reinterpret_cast<const float4*>(m + off);
         Vv = *reinterpret_cast<const float4*>(v + off);
     }
-    const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+    // lanes whose row starts later sit out the first steps under the exec mask (no per-element selects)
+    // (the next step's constants are loaded one iteration ahead, off the recurrence's critical path)
+    AdamHyper next = hist[t_lo + 1];
     for (int32_t t = t_lo + 1; t <= upto; ++t) {
-        float4 P2 = P, M2 = M, V2 = Vv;
-        adam_elem4(P2, Z, M2, V2, hist[t]);
-        if (t > t0) {
-            P = P2;
-            M = M2;
-            Vv = V2;
-        }
+        const AdamHyper hp = next;
+        next = hist[min(t + 1, upto)];
+        if (t > t0) adam_zero_grad_step4(P, M, Vv, hp);
     }
     if (!live) return;
     *reinterpret_cast<float4*>(p + off) = P;

@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--k", type=int, default=13)
+    ap.add_argument("--wd", type=float, default=0.0)
     a = ap.parse_args()
     asme = __graft_entry__.load_package()
     call, ptr, st = asme._lib.call, asme._lib.ptr, asme._lib.stream
@@ -24,7 +25,7 @@ def main():
     v = torch.zeros(V, D, device=dev)
     hist = torch.zeros(1024, 8, device=dev)
     for t in range(1, a.k + 1):
-        call("asme_lazy_adam_record_step", ptr(hist), t, 1e-3, 0.9, 0.999, 1e-8, 1e-3, st())
+        call("asme_lazy_adam_record_step", ptr(hist), t, 1e-3, 0.9, 0.999, 1e-8, a.wd, st())
     last = torch.zeros(V, dtype=torch.int32, device=dev)
     times = []
     for rep in range(4):
@@ -37,7 +38,7 @@ def main():
         times.append(e0.elapsed_time(e1))
     t = min(times[1:])
     gb = V * D * 4 * 6 / 1e9
-    print(f"flush {V} x {D}, k={a.k}: {t:.2f} ms  {gb / t:.2f} TB/s (algorithmic {gb:.1f} GB)")
+    print(f"flush {V} x {D}, k={a.k} wd={a.wd}: {t:.2f} ms  {gb / t:.2f} TB/s (algorithmic {gb:.1f} GB)")
 
 
 if __name__ == "__main__":
