@@ -1,16 +1,20 @@
-// Weight-stationary streaming GEMM for the token-major Linear layers, fp32 MFMA on gfx950.
+// Weight-stationary streaming GEMM for the token-major Linear layers: fp32 products on the bf16 matrix cores
+// (bf16x6 split operands, common.h) on gfx950.
 //
 // Reference semantics (paths relative to /root/reference/src/asme):
 //   nn.Linear projections         core/models/common/layers/transformer_layers.py:175-199 (Q,K,V,O)
 //   PositionwiseFeedForward       transformer_layers.py:212-220  W2(dropout(GELU_erf(W1 x)))
 // The shapes of the ASME transformer are tall and skinny: M = B*L tokens (2e5 at the bench shape) against
 // K, N <= 512.  So the kernel keeps one NB x K block of the weight in LDS for the workgroup's whole life
-// (loaded once; the hot loop has no barrier) and every wave streams its own 16-token tiles of X from HBM
-// straight into registers, kD k16 blocks in flight, while it multiplies the previous ones:
-//   C^T tile (NB features x 16 tokens) += W_blk (NB x 16 k) . X_tile^T (16 k x 16 tokens)
-// Lane (c16, g) of an MFMA supplies k = 4g..4g+3 of one 16-k block for its feature / token, so the X rows
-// are read as float4 (4 lanes = 64 contiguous bytes of a row) and the W block as conflict-free
-// ds_read_b128 (W image row r, 16-B slot s stored at slot s ^ (r & 15)).
+// (split once into three bf16 planes h, m, l; the hot loop has no barrier) and every wave streams its own
+// 16-token tiles of X from HBM straight into registers, kD k32 blocks in flight, while it multiplies the
+// previous ones:
+//   C^T tile (NB features x 16 tokens) += W_blk (NB x 32 k) . X_tile^T (32 k x 16 tokens)
+// as six v_mfma_f32_16x16x32_bf16 per 16-feature tile (mm, hl, lh, hm, mh, hh).  Lane (c16, g) of an MFMA
+// supplies k = 8g..8g+7 of one 32-k block for its feature / token, so the X rows are read as two float4 (4
+// lanes = 128 contiguous bytes of a row) and split in registers once per block for all CT feature tiles, and
+// the W planes as conflict-free ds_read_b128 (W image row r, 16-B slot s stored at slot s ^ (r & 15)).
+// Each feature tile's next-block W read goes out right after its MFMAs consumed the registers.
 // Epilogue: a finished tile's accumulators (+ bias) move to a stash and are written by buffer stores
 // spread over the NEXT tile's k blocks, one 16-feature tile per block -- nothing overwrites a store's source
 // registers until a tile later (an LDS read or MFMA landing on them right after the store stalls the
@@ -20,20 +24,20 @@
 //            WS_GELU_BWD    Y = C * A                                                   (through the activation)
 // A (the activation factor, written by the forward in place of the pre-activation, same bytes) makes the
 // backward epilogue a single multiply: no Philox, erf or exp in the input-gradient GEMM.
-// Dropout decisions are exactly those of asme_gelu_dropout_fwd/bwd (norm.hip): element m*N + n, one
-// Philox block per 4 consecutive elements, salt 5.
-// Measured at M = 204800 (tools/probe/sgemm_probe.py, fp32 MFMA peak 157 TF/s): K=128 -> N=512 113 TF/s,
-// K=512 -> N=128 126 TF/s, vs hipBLASLt 93 / 96.
+// Dropout decisions are exactly those of asme_gelu_dropout_fwd/bwd (norm.hip): one Philox block per pair of
+// 4-element chunks, 16-bit uniforms, salt 5 (common.h gelu_keep_bits8).
+// Measured at M = 204800 (tools/ws_bench.py; fp32-equivalent rate, bf16x6 ceiling 2516.6 / 6 = 419 TF/s):
+// K=128 -> N=128 174 TF/s, K=384 -> N=128 (input gradient) 179, K=128 -> N=512 124, K=512 -> N=128 131;
+// the fp32-MFMA version of this kernel (157 TF/s ceiling): 113-126.
 #include "common.h"
 
 using namespace asme;
 
 namespace {
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32v4 __attribute__((ext_vector_type(4)));
 
-constexpr int kD = 8;               // k16 blocks of X in flight per wave
+constexpr int kD = 4;               // k32 blocks of X in flight per wave
 constexpr int kWaves = 8;           // 512-thread workgroups, one per CU, two waves per SIMD
 constexpr uint32_t kDrop = 0x80000000u;  // >= every buffer's record count: the access is dropped / reads 0
 
@@ -47,9 +51,6 @@ struct WsEpi {
     uint64_t seed;
 };
 
-__device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 __device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s ^ (r & 15)); }
 __device__ __forceinline__ void bstore(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
     const u32v4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
@@ -69,29 +70,37 @@ template <int K, int CT, bool TRANS, int EPI>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ws_gemm_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W, int N, float* __restrict__ Y, WsEpi ep) {
     constexpr int NB = 16 * CT;  // output features per workgroup
-    constexpr int K4 = K / 4;
-    constexpr int NKB = K / 16;
-    static_assert(NKB % kD == 0, "the ring depth must divide the k16 blocks of a tile");
+    constexpr int K8 = K / 8;    // 16-B slots (8 bf16) of a W image row
+    constexpr int NKB = K / 32;
+    constexpr int PL = NB * K8;  // slots of one bf16 plane
+    static_assert(NKB % kD == 0, "the ring depth must divide the k32 blocks of a tile");
     static_assert(CT % 2 == 0, "GELU-dropout Philox blocks serve feature-tile pairs");
-    extern __shared__ __attribute__((aligned(16))) float4 lds4[];
+    extern __shared__ __attribute__((aligned(16))) uint4 lds16[];
     const int nblk = N / NB;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
     const int wg_per_nb = per_xcd / nblk;  // the workgroups of one XCD split over the feature blocks
     if (slot >= wg_per_nb * nblk) return;
     const int nb = slot % nblk;
     const int n0 = nb * NB;
-    // ---- the W block, once
-    if (!TRANS) {
-        for (int i = threadIdx.x; i < NB * K4; i += kWaves * 64) {
-            const int r = i / K4, s = i % K4;
-            lds4[wslot(r, s, K4)] = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + 4 * s);
+    // ---- the W block, once, split into its three bf16 planes (h, m, l)
+    for (int i = threadIdx.x; i < NB * K8; i += kWaves * 64) {
+        // TRANS: block element (r, k) = W[k][n0 + r], lanes on consecutive r (coalesced column reads)
+        const int r = TRANS ? i % NB : i / K8, s8 = TRANS ? i / NB : i % K8;
+        float4 a, b;
+        if (!TRANS) {
+            const float* w = W + (int64_t)(n0 + r) * K + 8 * s8;
+            a = *reinterpret_cast<const float4*>(w);
+            b = *reinterpret_cast<const float4*>(w + 4);
+        } else {
+            const float* w = W + (int64_t)(8 * s8) * N + n0 + r;
+            a = make_float4(w[0], w[N], w[2 * N], w[3 * N]);
+            b = make_float4(w[4 * N], w[5 * N], w[6 * N], w[7 * N]);
         }
-    } else {  // block element (r, k) = W[k][n0 + r]: lanes read consecutive r (coalesced)
-        float* l = reinterpret_cast<float*>(lds4);
-        for (int i = threadIdx.x; i < NB * K; i += kWaves * 64) {
-            const int r = i % NB, k = i / NB;
-            l[wslot(r, k >> 2, K4) * 4 + (k & 3)] = W[(int64_t)k * N + n0 + r];
-        }
+        const Bf3 p = split_bf3(a, b);
+        const int sl = wslot(r, s8, K8);
+        lds16[sl] = __builtin_bit_cast(uint4, p.h);
+        lds16[PL + sl] = __builtin_bit_cast(uint4, p.m);
+        lds16[2 * PL + sl] = __builtin_bit_cast(uint4, p.l);
     }
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
@@ -105,7 +114,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const int64_t t0 = lo + widx;
     auto xrow = [&](int64_t j) -> const float* {  // clamped rows are computed and dropped at the store
         int64_t m = (t0 + (j < my_tiles ? j : my_tiles - 1) * wcount) * 16 + c16;
-        return X + (m < M ? m : M - 1) * K + 4 * g;
+        return X + (m < M ? m : M - 1) * K + 8 * g;
     };
     const __amdgpu_buffer_rsrc_t yr = rsrc(Y, M * N * 4);
     const __amdgpu_buffer_rsrc_t pr = rsrc(EPI == WS_GELU_DROP ? (const void*)ep.pre_out : (const void*)ep.pre_in,
@@ -120,19 +129,30 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     uint32_t pend = 0;  // GELU-dropout bits of the odd feature tile of the current pair
     const float* rc = xrow(0);
     const float* rn = xrow(1);
-    float4 ring[kD];
+    float4 ring[2 * kD];  // k32 block d of X: ring[2d] (k 8g..8g+3), ring[2d + 1] (k 8g+4..8g+7)
 #pragma unroll
     for (int d = 0; d < kD; ++d) {
-        ring[d] = *reinterpret_cast<const float4*>(rc + d * 16);
+        ring[2 * d] = *reinterpret_cast<const float4*>(rc + d * 32);
+        ring[2 * d + 1] = *reinterpret_cast<const float4*>(rc + d * 32 + 4);
         __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's vmcnt waits assume it
     }
     float4 stash[CT], pre[CT];
     uint32_t soff = kDrop;  // byte offset of (row, n0 + 4g) of the stashed tile in Y
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) stash[ct] = pre[ct] = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 wc[CT];
+    // W operand of feature tile ct, k32 block kb: row ct*16 + c16, k 8g..8g+7 of the three planes
+    auto wload = [&](int ct, int kb) -> Bf3 {
+        const int sl = wslot(ct * 16 + c16, kb * 4 + g, K8);
+        Bf3 w;
+        w.h = __builtin_bit_cast(bf16x8, lds16[sl]);
+        w.m = __builtin_bit_cast(bf16x8, lds16[PL + sl]);
+        w.l = __builtin_bit_cast(bf16x8, lds16[2 * PL + sl]);
+        return w;
+    };
+    Bf3 wc[CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) wc[ct] = lds4[wslot(ct * 16 + c16, g, K4)];
+    for (int ct = 0; ct < CT; ++ct) wc[ct] = wload(ct, 0);
+    Bf3 xs = split_bf3(ring[0], ring[1]);
     // the stashed tile's epilogue for one 16-feature tile
     auto epilogue = [&](int ct) {
         const uint32_t off = soff + ct * 64;
@@ -164,32 +184,33 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     for (int64_t j = 0; j < my_tiles; ++j) {
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // kD blocks per trip, unrolled; the trips themselves stay a loop (a fully unrolled K = 384 tile spills)
+#pragma unroll 1
+        for (int kq = 0; kq < NKB; kq += kD)
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
+        for (int d = 0; d < kD; ++d) {
+            const int kb = kq + d;
             const int kbn = kb + 1 == NKB ? 0 : kb + 1;
-            float4 wn[CT];
+            // each feature tile's six MFMAs, then its next-block W read into the registers they consumed
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) wn[ct] = lds4[wslot(ct * 16 + c16, kbn * 4 + g, K4)];
-            __builtin_amdgcn_sched_barrier(0);  // the next block's W reads go out ahead of this block's MFMAs
-            const int d = kb % kD;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].x, ring[d].x, acc[ct]);
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].y, ring[d].y, acc[ct]);
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].z, ring[d].z, acc[ct]);
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wc[ct].w, ring[d].w, acc[ct]);
+            for (int ct = 0; ct < CT; ++ct) {
+                acc[ct] = mfma_bf3(wc[ct], xs, acc[ct]);
+                wc[ct] = wload(ct, kbn);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             // refill the slot just consumed: block kb + kD of this tile or of the next one (unconditional,
             // so the vmcnt bookkeeping stays exact; past the last tile it re-reads the last one)
-            ring[d] = *reinterpret_cast<const float4*>((kb + kD < NKB ? rc : rn) + ((kb + kD) % NKB) * 16);
-            // the previous tile's epilogue, one 16-feature tile per block (late in the tile, so the
-            // pre-activation loads WS_GELU_BWD issued at the tile boundary have landed)
+            const float* src = (kb + kD < NKB ? rc : rn) + ((kb + kD) % NKB) * 32;
+            ring[2 * d] = *reinterpret_cast<const float4*>(src);
+            ring[2 * d + 1] = *reinterpret_cast<const float4*>(src + 4);
+            // the next block's X terms
+            const int dn = (kb + 1) % kD;
+            xs = split_bf3(ring[2 * dn], ring[2 * dn + 1]);
+            // the previous tile's epilogue, spread over the blocks (late in the tile, so the pre-activation
+            // loads WS_GELU_BWD issued at the tile boundary have landed)
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct)
-                if ((ct + 1) * NKB / CT - 1 == kb) epilogue(ct);
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) wc[ct] = wn[ct];
+                if (((ct + 1) * NKB + CT - 1) / CT - 1 == kb) epilogue(ct);  // every ct lands in [0, NKB)
             __builtin_amdgcn_sched_barrier(0);
         }
         // tile done: to the stash (written during the next tile)
@@ -210,7 +231,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
 
 template <int K, int CT, bool TRANS, int EPI>
 int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
-    const size_t lds = (size_t)16 * CT * K * 4;
+    const size_t lds = (size_t)16 * CT * K * 6;  // three bf16 planes
     static bool attr = false;  // opt in above 64 KiB of dynamic LDS once per instantiation
     if (!attr) {
         const hipError_t e = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI>,
@@ -226,17 +247,27 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
     return hip_status(hipGetLastError(), "asme_ws_linear");
 }
 
-// features per workgroup: 64, or 96 when N / 64 does not divide the 32 workgroups of an XCD (N = 384)
-int pick_ct(int N) {
-    if (N % 64 == 0 && 32 % (N / 64) == 0) return 4;
-    if (N % 96 == 0 && 32 % (N / 96) == 0) return 6;
+constexpr int kLdsMax = 160 * 1024;
+
+// features per workgroup: 64; 96 when N / 64 does not divide the 32 workgroups of an XCD (N = 384, K = 128:
+// wider tiles at larger K run out of registers); 32 when a 64-feature block of the three bf16 planes would
+// not fit the LDS (K = 512); else 64 with the XCD's leftover workgroups idle
+int pick_ct(int N, int K) {
+    const bool fit4 = 64 * K * 6 <= kLdsMax;
+    if (N % 64 == 0 && 32 % (N / 64) == 0 && fit4) return 4;
+    if (K == 128 && N % 96 == 0 && 32 % (N / 96) == 0) return 6;
+    if (N % 32 == 0 && 32 % (N / 32) == 0 && 32 * K * 6 <= kLdsMax) return 2;
+    if (N % 64 == 0 && N / 64 <= 32 && fit4) return 4;
     return 0;
 }
 
 template <int K, bool TRANS, int EPI>
 int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
-    if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
-    return launch_ws<K, 6, TRANS, EPI>(X, M, W, N, Y, ep, s);
+    if constexpr (64 * K * 6 <= kLdsMax)
+        if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
+    if constexpr (K == 128)
+        if (ct == 6) return launch_ws<K, 6, TRANS, EPI>(X, M, W, N, Y, ep, s);
+    return launch_ws<K, 2, TRANS, EPI>(X, M, W, N, Y, ep, s);
 }
 
 template <bool TRANS, int EPI>
@@ -253,12 +284,10 @@ int dispatch_k(int K, int ct, const float* X, int64_t M, const float* W, int N, 
 }  // namespace
 
 // 1 when (M, K, N) is a shape the weight-stationary kernel takes: K in {128, 256, 384, 512}, N a multiple of
-// 64 (or 96) that splits the 32 workgroups of an XCD, the W block within 128 KiB of LDS, Y < 2 GiB.
+// 32, 64 or 96 that splits the 32 workgroups of an XCD, the split W block within 160 KiB of LDS, Y < 2 GiB.
 ASME_API int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N) {
     if (M <= 0 || (K != 128 && K != 256 && K != 384 && K != 512)) return 0;
-    const int ct = pick_ct((int)N);
-    if (ct == 0 || N > 4096) return 0;
-    if ((int64_t)16 * ct * K * 4 > 128 * 1024) return 0;
+    if (N > 4096 || pick_ct((int)N, (int)K) == 0) return 0;
     if (M * N * 4 >= (int64_t)kDrop || M * K * 4 >= ((int64_t)1 << 40)) return 0;
     return 1;
 }
@@ -278,7 +307,7 @@ ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W
                    "asme_ws_linear: 16-B alignment");
     ASME_CHECK_ARG(p >= 0.f && p < 1.f, "asme_ws_linear: dropout probability in [0, 1)");
     const WsEpi ep{bias, pre_out, pre_in, p, seed};
-    const int ct = pick_ct((int)N);
+    const int ct = pick_ct((int)N, (int)K);
     hipStream_t s = (hipStream_t)stream;
     if (trans) {
         if (epi == 0) return dispatch_k<true, WS_STORE>((int)K, ct, X, M, W, (int)N, Y, ep, s);

@@ -37,11 +37,30 @@ def test_ws_linear_matches_fp64(asme, dev, M, K, N):
     assert (y.double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
 
 
+@pytest.mark.parametrize("K,N", [(128, 512), (512, 128), (384, 128)])
+@pytest.mark.parametrize("dist", ["normal", "positive", "wide"])
+def test_ws_linear_bf16x6_error_at_fp32_level(asme, dev, K, N, dist):
+    """the fp32 products on split-bf16 MFMAs (csrc/common.h bf16x6) are as accurate as fp32 arithmetic: error vs
+    float64, relative to sum |x * w|, no worse than 1.25x torch's own fp32 GEMM on the same inputs"""
+    torch.manual_seed(K + N)
+    M = 8192
+    gen = {"normal": lambda *s: torch.randn(*s, device=dev),
+           "positive": lambda *s: torch.rand(*s, device=dev),
+           "wide": lambda *s: torch.randn(*s, device=dev) * torch.exp(3 * torch.randn(*s, device=dev))}[dist]
+    x, w = gen(M, K), gen(N, K)
+    ref = x.double() @ w.double().t()
+    scale = x.double().abs() @ w.double().abs().t()
+    ours = ((_call(asme, x, w, N, 0).double() - ref).abs() / scale).max().item()
+    theirs = (((x @ w.t()).double() - ref).abs() / scale).max().item()
+    assert ours <= 1.25 * theirs + 1e-9, (ours, theirs)
+    assert ours < 2e-6
+
+
 def test_ws_linear_rejects_unsupported(asme):
     lib = asme._lib.load()
     assert lib.asme_ws_linear_supported(100, 100, 128) == 0      # K not tiled
     assert lib.asme_ws_linear_supported(100, 128, 100) == 0      # N not a multiple of 64 / 96
-    assert lib.asme_ws_linear_supported(100, 512, 384) == 0      # W block over 128 KiB of LDS
+    assert lib.asme_ws_linear_supported(100, 512, 384) == 0      # split W block over 160 KiB of LDS
     assert lib.asme_ws_linear_supported(1 << 22, 128, 512) == 0  # Y over 2 GiB
 
 

@@ -32,7 +32,7 @@ def main():
     for K, N, trans, epi, p, hb in cfgs or [(128, 512, 0, 0, 0.0, 1), (128, 512, 0, 0, 0.0, 0), (128, 512, 0, 1, 0.0, 1),
                                     (128, 512, 0, 1, 0.2, 1), (128, 512, 1, 0, 0.0, 0), (128, 512, 1, 2, 0.2, 0),
                                     (512, 128, 0, 0, 0.0, 1), (128, 384, 0, 0, 0.0, 1), (128, 384, 0, 0, 0.0, 0),
-                                    (128, 128, 0, 0, 0.0, 1)]:
+                                    (128, 128, 0, 0, 0.0, 1), (384, 128, 1, 0, 0.0, 0), (512, 128, 1, 0, 0.0, 0)]:
         x = torch.randn(M, K, device=dev)
         w = torch.randn(N, K, device=dev) if not trans else torch.randn(K, N, device=dev)
         b = torch.randn(N, device=dev)
