@@ -4,115 +4,186 @@
 // gets dW = grad_out^T @ input from autograd.  Here T = B*L = 204,800 tokens and N, K <= 512, so the
 // product is a small output with a huge reduction: library GEMMs run it at 14-38 TFLOP/s (measured,
 // DESIGN.md §4).  This kernel splits the token dimension over many workgroups (split-T), each owning a
-// 128x128 output tile for one token chunk, accumulating with fp32 MFMA (v_mfma_f32_16x16x4f32, exact
-// f32 FMA chain) and writing an fp32 partial slab; a fixed-order column reduction then sums the slabs
-// (deterministic, no atomics).  The bias gradient is summed from the same LDS-staged dY tiles.
+// 128x128 output tile for one token chunk and writing an fp32 partial slab; a fixed-order column reduction
+// then sums the slabs (deterministic, no atomics).  The bias gradient is summed from the same dY registers.
+//
+// Products run on the bf16 matrix cores with split operands (bf16x6, common.h: error at or below fp32
+// MFMA's): a 32-token block of dY and X is split in registers into three bf16 planes and stored transposed
+// in LDS -- per column, the 32 tokens as four 16-B slots of 8 -- so the MFMA operand (8 consecutive tokens
+// of one column, v_mfma_f32_16x16x32_bf16) is one ds_read_b128 per plane.  The slot layout (tslot) is
+// conflict-free for both the ds_read_b128 lane groups and the ds_write_b128 8-lane groups.
 //
 // Layout: A = dY (T x N, row stride lda), B = X (T x K, row stride ldb), both row-major fp32.
-// Workgroup = 4 waves in a 2x2 grid over the 128x128 tile; each wave owns 64x64 = 4x4 MFMA tiles
-// (16 accumulators).  Token rows stream through LDS 32 at a time (register-prefetched one block ahead);
-// the LDS row stride of 144 floats puts the two 16-lane halves of a b32 read on disjoint banks.
+// Workgroup = 8 waves (two per SIMD, one workgroup per CU) in a 2x4 grid over the 128x128 tile; each wave
+// owns 64x32 = 4x2 MFMA tiles.  The LDS holds two token blocks (double buffer, 96 KiB): while the waves
+// multiply block n, they split and store block n+1 (loaded into registers two blocks earlier) into the other
+// buffer and issue the loads of block n+3 -- one barrier per block.  Waves 0-3 load dY, 4-7 load X, each
+// thread 8 tokens x 2 columns (rows of 512 contiguous bytes per wave).
 #include "common.h"
 
 using namespace asme;
 
 namespace {
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
+constexpr int kTile = 128;         // output tile (N and K)
+constexpr int kTT = 32;            // token rows per LDS block
+constexpr int kWgThreads = 512;
+constexpr int kPlane = kTile * 4;  // 16-B slots of one bf16 plane of one operand (128 columns x 4 slots)
+constexpr int kBuf = 6 * kPlane;   // one token block: dY planes h, m, l then X planes h, m, l
 
-constexpr int kTile = 128;   // output tile (N and K)
-constexpr int kTT = 32;      // token rows per LDS block
-constexpr int kLds = 144;    // LDS row stride (floats)
-
-__device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+// 16-B slot of (column c, token slot s): column position c ^ ((c >> 1) & 1), slot ((c >> 2) ^ 3s) mod 4.
+// ds_read_b128 (lanes {0-3,12-15,20-27}, ...: 16 consecutive columns, s = lane / 16) and ds_write_b128
+// (8 contiguous lanes: columns 2i + jj, one s) both land on distinct 16-B bank slots.
+__device__ __forceinline__ int tslot(int c, int s) {
+    return (c ^ ((c >> 1) & 1)) * 4 + ((((c >> 2) & 3) ^ (3 * s)) & 3);
 }
 
-// thread i of 256 loads 4 float4 of a kTT x 128 block: row = (i / 32) + 8*q, col4 = i % 32
-__device__ __forceinline__ void load_block(const float* __restrict__ base, int64_t ld, int64_t t0, int64_t T,
-                                           int col0, int ncols, float4 (&r)[4]) {
-    const int c4 = (threadIdx.x & 31) * 4;
+// rows t0 + 8 rg .. + 7, columns col0 + 2 cg, + 1 of a row-major operand (zero past T / ncols).  `full`
+// (workgroup-uniform: the whole 32-row block and 128 columns in range) takes the branch-free form.
+__device__ __forceinline__ void load_cols(const float* __restrict__ base, int64_t ld, int64_t t0, int64_t T,
+                                          int col0, int ncols, int rg, int cg, bool full, float2 (&r)[8]) {
+    const float* p = base + (t0 + 8 * rg) * ld + col0 + 2 * cg;
+    if (full) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int64_t t = t0 + (threadIdx.x >> 5) + 8 * q;
-        if (t < T && col0 + c4 < ncols)
-            r[q] = *reinterpret_cast<const float4*>(base + t * ld + col0 + c4);
-        else
-            r[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < 8; ++q) r[q] = *reinterpret_cast<const float2*>(p + q * ld);
+        return;
+    }
+    const bool col_ok = col0 + 2 * cg < ncols;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int64_t t = t0 + 8 * rg + q;
+        r[q] = (t < T && col_ok) ? *reinterpret_cast<const float2*>(p + q * ld) : make_float2(0.f, 0.f);
     }
 }
 
-__device__ __forceinline__ void store_block(float* __restrict__ s, const float4 (&r)[4]) {
-    const int c4 = (threadIdx.x & 31) * 4;
+// the thread's 2 columns x 8 tokens, split, into token slot rg of those columns of the three planes
+__device__ __forceinline__ void store_cols(uint4* __restrict__ planes, int rg, int cg, const float2 (&r)[8]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(s + ((threadIdx.x >> 5) + 8 * q) * kLds + c4) = r[q];
+    for (int jj = 0; jj < 2; ++jj) {
+        const float4 a = jj == 0 ? make_float4(r[0].x, r[1].x, r[2].x, r[3].x)
+                                 : make_float4(r[0].y, r[1].y, r[2].y, r[3].y);
+        const float4 b = jj == 0 ? make_float4(r[4].x, r[5].x, r[6].x, r[7].x)
+                                 : make_float4(r[4].y, r[5].y, r[6].y, r[7].y);
+        const Bf3 p = split_bf3(a, b);
+        const int sl = tslot(2 * cg + jj, rg);
+        planes[sl] = __builtin_bit_cast(uint4, p.h);
+        planes[kPlane + sl] = __builtin_bit_cast(uint4, p.m);
+        planes[2 * kPlane + sl] = __builtin_bit_cast(uint4, p.l);
+    }
 }
 
-__global__ __launch_bounds__(256) void weight_grad_kernel(const float* __restrict__ A, int64_t lda,
-                                                          const float* __restrict__ B, int64_t ldb, int64_t T,
-                                                          int N, int K, int64_t chunk_rows,
-                                                          float* __restrict__ part, float* __restrict__ bias_part) {
-    __shared__ __attribute__((aligned(16))) float As[kTT * kLds];
-    __shared__ __attribute__((aligned(16))) float Bs[kTT * kLds];
-    const int n0 = blockIdx.x * kTile, k0 = blockIdx.y * kTile;
-    const int64_t chunk = blockIdx.z;
+__global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void weight_grad_kernel(
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, int64_t T, int N, int K,
+    int64_t chunk_rows, float* __restrict__ part, float* __restrict__ bias_part) {
+    extern __shared__ uint4 lds[];  // two token blocks of kBuf slots
+    // XCD-aware order: the output tiles of one token chunk are consecutive workgroups of ONE XCD (ids
+    // xcd, xcd + 8, ...), resident together, so the dY / X rows they share come from that XCD's L2 once
+    const int ntn = (N + kTile - 1) / kTile, ntiles = ntn * ((K + kTile - 1) / kTile);
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int tile = slot % ntiles;
+    const int64_t chunk = (int64_t)(slot / ntiles) * 8 + xcd;
+    if (chunk * chunk_rows >= T) return;
+    const int tn = tile % ntn, tk = tile / ntn;
+    const int n0 = tn * kTile, k0 = tk * kTile;
     const int64_t t_begin = chunk * chunk_rows;
     const int64_t t_end = min(T, t_begin + chunk_rows);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
-    const int wr = wave >> 1, wc = wave & 1;
-    const bool do_bias = bias_part != nullptr && blockIdx.y == 0;
+    const int wr = wave >> 2, wc = wave & 3;  // 64 dY columns x 32 X columns
+    // loader role: threads 0-255 dY, 256-511 X (wave-uniform)
+    const bool load_a = threadIdx.x < 256;
+    const int u = threadIdx.x & 255, cg = u & 63, rg = u >> 6;
+    const float* src = load_a ? A : B;
+    const int64_t ld = load_a ? lda : ldb;
+    const int col0 = load_a ? n0 : k0, ncols = load_a ? N : K;
+    const int my_planes = load_a ? 0 : 3 * kPlane;
+    const bool do_bias = bias_part != nullptr && tk == 0 && load_a;
+    float2 bsum = make_float2(0.f, 0.f);  // dY columns n0 + 2cg, + 1 over this thread's rows
+    const bool cols_full = n0 + kTile <= N && k0 + kTile <= K;
 
-    floatx4 acc[4][4];
+    floatx4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float bsum = 0.f;  // threads 0..127: column n0 + tid of the bias gradient
+        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    float4 ra[4], rb[4];
-    load_block(A, lda, t_begin, t_end, n0, N, ra);
-    load_block(B, ldb, t_begin, t_end, k0, K, rb);
-    for (int64_t t0 = t_begin; t0 < t_end; t0 += kTT) {
+    auto load = [&](int64_t t0, float2 (&r)[8]) {
+        if (t0 < t_end) load_cols(src, ld, t0, t_end, col0, ncols, rg, cg, cols_full && t0 + kTT <= t_end, r);
+    };
+    // the block at t0 (in r) into LDS buffer buf; r then takes the block two ahead
+    auto stage = [&](int64_t t0, float2 (&r)[8], int buf) {
+        if (t0 >= t_end) return;
+        store_cols(lds + buf * kBuf + my_planes, rg, cg, r);
+        if (do_bias) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                bsum.x += r[q].x;
+                bsum.y += r[q].y;
+            }
+        }
+        load(t0 + 2 * kTT, r);
+    };
+    auto compute = [&](int buf) {
+        const uint4* L = lds + buf * kBuf;
+        Bf3 b[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int sl = tslot(wc * 32 + j * 16 + c16, g);
+            b[j].h = __builtin_bit_cast(bf16x8, L[3 * kPlane + sl]);
+            b[j].m = __builtin_bit_cast(bf16x8, L[4 * kPlane + sl]);
+            b[j].l = __builtin_bit_cast(bf16x8, L[5 * kPlane + sl]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int sl = tslot(wr * 64 + i * 16 + c16, g);
+            Bf3 a;
+            a.h = __builtin_bit_cast(bf16x8, L[sl]);
+            a.m = __builtin_bit_cast(bf16x8, L[kPlane + sl]);
+            a.l = __builtin_bit_cast(bf16x8, L[2 * kPlane + sl]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf3(a, b[j], acc[i][j]);
+        }
+    };
+    float2 r0[8], r1[8];  // two blocks in flight (the HBM latency outlasts one block's MFMAs)
+    load(t_begin, r0);
+    load(t_begin + kTT, r1);
+    stage(t_begin, r0, 0);
+    __syncthreads();
+    for (int64_t t0 = t_begin; t0 < t_end; t0 += 2 * kTT) {
+        stage(t0 + kTT, r1, 1);
+        compute(0);
         __syncthreads();
-        store_block(As, ra);
-        store_block(Bs, rb);
+        if (t0 + kTT >= t_end) break;
+        stage(t0 + 2 * kTT, r0, 0);
+        compute(1);
         __syncthreads();
-        if (t0 + kTT < t_end) {  // prefetch the next block while this one is consumed
-            load_block(A, lda, t0 + kTT, t_end, n0, N, ra);
-            load_block(B, ldb, t0 + kTT, t_end, k0, K, rb);
-        }
-        if (do_bias && threadIdx.x < kTile) {
-#pragma unroll 8
-            for (int r = 0; r < kTT; ++r) bsum += As[r * kLds + threadIdx.x];
-        }
-#pragma unroll
-        for (int kk = 0; kk < kTT / 4; ++kk) {
-            const int trow = (kk * 4 + g) * kLds;
-            float a[4], b[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = As[trow + wr * 64 + i * 16 + c16];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = Bs[trow + wc * 64 + j * 16 + c16];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-        }
     }
-    // partial slab: part[chunk][n][k]; lane holds rows n = ... + 4g + r, column k = ... + c16
+    // partial slab: part[chunk][n][k]; lane holds rows n = ... + 4g + q, column k = ... + c16
     float* P = part + chunk * (int64_t)N * K;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int n = n0 + wr * 64 + i * 16 + 4 * g + r;
-                const int k = k0 + wc * 64 + j * 16 + c16;
-                if (n < N && k < K) P[(int64_t)n * K + k] = acc[i][j][r];
+            for (int q = 0; q < 4; ++q) {
+                const int n = n0 + wr * 64 + i * 16 + 4 * g + q;
+                const int k = k0 + wc * 32 + j * 16 + c16;
+                if (n < N && k < K) P[(int64_t)n * K + k] = acc[i][j][q];
             }
-    if (do_bias && threadIdx.x < kTile && n0 + (int)threadIdx.x < N)
-        bias_part[chunk * (int64_t)N + n0 + threadIdx.x] = bsum;
+    if (bias_part != nullptr && tk == 0) {  // the 4 row groups' column sums, in row-group order
+        float2* red = reinterpret_cast<float2*>(lds);  // (the loop's last barrier retired every LDS read)
+        if (load_a) red[rg * 64 + cg] = bsum;
+        __syncthreads();
+        if (threadIdx.x < 64 && n0 + 2 * (int)threadIdx.x < N) {
+            float2 s = red[threadIdx.x];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                const float2 v = red[q * 64 + threadIdx.x];
+                s.x += v.x;
+                s.y += v.y;
+            }
+            *reinterpret_cast<float2*>(bias_part + chunk * (int64_t)N + n0 + 2 * threadIdx.x) = s;
+        }
+    }
 }
 
 // column sums with a fixed order (see reduce_rows_kernel in embedding.hip)
@@ -140,10 +211,11 @@ struct Plan {
 
 Plan make_plan(int64_t T, int64_t N, int64_t K) {
     const int64_t tiles = ((N + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-    int64_t want = std::max<int64_t>(1, 512 / tiles);  // ~2 workgroups per CU
+    // one workgroup per CU (96 KiB of LDS each): chunks a multiple of 8 (one per XCD lane), tiles x chunks <= 256
+    const int64_t want = std::max<int64_t>(8, (256 / tiles) / 8 * 8);
     int64_t rows = (T + want - 1) / want;
     rows = std::max<int64_t>(kTT, ((rows + kTT - 1) / kTT) * kTT);
-    return {(T + rows - 1) / rows, rows};
+    return {(T + rows - 1) / rows, rows};  // chunks holding tokens; the grid rounds them up to a multiple of 8
 }
 
 }  // namespace
@@ -168,9 +240,16 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
     hipStream_t s = (hipStream_t)stream;
     float* part = workspace;
     float* bpart = db ? workspace + p.nchunks * out_features * in_features : nullptr;
-    const dim3 grid((unsigned)((out_features + kTile - 1) / kTile), (unsigned)((in_features + kTile - 1) / kTile),
-                    (unsigned)p.nchunks);
-    hipLaunchKernelGGL(weight_grad_kernel, grid, dim3(256), 0, s, dy, ld_dy, x, ld_x, n_tokens, (int)out_features,
+    const int64_t ntiles = ((out_features + kTile - 1) / kTile) * ((in_features + kTile - 1) / kTile);
+    const dim3 grid((unsigned)(ntiles * ((p.nchunks + 7) / 8) * 8));
+    static bool attr = false;  // 96 KiB of dynamic LDS: opt in once
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)weight_grad_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kBuf * 16);
+        if (e != hipSuccess) return hip_status(e, "asme_linear_weight_grad: LDS opt-in");
+        attr = true;
+    }
+    hipLaunchKernelGGL(weight_grad_kernel, grid, dim3(kWgThreads), 2 * kBuf * 16, s, dy, ld_dy, x, ld_x, n_tokens, (int)out_features,
                        (int)in_features, p.chunk_rows, part, bpart);
     const int64_t width = out_features * in_features;
     hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width + kRedCols - 1) / kRedCols)), dim3(1024), 0, s, part,
