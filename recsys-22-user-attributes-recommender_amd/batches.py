@@ -17,7 +17,7 @@ cloze kernel can also replay given draws (tests replay the reference's torch CPU
 """
 from __future__ import annotations
 
-from typing import Dict, Optional, Sequence
+from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 
@@ -144,3 +144,27 @@ class ClozeMaskProcessor:
              self.tokenizer.mask_token_id, self.mask_prob, self.only_last_item_mask_prob, ptr(du), ptr(dr), seed,
              ptr(out), ptr(target), stream())
         return {ITEM_SEQ_ENTRY_NAME: out, TARGET_ENTRY_NAME: target}
+
+
+class LastItemMaskProcessor:
+    """data/datasets/processors/last_item_mask.py:9-44 (item sequence target) + the collate, batched on the GPU:
+    the MASK token appended after each session's last item (BERT4Rec evaluation input), left-truncated to
+    max_seq_length, right-padded."""
+
+    def __init__(self, tokenizers, masking_targets=None):
+        if masking_targets not in (None, [ITEM_SEQ_ENTRY_NAME]):
+            raise NotImplementedError("masking of attribute sequences is outside the MI355X hot path")
+        self.tokenizer = _item_tokenizer(tokenizers)
+
+    def process_batch(self, items: torch.Tensor, lengths: torch.Tensor, max_seq_length: Optional[int] = None
+                      ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """items (B, L) collated (right-padded) sessions, lengths (B,) -> (items (B, max_seq_length), lengths)"""
+        items = items.to(torch.int64).contiguous()
+        B, L = items.shape
+        Lo = L if max_seq_length is None else int(max_seq_length)
+        lengths = lengths.to(device=items.device, dtype=torch.int64).contiguous()
+        out = torch.empty(B, Lo, device=items.device, dtype=torch.int64)
+        out_len = torch.empty(B, device=items.device, dtype=torch.int64)
+        call("asme_last_item_mask", ptr(items), ptr(lengths), B, L, Lo, self.tokenizer.mask_token_id,
+             self.tokenizer.pad_token_id, ptr(out), ptr(out_len), stream())
+        return out, out_len

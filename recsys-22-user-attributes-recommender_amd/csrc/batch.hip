@@ -70,6 +70,24 @@ __global__ __launch_bounds__(256) void position_batch_kernel(const int64_t* __re
     }
 }
 
+// LastItemMaskProcessor (data/datasets/processors/last_item_mask.py:35-44) ahead of the collate: the session gets
+// the MASK token appended, then the collate keeps the last L_out entries, right-padded.  On an already collated
+// row (the last min(len, L_in) items, L_in >= L_out - 1) that is: the last min(len, L_out - 1) items, MASK, PAD.
+__global__ __launch_bounds__(256) void last_item_mask_kernel(const int64_t* __restrict__ items,
+                                                             const int64_t* __restrict__ lengths, int64_t B,
+                                                             int64_t L_in, int64_t L_out, int64_t mask_id, int64_t pad,
+                                                             int64_t* __restrict__ out, int64_t* __restrict__ out_len) {
+    const int64_t b = blockIdx.x;
+    if (b >= B) return;
+    int64_t len = lengths[b];
+    len = len < 0 ? 0 : (len > L_in ? L_in : len);
+    const int64_t keep = len < L_out - 1 ? len : L_out - 1;  // items kept before the MASK
+    const int64_t first = len - keep;
+    for (int64_t i = threadIdx.x; i < L_out; i += blockDim.x)
+        out[b * L_out + i] = i < keep ? items[b * L_in + first + i] : (i == keep ? mask_id : pad);
+    if (threadIdx.x == 0 && out_len) out_len[b] = keep + 1;
+}
+
 // ------------------------------------------------------------------------------------- pos / neg sampler
 // One wave per session.  x, pos: the collated s[:-1], s[1:]; neg: for each kept position one id drawn uniformly
 // from [0, V) and redrawn (next Philox counter) while it is special or occurs ANYWHERE in the full session (the
@@ -213,6 +231,20 @@ ASME_API int asme_position_batch(const int64_t* flat, const int64_t* offsets, in
     hipLaunchKernelGGL(position_batch_kernel, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, flat, offsets,
                        n_sessions, pairs, batch, seq_len, pad, out, out_len, target, err_flag);
     ASME_LAUNCH_CHECK("asme_position_batch");
+}
+
+// items (B, L_in) right-padded sessions with lengths (B,) -> out (B, L_out): MASK appended after the last item,
+// left-truncated to L_out, right-padded; out_len = the new lengths (nullable)
+ASME_API int asme_last_item_mask(const int64_t* items, const int64_t* lengths, int64_t batch, int64_t in_len,
+                                 int64_t out_len_max, int64_t mask_id, int64_t pad, int64_t* out, int64_t* out_len,
+                                 void* stream) {
+    ASME_CHECK_ARG(items && lengths && out, "asme_last_item_mask: null pointer");
+    ASME_CHECK_ARG(batch >= 0 && out_len_max >= 1 && in_len >= out_len_max - 1 && in_len >= 0,
+                   "asme_last_item_mask: bad shape (needs in_len >= out_len - 1)");
+    if (batch == 0) return 0;
+    hipLaunchKernelGGL(last_item_mask_kernel, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, items, lengths,
+                       batch, in_len, out_len_max, mask_id, pad, out, out_len);
+    ASME_LAUNCH_CHECK("asme_last_item_mask");
 }
 
 ASME_API int asme_posneg_sample(const int64_t* flat, const int64_t* offsets, int64_t n_sessions,

@@ -1,5 +1,5 @@
 """GPU batch producers (csrc/batch.hip, asme_amd.batches) against the oracle's restatement of the reference's
-processors (oracle/asme_oracle.py: cloze_mask, pos_neg, collate_pad), which itself reproduces the reference's
+processors (oracle/asme_oracle.py: cloze_mask, pos_neg, last_item_mask, collate_pad), which itself reproduces the reference's
 own known-answer tests (tests/test_reference_kats.py).
 
 Cloze masking replays the reference's torch CPU generator stream (oracle.cloze_draws) and must match the
@@ -96,6 +96,22 @@ def test_padded_session_batch_matches_collate(asme, dev):
     want = torch.tensor([O.collate_pad(sessions[i], 50) for i in idx.tolist()])
     assert torch.equal(out.cpu(), want)
     assert lengths.cpu().tolist() == [min(len(sessions[i]), 50) for i in idx.tolist()]
+
+
+@pytest.mark.parametrize("L_in,L_out", [(50, 50), (49, 50), (64, 20)])
+def test_last_item_mask_matches_processor_then_collate(asme, dev, L_in, L_out):
+    """LastItemMaskProcessor (MASK appended to the session) then the collate (left truncation to L_out, right
+    padding), against the oracle restatement applied to the full sessions; lengths 0..L_out+ covered"""
+    g = np.random.default_rng(L_in + L_out)
+    sessions = [[int(v) for v in g.integers(3, 500, size=int(n))] for n in list(range(0, 80)) + [L_out - 1, L_out]]
+    V = 600
+    tok = _tok(asme, V)
+    items, lengths = _collated(sessions, L_in, tok.pad_token_id)
+    proc = asme.batches.LastItemMaskProcessor({"item": tok})
+    out, out_len = proc.process_batch(items.to(dev), lengths.to(dev), L_out)
+    want = [O.collate_pad(O.last_item_mask(s, tok.mask_token_id), L_out, tok.pad_token_id) for s in sessions]
+    assert out.cpu().tolist() == want
+    assert out_len.cpu().tolist() == [min(len(s) + 1, L_out) for s in sessions]
 
 
 def test_posneg_sampler_contract(asme, dev):

@@ -106,3 +106,9 @@ def test_oracle_cloze_draws_replay():
                     out[i] = 1 if q < 0.8 else (int(r[b, i]) if q < 0.9 else s[i])
                     tgt[i] = s[i]
         assert (out, tgt) == ref[b], b
+
+
+def test_oracle_last_item_mask_reference_example():
+    """the processor's own docstring example (last_item_mask.py:13-19): [1, 5, 7, 8] -> [1, 5, 7, 8, 101]"""
+    assert O.last_item_mask([1, 5, 7, 8], mask_id=101) == [1, 5, 7, 8, 101]
+    assert O.collate_pad(O.last_item_mask([1, 5, 7, 8], mask_id=101), 3, pad=0) == [7, 8, 101]
