@@ -39,6 +39,7 @@ typedef unsigned u32v4 __attribute__((ext_vector_type(4)));
 
 constexpr int kD = 4;               // k32 blocks of X in flight per wave
 constexpr int kWaves = 8;           // 512-thread workgroups, one per CU, two waves per SIMD
+constexpr int kLdsMax = 160 * 1024;
 constexpr uint32_t kDrop = 0x80000000u;  // >= every buffer's record count: the access is dropped / reads 0
 
 enum { WS_STORE = 0, WS_GELU_DROP = 1, WS_GELU_BWD = 2 };
@@ -75,6 +76,11 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     constexpr int PL = NB * K8;  // slots of one bf16 plane
     static_assert(NKB % kD == 0, "the ring depth must divide the k32 blocks of a tile");
     static_assert(CT % 2 == 0, "GELU-dropout Philox blocks serve feature-tile pairs");
+    // row-major staging of the finished tile (per wave, 16 rows x NB, 16-B row pad) so each store instruction
+    // writes whole rows (16 lanes x 16 B = 256 B of one row at NB = 64) instead of 16 rows x 64 B (measured:
+    // N = 384 / 512 launches 12-23 % faster); not where the W planes leave no room for it
+    constexpr int NB4 = NB / 4, SROW = NB + 4;
+    constexpr bool kStage = CT >= 4 && NB * K * 6 + kWaves * 16 * SROW * 4 <= kLdsMax;  // (CT = 2: no gain)
     extern __shared__ __attribute__((aligned(16))) uint4 lds16[];
     const int nblk = N / NB;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
@@ -138,6 +144,13 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     }
     float4 stash[CT], pre[CT];
     uint32_t soff = kDrop;  // byte offset of (row, n0 + 4g) of the stashed tile in Y
+    int64_t srow0 = M;      // staged: first token of the stashed tile (M: none yet, every store dropped)
+    float* stg = reinterpret_cast<float*>(lds16 + 3 * PL) + (threadIdx.x >> 6) * 16 * SROW;
+    // staged store instruction ct: float4 64 ct + lane of the tile (row-major), its byte offset in Y
+    auto staged_off = [&](int ct, int64_t r0) -> uint32_t {
+        const int idx = 64 * ct + (threadIdx.x & 63), row = idx / NB4, c4 = idx % NB4;
+        return r0 + row < M ? (uint32_t)(((r0 + row) * N + n0 + 4 * c4) * 4) : kDrop;
+    };
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) stash[ct] = pre[ct] = make_float4(0.f, 0.f, 0.f, 0.f);
     // W operand of feature tile ct, k32 block kb: row ct*16 + c16, k 8g..8g+7 of the three planes
@@ -155,6 +168,29 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     Bf3 xs = split_bf3(ring[0], ring[1]);
     // the stashed tile's epilogue for one 16-feature tile
     auto epilogue = [&](int ct) {
+        if constexpr (kStage) {
+            const int idx = 64 * ct + (threadIdx.x & 63);
+            const float4 v = *reinterpret_cast<const float4*>(stg + (idx / NB4) * SROW + 4 * (idx % NB4));
+            const uint32_t off = staged_off(ct, srow0);
+            if constexpr (EPI == WS_STORE) {
+                bstore(v, yr, off);
+            } else if constexpr (EPI == WS_GELU_DROP) {
+                // (a lane holds one 4-element chunk here: its own half of the chunk pair's Philox block)
+                float u[4] = {1.f, 1.f, 1.f, 1.f};
+                if (ep.p > 0.f) gelu_keep_factors(gelu_keep_bits4(ep.seed, (uint64_t)(off >> 4), thr), keep_k, u);
+                float gl[4], gd[4];
+                gelu_erf_and_grad(v.x, gl[0], gd[0]);
+                gelu_erf_and_grad(v.y, gl[1], gd[1]);
+                gelu_erf_and_grad(v.z, gl[2], gd[2]);
+                gelu_erf_and_grad(v.w, gl[3], gd[3]);
+                bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off);
+                bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off);
+            } else {
+                const float4 f = pre[ct];
+                bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off);
+            }
+            return;
+        }
         const uint32_t off = soff + ct * 64;
         float4 v = stash[ct];
         if constexpr (EPI == WS_STORE) {
@@ -216,11 +252,22 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         // tile done: to the stash (written during the next tile)
         const int64_t m = (t0 + j * wcount) * 16 + c16;
         soff = m < M ? (uint32_t)((m * N + n0 + 4 * g) * 4) : kDrop;
+        if constexpr (kStage) {
+            srow0 = (t0 + j * wcount) * 16;
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-            stash[ct] = make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
-                                    acc[ct][3] + breg[ct].w);
-            if constexpr (EPI == WS_GELU_BWD) pre[ct] = bload(pr, soff + ct * 64);
+            for (int ct = 0; ct < CT; ++ct) {
+                *reinterpret_cast<float4*>(stg + c16 * SROW + ct * 16 + 4 * g) =
+                    make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
+                                acc[ct][3] + breg[ct].w);
+                if constexpr (EPI == WS_GELU_BWD) pre[ct] = bload(pr, staged_off(ct, srow0));
+            }
+        } else {
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                stash[ct] = make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
+                                        acc[ct][3] + breg[ct].w);
+                if constexpr (EPI == WS_GELU_BWD) pre[ct] = bload(pr, soff + ct * 64);
+            }
         }
         rc = rn;
         rn = xrow(j + 2);
@@ -231,7 +278,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
 
 template <int K, int CT, bool TRANS, int EPI>
 int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
-    const size_t lds = (size_t)16 * CT * K * 6;  // three bf16 planes
+    constexpr int NB = 16 * CT;
+    const size_t planes = (size_t)NB * K * 6;  // three bf16 planes
+    const size_t stage = (size_t)kWaves * 16 * (NB + 4) * 4;
+    const size_t lds = planes + (CT >= 4 && planes + stage <= (size_t)kLdsMax ? stage : 0);
     static bool attr = false;  // opt in above 64 KiB of dynamic LDS once per instantiation
     if (!attr) {
         const hipError_t e = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI>,
@@ -246,8 +296,6 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
                        N, Y, ep);
     return hip_status(hipGetLastError(), "asme_ws_linear");
 }
-
-constexpr int kLdsMax = 160 * 1024;
 
 // features per workgroup: 64; 96 when N / 64 does not divide the 32 workgroups of an XCD (N = 384, K = 128:
 // wider tiles at larger K run out of registers); 32 when a 64-feature block of the three bf16 planes would
