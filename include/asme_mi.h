@@ -12,7 +12,10 @@
  * Conventions
  *   - All pointers are DEVICE pointers (caller-owned; kernels never allocate or free), except the
  *     pointer ARRAYS of asme_adam_step, which are host arrays of device pointers.
- *   - fp32 storage and fp32 arithmetic; ids are int64; masks are uint8 (0 / 1).
+ *   - fp32 storage and fp32 arithmetic; ids are int64; masks are uint8 (0 / 1).  The Linear GEMMs
+ *     (asme_ws_linear, asme_linear_weight_grad) form their fp32 products on the bf16 matrix cores from
+ *     operands split exactly into three bf16 terms (six MFMAs per product tile, fp32 accumulation): error vs
+ *     float64 at or below the fp32 MFMA's (DESIGN.md §4 "bf16x6").
  *   - `stream` is a hipStream_t (NULL = default stream).  Every call is asynchronous and
  *     stream-ordered; no call synchronises the device.
  *   - Return value: 0 = OK, -1 = invalid argument, -2 = HIP launch error.  The message of the last

@@ -479,6 +479,29 @@ def test_linear_weight_grad(asme, dev, T, N, K):
     assert _rel(xx.grad, dy.double() @ w.detach().double()) < 1e-5
 
 
+@pytest.mark.parametrize("N,K", [(384, 128), (128, 512)])
+@pytest.mark.parametrize("dist", ["normal", "wide"])
+def test_linear_weight_grad_bf16x6_error_at_fp32_level(asme, dev, N, K, dist):
+    """dW = dY^T X on split-bf16 MFMAs (bf16x6): error vs float64, relative to sum |dy * x|, no worse than
+    1.25x torch's own fp32 GEMM on the same inputs (T = 20,000 tokens: a long reduction)"""
+    torch.manual_seed(N + K)
+    T = 20000
+    gen = {"normal": lambda *s: torch.randn(*s, device=dev),
+           "wide": lambda *s: torch.randn(*s, device=dev) * torch.exp(2 * torch.randn(*s, device=dev))}[dist]
+    x, dy = gen(T, K), gen(T, N)
+    L = asme._lib
+    nb = int(L.load().asme_linear_weight_grad_workspace(T, N, K))
+    ws = torch.empty(nb // 4, device=dev)
+    dw = torch.empty(N, K, device=dev)
+    L.call("asme_linear_weight_grad", L.ptr(dy), N, L.ptr(x), K, T, N, K, L.ptr(ws), nb, L.ptr(dw), None, 0,
+           L.stream())
+    ref = dy.double().t() @ x.double()
+    scale = dy.double().abs().t() @ x.double().abs()
+    ours = ((dw.double() - ref).abs() / scale).max().item()
+    theirs = (((dy.t() @ x).double() - ref).abs() / scale).max().item()
+    assert ours <= 1.25 * theirs + 1e-9, (ours, theirs)
+
+
 @pytest.mark.parametrize("d", [32, 64, 128])
 @pytest.mark.parametrize("nq,V", [(5, 37), (130, 1000), (300, 4099)])
 @pytest.mark.parametrize("with_bias", [False, True])
