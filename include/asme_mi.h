@@ -80,6 +80,11 @@ int asme_layernorm_fwd(const float* x, int64_t n_rows, int64_t dim, const float*
                        float* y, float* stats, void* stream);
 int asme_layernorm_bwd(const float* x, int64_t n_rows, int64_t dim, const float* w, const float* stats,
                        const float* dy, float* dx, int accumulate, float* partials, int64_t n_partials, void* stream);
+/* dx = LN backward of dy + dadd (nullable): the first block input feeds both its pre-LN and the residual, so its
+ * two gradients are summed in the same pass (autograd's separate add, transformer_layers.py:120-130) */
+int asme_layernorm_bwd_add(const float* x, int64_t n_rows, int64_t dim, const float* w, const float* stats,
+                           const float* dy, const float* dadd, float* dx, float* partials, int64_t n_partials,
+                           void* stream);
 /* s = drop_b(res + drop_a(y)); ln_out = LN(s) (LN optional: w == NULL) */
 int asme_residual_ln_fwd(const float* res, const float* y, int64_t n_rows, int64_t dim, float p_a, uint64_t seed_a,
                          float p_b, uint64_t seed_b, const float* w, const float* b, float eps, float* s_out,

@@ -32,6 +32,7 @@ SIGNATURES = {
     "asme_gather_sum_bwd": [p, p, i64, i64, i32, p, i64, i64, p],
     "asme_layernorm_fwd": [p, i64, i64, p, p, f32, p, p, p],
     "asme_layernorm_bwd": [p, i64, i64, p, p, p, p, i32, p, i64, p],
+    "asme_layernorm_bwd_add": [p, i64, i64, p, p, p, p, p, p, i64, p],
     "asme_residual_ln_fwd": [p, p, i64, i64, f32, u64, f32, u64, p, p, f32, p, p, p, p],
     "asme_residual_ln_bwd": [p, i64, i64, f32, u64, f32, u64, p, p, p, p, p, p, p, i64, p],
     "asme_attention_set_mode": [i32],

@@ -43,7 +43,8 @@ template <class R>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, int64_t T, int D,
                                                      const float* __restrict__ w, const float* __restrict__ stats,
                                                      const float* __restrict__ dy, float* __restrict__ dx,
-                                                     int accumulate, float* __restrict__ partials) {
+                                                     int accumulate, const float* __restrict__ dadd,
+                                                     float* __restrict__ partials) {
     const int lane = threadIdx.x & 63, sub = lane % R::LPR, wave = threadIdx.x >> 6;
     float acc[2][R::NV][R::W];
     row_zero<R>(acc[0]);
@@ -71,9 +72,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
             }
         row_ln_bwd<R>(g, xh, w, r, sub, D, gx);
         if (!live) continue;
-        if (accumulate) {
+        if (accumulate || dadd) {  // dx = LN'(dy) + dx (accumulate) or + dadd (a second gradient of x)
             RowVals<R> old;
-            row_load<R>(dx + t * D, sub, D, old);
+            row_load<R>((dadd ? dadd : dx) + t * D, sub, D, old);
 #pragma unroll
             for (int j = 0; j < R::NV; ++j)
 #pragma unroll
@@ -261,10 +262,27 @@ ASME_API int asme_layernorm_bwd(const float* x, int64_t n_rows, int64_t dim, con
     if (with_row_layout(dim, [&](auto layout) {
             using R = decltype(layout);
             hipLaunchKernelGGL(ln_bwd_kernel<R>, dim3((unsigned)n_partials), dim3(256), lds, (hipStream_t)stream, x,
-                               n_rows, (int)dim, w, stats, dy, dx, accumulate, partials);
+                               n_rows, (int)dim, w, stats, dy, dx, accumulate, (const float*)nullptr, partials);
         }))
         return -1;
     ASME_LAUNCH_CHECK("asme_layernorm_bwd");
+}
+
+// dx = LN backward of dy + dadd: a tensor feeding both a LayerNorm and a residual (the first pre-LN block
+// input) gets its two gradients summed here instead of by a separate add pass.  dadd nullable.
+ASME_API int asme_layernorm_bwd_add(const float* x, int64_t n_rows, int64_t dim, const float* w, const float* stats,
+                                    const float* dy, const float* dadd, float* dx, float* partials,
+                                    int64_t n_partials, void* stream) {
+    ASME_CHECK_ARG(x && w && stats && dy && dx && partials && n_partials >= 1, "asme_layernorm_bwd_add: bad argument");
+    if (n_rows == 0) return 0;
+    const size_t lds = (size_t)kWaves * 2 * dim * sizeof(float);
+    if (with_row_layout(dim, [&](auto layout) {
+            using R = decltype(layout);
+            hipLaunchKernelGGL(ln_bwd_kernel<R>, dim3((unsigned)n_partials), dim3(256), lds, (hipStream_t)stream, x,
+                               n_rows, (int)dim, w, stats, dy, dx, 0, dadd, partials);
+        }))
+        return -1;
+    ASME_LAUNCH_CHECK("asme_layernorm_bwd_add");
 }
 
 ASME_API int asme_residual_ln_fwd(const float* res, const float* y, int64_t n_rows, int64_t dim, float p_a,

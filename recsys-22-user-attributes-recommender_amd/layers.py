@@ -252,7 +252,7 @@ class TransformerLayer(nn.Module):
         b0 = blocks[0]
         if FUSED_STACK and fused.fusable(x.shape[-1], b0.feed_forward.w_1.weight.shape[0], b0.attention.heads, x):
             return fused.transformer_stack(x, key_valid, blocks, causal, tr)
-        ln = ops.layer_norm(x, blocks[0].input_sublayer.norm)
+        x, ln = ops.layer_norm_pass(x, blocks[0].input_sublayer.norm)
         for i, blk in enumerate(blocks):
             att, ff = blk.attention, blk.feed_forward
             w_qkv, b_qkv = att.qkv_weights()

@@ -566,6 +566,43 @@ def layer_norm(x, norm: torch.nn.LayerNorm):
     return _LayerNormFn.apply(x, norm.weight, norm.bias, norm.eps)
 
 
+class _LayerNormPassFn(torch.autograd.Function):
+    """(x, LN(x)) for a tensor that feeds both a LayerNorm and a residual (the first pre-LN block's input,
+    transformer_layers.py:120-130): the backward sums the two gradients of x inside the LN backward pass."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps: float):
+        shape = x.shape
+        D = shape[-1]
+        x2 = _f32(x).reshape(-1, D)
+        n = x2.shape[0]
+        y = torch.empty_like(x2)
+        stats = torch.empty(n, 2, device=x.device, dtype=torch.float32)
+        call("asme_layernorm_fwd", ptr(x2), n, D, ptr(w), ptr(b), eps, ptr(y), ptr(stats), stream())
+        ctx.save_for_backward(x2, w, stats)
+        return x.view_as(x), y.view(shape)
+
+    @staticmethod
+    def backward(ctx, d_x, dy):
+        x2, w, stats = ctx.saved_tensors
+        n, D = x2.shape
+        if dy is None:
+            return d_x, None, None, None
+        dy2 = _f32(dy).reshape(n, D)
+        dadd = None if d_x is None else _f32(d_x).reshape(n, D)
+        dx = torch.empty_like(x2)
+        part = torch.empty(_N_PARTIALS, 2 * D, device=x2.device, dtype=torch.float32)
+        call("asme_layernorm_bwd_add", ptr(x2), n, D, ptr(w), ptr(stats), ptr(dy2), ptr(dadd), ptr(dx), ptr(part),
+             _N_PARTIALS, stream())
+        red = _reduce_partials(part, 2 * D)
+        return dx.view(dy.shape), red[:D], red[D:], None
+
+
+def layer_norm_pass(x, norm: torch.nn.LayerNorm):
+    """(x, norm(x)); use the returned x wherever x is used again so its gradients meet in one pass"""
+    return _LayerNormPassFn.apply(x, norm.weight, norm.bias, norm.eps)
+
+
 class _ResidualLNFn(torch.autograd.Function):
     """SublayerConnection epilogue + block dropout + next pre-LN (transformer_layers.py:120-130, 251-258):
     s = drop_b(res + drop_a(y));  ln = LN(s)"""
