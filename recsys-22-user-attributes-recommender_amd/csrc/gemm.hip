@@ -158,7 +158,9 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         __syncthreads();
     }
     // partial slab: part[chunk][n][k]; lane holds rows n = ... + 4g + q, column k = ... + c16
-    float* P = part + chunk * (int64_t)N * K;
+    // chunk slab: [N x K dW partial | N db partial (when db is requested)]
+    const int64_t slab = (int64_t)N * K + (bias_part != nullptr ? N : 0);
+    float* P = part + chunk * slab;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -181,15 +183,19 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
                 s.x += v.x;
                 s.y += v.y;
             }
-            *reinterpret_cast<float2*>(bias_part + chunk * (int64_t)N + n0 + 2 * threadIdx.x) = s;
+            *reinterpret_cast<float2*>(P + (int64_t)N * K + n0 + 2 * threadIdx.x) = s;
         }
     }
 }
 
 // column sums with a fixed order (see reduce_rows_kernel in embedding.hip)
 constexpr int kRedCols = 64, kRedGroups = 16;
-__global__ __launch_bounds__(1024) void sum_slabs_kernel(const float* __restrict__ part, int64_t nrows, int64_t width,
-                                                         float* __restrict__ out, int accumulate) {
+// Column c of the slabs (row stride width_w + width_b) goes to out_w[c] (c < width_w) or out_b[c - width_w]:
+// the dW and db partials of one weight gradient reduced by one launch.
+__global__ __launch_bounds__(1024) void sum_slabs_kernel(const float* __restrict__ part, int64_t nrows,
+                                                         int64_t width_w, float* __restrict__ out_w, int64_t width_b,
+                                                         float* __restrict__ out_b, int accumulate) {
+    const int64_t width = width_w + width_b;
     __shared__ float red[kRedGroups][kRedCols];
     const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
     const int64_t c = (int64_t)blockIdx.x * kRedCols + col;
@@ -212,7 +218,10 @@ __global__ __launch_bounds__(1024) void sum_slabs_kernel(const float* __restrict
         if (grp < h) red[grp][col] += red[grp + h][col];
         __syncthreads();
     }
-    if (grp == 0 && c < width) out[c] = accumulate ? out[c] + red[0][col] : red[0][col];
+    if (grp == 0 && c < width) {
+        float* o = c < width_w ? out_w + c : out_b + (c - width_w);
+        *o = accumulate ? *o + red[0][col] : red[0][col];
+    }
 }
 
 struct Plan {
@@ -249,7 +258,7 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
     const Plan p = make_plan(n_tokens, out_features, in_features);
     hipStream_t s = (hipStream_t)stream;
     float* part = workspace;
-    float* bpart = db ? workspace + p.nchunks * out_features * in_features : nullptr;
+    float* bpart = db ? workspace : nullptr;  // (a flag: the bias partials sit in each chunk's slab)
     const int64_t ntiles = ((out_features + kTile - 1) / kTile) * ((in_features + kTile - 1) / kTile);
     const dim3 grid((unsigned)(ntiles * ((p.nchunks + 7) / 8) * 8));
     static bool attr = false;  // 96 KiB of dynamic LDS: opt in once
@@ -261,11 +270,8 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
     }
     hipLaunchKernelGGL(weight_grad_kernel, grid, dim3(kWgThreads), 2 * kBuf * 16, s, dy, ld_dy, x, ld_x, n_tokens, (int)out_features,
                        (int)in_features, p.chunk_rows, part, bpart);
-    const int64_t width = out_features * in_features;
-    hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width + kRedCols - 1) / kRedCols)), dim3(1024), 0, s, part,
-                       p.nchunks, width, dw, accumulate);
-    if (db)
-        hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((out_features + kRedCols - 1) / kRedCols)), dim3(1024),
-                           0, s, bpart, p.nchunks, out_features, db, accumulate);
+    const int64_t width_w = out_features * in_features, width_b = db ? out_features : 0;
+    hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width_w + width_b + kRedCols - 1) / kRedCols)), dim3(1024), 0,
+                       s, part, p.nchunks, width_w, dw, width_b, db, accumulate);
     ASME_LAUNCH_CHECK("asme_linear_weight_grad");
 }
