@@ -9,6 +9,7 @@ Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline acc
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import platform
@@ -28,6 +29,13 @@ PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
 # ceiling is the dense bf16 MFMA peak (2516.6 TF/s = 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz) over 6
 PEAK_BF16X6_TFS = 2516.6 / 6
 BF16X6_KERNELS = {"asme_ws_linear", "asme_linear_weight_grad"}
+
+
+def instrumented_steps(steps):
+    """timed steps whose C-ABI calls carry HIP start/stop events for the per-kernel rooflines: the last two.
+    The events cost ~2 us of device time each (~0.25 ms per step with every timed kernel bracketed, measured
+    with --kernel-events off), so bracketing every step would understate the step rate by ~3 %."""
+    return min(steps, 2)
 
 
 def mfma_peak(name):
@@ -52,6 +60,8 @@ def parse():
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--table-grad", choices=["sparse", "dense"], default="sparse")
     ap.add_argument("--ids", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--kernel-events", choices=["on", "off"], default="on",
+                    help="HIP events around the timed kernels (off: no per-kernel rooflines; for A/B of their cost)")
     ap.add_argument("--producer", choices=["resident", "gpu"], default="resident",
                     help="resident: two pre-built device batches; gpu: every step samples its batch from sessions "
                          "in HBM with the GPU pos/neg sampler (asme_posneg_sample) inside the timed step")
@@ -181,8 +191,8 @@ def bench_bert4rec(args, asme, dev, world, rank):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with timer:
-        for i in range(args.steps):
+    for i in range(args.steps):
+        with timer if i >= args.steps - instrumented_steps(args.steps) else contextlib.nullcontext():
             step(args.warmup + i)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -297,7 +307,8 @@ def main():
     torch.cuda.synchronize()
 
     # per-kernel device time of the dominant kernel (HIP events on the launching stream)
-    timer = asme._lib.KernelTimer(["asme_adam_rows_step", "asme_attention_fwd", "asme_attention_bwd",
+    timer = asme._lib.KernelTimer([] if args.kernel_events == "off" else [
+                                   "asme_adam_rows_step", "asme_attention_fwd", "asme_attention_bwd",
                                    "asme_embedding_fwd", "asme_embedding_bwd", "asme_lazy_adam_catch_up",
                                    "asme_lazy_adam_apply", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
@@ -315,8 +326,8 @@ def main():
         _orig_release(plan)
 
     asme.ops.SparseTablePlan.release = _release
-    with timer:
-        for i in range(args.steps):
+    for i in range(args.steps):
+        with timer if i >= args.steps - instrumented_steps(args.steps) else contextlib.nullcontext():
             step_fn(get_batch(args.warmup + i), i)
     # lazily deferred zero-gradient Adam updates of the item table are part of the work: apply them all
     # (exact dense-Adam state) inside the timed region, timed on its own
