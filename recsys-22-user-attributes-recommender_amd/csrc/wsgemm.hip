@@ -50,6 +50,11 @@ struct WsEpi {
     const float* pre_in; // WS_GELU_BWD: activation factor in
     float p;             // dropout probability (0: none)
     uint64_t seed;
+    // split-K over K = 512 (two K = 256 launches): row strides of X and (non-trans) W, the first k column, and
+    // WS_STORE accumulating into Y (the second half)
+    int64_t ldx, ldw;
+    int kofs;
+    int accumulate;
 };
 
 __device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s ^ (r & 15)); }
@@ -94,11 +99,11 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         const int r = TRANS ? i % NB : i / K8, s8 = TRANS ? i / NB : i % K8;
         float4 a, b;
         if (!TRANS) {
-            const float* w = W + (int64_t)(n0 + r) * K + 8 * s8;
+            const float* w = W + (int64_t)(n0 + r) * ep.ldw + ep.kofs + 8 * s8;
             a = *reinterpret_cast<const float4*>(w);
             b = *reinterpret_cast<const float4*>(w + 4);
         } else {
-            const float* w = W + (int64_t)(8 * s8) * N + n0 + r;
+            const float* w = W + (int64_t)(ep.kofs + 8 * s8) * N + n0 + r;
             a = make_float4(w[0], w[N], w[2 * N], w[3 * N]);
             b = make_float4(w[4 * N], w[5 * N], w[6 * N], w[7 * N]);
         }
@@ -120,7 +125,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const int64_t t0 = lo + widx;
     auto xrow = [&](int64_t j) -> const float* {  // clamped rows are computed and dropped at the store
         int64_t m = (t0 + (j < my_tiles ? j : my_tiles - 1) * wcount) * 16 + c16;
-        return X + (m < M ? m : M - 1) * K + 8 * g;
+        return X + (m < M ? m : M - 1) * ep.ldx + ep.kofs + 8 * g;
     };
     const __amdgpu_buffer_rsrc_t yr = rsrc(Y, M * N * 4);
     const __amdgpu_buffer_rsrc_t pr = rsrc(EPI == WS_GELU_DROP ? (const void*)ep.pre_out : (const void*)ep.pre_in,
@@ -173,7 +178,12 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             const float4 v = *reinterpret_cast<const float4*>(stg + (idx / NB4) * SROW + 4 * (idx % NB4));
             const uint32_t off = staged_off(ct, srow0);
             if constexpr (EPI == WS_STORE) {
-                bstore(v, yr, off);
+                if (ep.accumulate) {
+                    const float4 o = bload(yr, off);
+                    bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off);
+                } else {
+                    bstore(v, yr, off);
+                }
             } else if constexpr (EPI == WS_GELU_DROP) {
                 // (a lane holds one 4-element chunk here: its own half of the chunk pair's Philox block)
                 float u[4] = {1.f, 1.f, 1.f, 1.f};
@@ -194,6 +204,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         const uint32_t off = soff + ct * 64;
         float4 v = stash[ct];
         if constexpr (EPI == WS_STORE) {
+            if (ep.accumulate) {
+                const float4 o = bload(yr, off);
+                v = make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
+            }
             bstore(v, yr, off);
         } else if constexpr (EPI == WS_GELU_DROP) {
             float u[4] = {1.f, 1.f, 1.f, 1.f};
@@ -354,9 +368,20 @@ ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W
     ASME_CHECK_ARG(((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 15) == 0 && ((uintptr_t)W & 15) == 0,
                    "asme_ws_linear: 16-B alignment");
     ASME_CHECK_ARG(p >= 0.f && p < 1.f, "asme_ws_linear: dropout probability in [0, 1)");
-    const WsEpi ep{bias, pre_out, pre_in, p, seed};
+    const WsEpi ep{bias, pre_out, pre_in, p, seed, K, K, 0, 0};
     const int ct = pick_ct((int)N, (int)K);
     hipStream_t s = (hipStream_t)stream;
+    // K = 512 plain stores: two K = 256 halves with 64-feature blocks (the 512-deep split W block only fits 32
+    // features, which splits and re-reads X four times); the second half accumulates into Y
+    if (K == 512 && epi == 0 && pick_ct((int)N, 256) == 4) {
+        const WsEpi e1{bias, nullptr, nullptr, 0.f, 0, 512, 512, 0, 0};
+        const WsEpi e2{nullptr, nullptr, nullptr, 0.f, 0, 512, 512, 256, 1};
+        const int rc = trans ? launch_ws<256, 4, true, WS_STORE>(X, M, W, (int)N, Y, e1, s)
+                             : launch_ws<256, 4, false, WS_STORE>(X, M, W, (int)N, Y, e1, s);
+        if (rc != 0) return rc;
+        return trans ? launch_ws<256, 4, true, WS_STORE>(X, M, W, (int)N, Y, e2, s)
+                     : launch_ws<256, 4, false, WS_STORE>(X, M, W, (int)N, Y, e2, s);
+    }
     if (trans) {
         if (epi == 0) return dispatch_k<true, WS_STORE>((int)K, ct, X, M, W, (int)N, Y, ep, s);
         if (epi == 1) return dispatch_k<true, WS_GELU_DROP>((int)K, ct, X, M, W, (int)N, Y, ep, s);

@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1; echo "tests rc=$?" >> gpurun_out/t.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-timeout -k 10 300 python bench.py > gpurun_out/b1.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --cpu-baseline 0 > gpurun_out/b1.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --cpu-baseline 0 > gpurun_out/b2.log 2>&1 || exit 1
