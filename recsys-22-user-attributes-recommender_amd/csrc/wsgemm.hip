@@ -26,9 +26,9 @@
 // backward epilogue a single multiply: no Philox, erf or exp in the input-gradient GEMM.
 // Dropout decisions are exactly those of asme_gelu_dropout_fwd/bwd (norm.hip): one Philox block per pair of
 // 4-element chunks, 16-bit uniforms, salt 5 (common.h gelu_keep_bits8).
-// Measured at M = 204800 (tools/ws_bench.py; fp32-equivalent rate, bf16x6 ceiling 2516.6 / 6 = 419 TF/s):
-// K=128 -> N=128 174 TF/s, K=384 -> N=128 (input gradient) 179, K=128 -> N=512 124, K=512 -> N=128 131;
-// the fp32-MFMA version of this kernel (157 TF/s ceiling): 113-126.
+// Measured at M = 204800 (tools/probe/ab_ws.py; fp32-equivalent rate, bf16x6 ceiling 2516.6 / 6 = 419 TF/s):
+// K=128 -> N=128 165 TF/s, K=384 -> N=128 (input gradient) 181, K=128 -> N=512 142 (row-staged stores),
+// K=512 -> N=128 145 (as two K = 256 halves); the fp32-MFMA version of this kernel (157 TF/s ceiling): 113-126.
 #include "common.h"
 
 using namespace asme;
