@@ -188,17 +188,18 @@ int asme_adam_rows_step(float* param, float* exp_avg, float* exp_avg_sq, int64_t
 
 /* Lazy dense Adam ("exact catch-up"): bit-identical to asme_adam_rows_step every step, but a row with a
  * zero gradient is only rewritten when it is next read.  last_step (rows int32) = step each row is up to
- * date with; hist (capacity, 8) float = per-step constants written by asme_lazy_adam_record_step. */
-int asme_lazy_adam_record_step(float* hist, int64_t step, float lr, float beta1, float beta2, float eps,
-                               float weight_decay, void* stream);
+ * date with; hist (hist_rows, 8) float = per-step constants written by asme_lazy_adam_record_step; every
+ * step named (step / upto) must be < hist_rows, else the call fails with ASME_ERR_ARG. */
+int asme_lazy_adam_record_step(float* hist, int64_t hist_rows, int64_t step, float lr, float beta1, float beta2,
+                               float eps, float weight_decay, void* stream);
 /* replay zero-gradient steps (last_step[r], upto] for rows[0..*count) (rows == NULL: all rows 0..cap) */
 int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, int64_t cap, int32_t* last_step,
                             float* param, float* exp_avg, float* exp_avg_sq, int64_t dim, const float* hist,
-                            int64_t upto, void* stream);
+                            int64_t hist_rows, int64_t upto, void* stream);
 /* step `step` with the real gradient grad_rows[s] for rows[s], s < *count (rows already at step-1) */
 int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap, const float* grad_rows,
                          int32_t* last_step, float* param, float* exp_avg, float* exp_avg_sq, int64_t dim,
-                         const float* hist, int64_t step, void* stream);
+                         const float* hist, int64_t hist_rows, int64_t step, void* stream);
 
 /* ---- input producers: sessions in HBM as flat item ids + offsets (n_sessions + 1) ---------
  * asme_session_batch: collate (data/collate.py:42-111): out (batch, seq_len) = the last min(len - drop_last,

@@ -423,10 +423,11 @@ __global__ __launch_bounds__(256) void lazy_apply_kernel(const int64_t* __restri
     }
 }  // namespace
 
-// hist[step] = the Adam constants of `step` (hist: (capacity, 8) floats on the device)
-ASME_API int asme_lazy_adam_record_step(float* hist, int64_t step, float lr, float beta1, float beta2, float eps,
-                                        float weight_decay, void* stream) {
+// hist[step] = the Adam constants of `step` (hist: (hist_rows, 8) floats on the device; step < hist_rows)
+ASME_API int asme_lazy_adam_record_step(float* hist, int64_t hist_rows, int64_t step, float lr, float beta1,
+                                        float beta2, float eps, float weight_decay, void* stream) {
     ASME_CHECK_ARG(hist && step >= 1, "asme_lazy_adam_record_step: bad argument");
+    ASME_CHECK_ARG(step < hist_rows, "asme_lazy_adam_record_step: step beyond the history capacity");
     const AdamHyper hp = make_hyper(lr, beta1, beta2, eps, weight_decay, step);
     hipLaunchKernelGGL(record_step_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hist, step, hp);
     ASME_LAUNCH_CHECK("asme_lazy_adam_record_step");
@@ -435,8 +436,9 @@ ASME_API int asme_lazy_adam_record_step(float* hist, int64_t step, float lr, flo
 // bring rows[0..count) (rows == NULL: every row 0..cap) up to date through step `upto` with zero gradient
 ASME_API int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, int64_t cap, int32_t* last_step,
                                      float* param, float* exp_avg, float* exp_avg_sq, int64_t dim, const float* hist,
-                                     int64_t upto, void* stream) {
+                                     int64_t hist_rows, int64_t upto, void* stream) {
     ASME_CHECK_ARG(last_step && param && exp_avg && exp_avg_sq && hist, "asme_lazy_adam_catch_up: null pointer");
+    ASME_CHECK_ARG(upto < hist_rows, "asme_lazy_adam_catch_up: step beyond the history capacity");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && upto >= 0 && upto < (1LL << 31), "asme_lazy_adam_catch_up: bad shape");
     if (cap == 0 || upto == 0) return 0;
     if (v4_ok(dim, param, exp_avg, exp_avg_sq)) {
@@ -458,9 +460,10 @@ ASME_API int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, 
 
 ASME_API int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap, const float* grad_rows,
                                   int32_t* last_step, float* param, float* exp_avg, float* exp_avg_sq, int64_t dim,
-                                  const float* hist, int64_t step, void* stream) {
+                                  const float* hist, int64_t hist_rows, int64_t step, void* stream) {
     ASME_CHECK_ARG(rows && count && grad_rows && last_step && param && exp_avg && exp_avg_sq && hist,
                    "asme_lazy_adam_apply: null pointer");
+    ASME_CHECK_ARG(step < hist_rows, "asme_lazy_adam_apply: step beyond the history capacity");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && step >= 1, "asme_lazy_adam_apply: bad shape");
     if (cap == 0) return 0;
     if (v4_ok(dim, param, exp_avg, exp_avg_sq) && ((uintptr_t)grad_rows & 15) == 0) {

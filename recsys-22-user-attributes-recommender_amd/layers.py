@@ -292,7 +292,7 @@ class FFNSequenceRepresentationModifierComponent(nn.Module):
 
     def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
         lin, _, norm = self.transform
-        return ops.layer_norm(ops.gelu_dropout(F.linear(encoded, lin.weight, lin.bias), 0.0), norm)
+        return ops.layer_norm(ops.gelu_dropout(ops.linear(encoded, lin.weight, lin.bias), 0.0), norm)
 
 
 def _merge(x: torch.Tensor, ctx: torch.Tensor, fn: str) -> torch.Tensor:
@@ -320,7 +320,7 @@ class PostFusionContextSequenceRepresentationModifierComponent(nn.Module):
     def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
         x = _merge(encoded, _attribute_sum(self.postfusion_attribute_embeddings, sequence), self.merge_function)
         lin, _, norm = self.transform
-        return ops.layer_norm(ops.gelu_dropout(F.linear(x, lin.weight, lin.bias), 0.0), norm)
+        return ops.layer_norm(ops.gelu_dropout(ops.linear(x, lin.weight, lin.bias), 0.0), norm)
 
 
 class PostFusionIdentitySequenceRepresentationModifierLayer(nn.Module):

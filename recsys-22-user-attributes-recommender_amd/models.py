@@ -32,6 +32,9 @@ class SequenceRecommenderModel(nn.Module):
         self._sequence_representation_modifier_layer = sequence_representation_modifier_layer
         self._projection_layer = projection_layer
         self.register_state_dict_pre_hook(lambda module, prefix, keep_vars: module.flush_table())
+        # before a load: bring the table and its Adam moments current, so the loaded rows are not later
+        # "caught up" with zero-gradient steps they never missed
+        self.register_load_state_dict_pre_hook(lambda module, *args: module.flush_table())
 
     def flush_table(self):
         """Apply pending lazy-Adam updates of the item table (see ops.LazyTableState)."""

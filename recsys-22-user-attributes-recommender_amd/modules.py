@@ -11,7 +11,9 @@ Differences that do not change results:
     (B, L, |V|) logits tensor is never built);
   * validation of sasrec-neg uses predict_step (the reference calls an undefined self.predict, Q13);
   * `table_grad="sparse"` keeps the item-table gradient row-sparse and lets FusedAdam apply the exact
-    dense Adam update (Q7) without a dense (|V|, d) gradient.
+    dense Adam update (Q7) without a dense (|V|, d) gradient.  It is the default (table_grad=None) for
+    every model whose item table is only read through the gather kernels (table_grad_sparse_ok());
+    tied / full-catalogue heads that read the whole table keep the dense gradient.
 Batch keys: item, item.target, positive_samples, negative_samples (data/datasets/__init__.py:5-14).
 """
 from __future__ import annotations
@@ -50,9 +52,10 @@ except Exception:  # pragma: no cover - Lightning is not part of this image
             pass
 
 
-# catalogue size from which validation ranks targets with the fused kernel by default (a (1024, 2^20)
-# fp32 prediction tensor is 4 GiB; the reference materialises (B, |V|, d) even before that)
-FUSED_EVAL_MIN_ITEMS = 1 << 20
+# catalogue size from which validation ranks targets with the fused kernel (asme_catalog_rank) by default: every
+# size -- the ranks (and so NDCG / recall / MRR) are those of the materialised scores, without the (B, |V|)
+# prediction tensor (4 GiB at B = 1024, |V| = 2^20) or its sort; fused_eval=False materialises them
+FUSED_EVAL_MIN_ITEMS = 0
 
 
 def get_padding_mask(sequence: torch.Tensor, tokenizer) -> torch.Tensor:
@@ -89,7 +92,9 @@ def build_eval_step_return_dict(input_sequence, predictions, targets, mask=None)
 class _TableGradMixin:
     """Row-sparse item-table gradients (see ops.SparseTablePlan / optim.FusedAdam)."""
 
-    def _init_table_grad(self, mode: str):
+    def _init_table_grad(self, mode: Optional[str]):
+        if mode is None:
+            mode = "sparse" if self.model.table_grad_sparse_ok() else "dense"
         if mode not in ("dense", "sparse"):
             raise ValueError("table_grad must be 'dense' or 'sparse'")
         if mode == "sparse" and not self.model.table_grad_sparse_ok():
@@ -111,6 +116,17 @@ class _TableGradMixin:
             tg.plan.release()
         tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map)
 
+    @staticmethod
+    def _ids_i64(batch, keys):
+        """the id tensors the sparse plan registers must be the very tensors the model later reads: normalise
+        int32 / non-contiguous dataloader ids to int64 contiguous once, up front"""
+        out = dict(batch)
+        for k in keys:
+            t = out.get(k)
+            if t is not None and (t.dtype != torch.int64 or not t.is_contiguous()):
+                out[k] = t.to(torch.int64).contiguous()
+        return out
+
     def _flush_table(self):
         self.model.flush_table()
 
@@ -122,7 +138,7 @@ class _TableGradMixin:
 class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
     def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
                  beta_2: float = 0.998, weight_decay: float = 1e-3,
-                 loss_function=None, table_grad: str = "dense", fused_eval: Optional[bool] = None):
+                 loss_function=None, table_grad: Optional[str] = None, fused_eval: Optional[bool] = None):
         super().__init__()
         self.model = model
         self.learning_rate, self.beta_1, self.beta_2, self.weight_decay = learning_rate, beta_1, beta_2, weight_decay
@@ -135,6 +151,7 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         self.fused_eval = fused_eval
 
     def training_step(self, batch, batch_idx):
+        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME))
         input_seq = batch[ITEM_SEQ_ENTRY_NAME]
         padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
         pos, neg = batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]
@@ -230,7 +247,7 @@ def _rows_cross_entropy(model, sequence, rows, targets, pad: int) -> torch.Tenso
 
 class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
     def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
-                 beta_2: float = 0.998, weight_decay: float = 0, loss_function=None, table_grad: str = "dense"):
+                 beta_2: float = 0.998, weight_decay: float = 0, loss_function=None, table_grad: Optional[str] = None):
         super().__init__()
         self.model = model
         self.learning_rate, self.beta_1, self.beta_2, self.weight_decay = learning_rate, beta_1, beta_2, weight_decay
@@ -243,6 +260,7 @@ class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
         return self.model(build_model_input(self.model, self.item_tokenizer, batch))
 
     def training_step(self, batch, batch_idx):
+        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME,))
         target = batch[TARGET_ENTRY_NAME]
         pad = self.item_tokenizer.pad_token_id
         ce_loss = isinstance(self.loss_function, (SASRecFullSequenceCrossEntropyLoss, SingleTargetCrossEntropyLoss))
@@ -295,7 +313,7 @@ class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
 class MaskedTrainingModule(_TableGradMixin, _Base):
     def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
                  beta_2: float = 0.998, weight_decay: float = 0.001, num_warmup_steps: int = 10000,
-                 table_grad: str = "dense"):
+                 table_grad: Optional[str] = None):
         super().__init__()
         self.model = model
         self.learning_rate, self.beta_1, self.beta_2 = learning_rate, beta_1, beta_2
@@ -309,6 +327,7 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         return self.model(build_model_input(self.model, self.item_tokenizer, batch))
 
     def training_step(self, batch, batch_idx):
+        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME,))
         target = batch[TARGET_ENTRY_NAME]
         if target.dim() > 2:
             raise NotImplementedError("basket (multi-target) masked training is outside the MI355X hot path")

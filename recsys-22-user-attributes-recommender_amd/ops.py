@@ -71,11 +71,14 @@ class LazyTableState:
         self.step = 0
 
     def record(self, step: int, lr, b1, b2, eps, wd):
-        if step >= self.hist.shape[0]:
-            grown = torch.zeros(2 * self.hist.shape[0], 8, dtype=torch.float32, device=self.hist.device)
+        cap = self.hist.shape[0]
+        while step >= cap:  # a resumed run can start at any step
+            cap *= 2
+        if cap != self.hist.shape[0]:
+            grown = torch.zeros(cap, 8, dtype=torch.float32, device=self.hist.device)
             grown[: self.hist.shape[0]] = self.hist
             self.hist = grown
-        call("asme_lazy_adam_record_step", ptr(self.hist), step, lr, b1, b2, eps, wd, stream())
+        call("asme_lazy_adam_record_step", ptr(self.hist), cap, step, lr, b1, b2, eps, wd, stream())
         self.step = step
 
     def catch_up(self, rows: Optional[torch.Tensor] = None, count: Optional[torch.Tensor] = None, cap: int = 0):
@@ -85,13 +88,13 @@ class LazyTableState:
         if rows is None:
             cap = V
         call("asme_lazy_adam_catch_up", ptr(rows), ptr(count), cap, ptr(self.last_step), ptr(self.param),
-             ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist), self.step, stream())
+             ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist), self.hist.shape[0], self.step, stream())
 
     def apply(self, plan: "SparseTablePlan", step: int):
         D = self.param.shape[1]
         call("asme_lazy_adam_apply", ptr(plan.unique), ptr(plan.count), plan.capacity, ptr(plan.grad_rows),
              ptr(self.last_step), ptr(self.param), ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist),
-             step, stream())
+             self.hist.shape[0], step, stream())
 
     def flush(self):
         """bring every row up to date (before evaluation, checkpointing or any other reader)."""
@@ -446,19 +449,40 @@ def _weight_grad(dy2, x2, has_bias: bool):
     return dw, db
 
 
+def _tile4_ok(*ts) -> bool:
+    """shapes the general fp32-MFMA Linear kernels (csrc/linear.hip) take: contiguous, every row a multiple
+    of 4 floats, 16-B aligned"""
+    return all(t.is_contiguous() and t.shape[-1] % 4 == 0 and t.data_ptr() % 16 == 0 for t in ts)
+
+
 def _linear_fwd(x2, w, b):
+    """x2 . w^T + b: the weight-stationary bf16x6 GEMM where it tiles (K in {128..512}), otherwise the
+    general fp32-MFMA kernel (asme_linear_fwd); a library GEMM only for rows that are not a multiple of 4
+    floats (no kernel here tiles them)"""
     M, K = x2.shape
     N = w.shape[0]
-    if _ws_ok(M, K, N) and w.is_contiguous() and (b is None or b.is_contiguous()):
+    w = _f32(w)
+    b = _f32(b) if b is not None else None
+    if _ws_ok(M, K, N):
         return _ws(x2, w, N, 0, bias=b)
+    if _tile4_ok(x2, w) and N % 4 == 0:
+        y = torch.empty(M, N, device=x2.device, dtype=torch.float32)
+        call("asme_linear_fwd", ptr(x2), K, M, K, ptr(w), ptr(b), N, ptr(y), N, stream())
+        return y
     return torch.nn.functional.linear(x2, w, b)
 
 
 def _linear_dx(dy2, w):
+    """dy2 . w (the input gradient of a Linear with weight w: N x K), same kernel choice as _linear_fwd"""
     M, N = dy2.shape
     K = w.shape[1]
-    if _ws_ok(M, N, K) and w.is_contiguous():
+    w = _f32(w)
+    if _ws_ok(M, N, K):
         return _ws(dy2, w, K, 1)
+    if _tile4_ok(dy2, w) and N % 4 == 0:
+        dx = torch.empty(M, K, device=dy2.device, dtype=torch.float32)
+        call("asme_linear_dx", ptr(dy2), N, M, N, ptr(w), K, ptr(dx), K, 0, stream())
+        return dx
     return dy2 @ w
 
 

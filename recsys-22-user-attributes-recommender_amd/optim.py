@@ -32,6 +32,25 @@ class FusedAdam(torch.optim.Optimizer):
                 if tg is not None and tg.lazy is not None:
                     tg.lazy.flush()
 
+    def state_dict(self):
+        """flush first: lazily-deferred table rows must be current in the saved moments"""
+        self.flush()
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        """flush, then drop every lazy table state: it holds references to the old moment tensors and the
+        old step; it is rebuilt from the loaded state at the next sparse step"""
+        self.flush()
+        for group in self.param_groups:
+            for p in group["params"]:
+                tg = getattr(p, "_asme_table_grad", None)
+                if tg is not None:
+                    tg.lazy = None
+        super().load_state_dict(state_dict)
+        for st in self.state.values():  # torch may restore `step` as a tensor; the kernels take an int
+            if "step" in st and torch.is_tensor(st["step"]):
+                st["step"] = int(st["step"].item())
+
     def _state(self, p):
         st = self.state[p]
         if not st:

@@ -28,7 +28,8 @@ import torch.distributed as dist
 
 from . import ops
 from .modules import (ITEM_SEQ_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME,
-                      SequenceNextItemPredictionTrainingModule, get_additional_meta_data, get_padding_mask)
+                      TARGET_ENTRY_NAME, SequenceNextItemPredictionTrainingModule, build_eval_step_return_dict,
+                      get_additional_meta_data, get_padding_mask)
 from .sequence import InputSequence
 
 
@@ -166,27 +167,37 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
             self._req_map = torch.full((self.vocab,), -1, dtype=torch.int32, device=dev)
             self._own_map = torch.full((max(1, self.exchange.local_rows),), -1, dtype=torch.int32, device=dev)
 
-    def training_step(self, batch, batch_idx):
-        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
-        pos, neg = batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]
+    def _fetch(self, id_sets, train: bool):
+        """dedup the ids of `id_sets`, route them to their owners, gather the (caught-up) rows and return
+        (exchange state, owner plan or None, compact rows in send order, each id set remapped to them)"""
         shard = self.model.item_table()
         self._maps(shard.device)
         # 1. requester: dedup every id of the step
-        req = ops.SparseTablePlan.for_ids(self.vocab, [input_seq, pos, neg], self._req_map)
+        req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
         U = req.n_unique()
         unique = req.unique[:U]
         # 2. route ids to owners; owners catch their rows up (lazy Adam) and gather them
         st = self.exchange.request(unique)
-        own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
-        own.grad_scale = 1.0 / self.exchange.world  # DDP gradient averaging, applied in the ordered row sums
+        own = None
+        if train:
+            own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
+            own.grad_scale = 1.0 / self.exchange.world  # DDP gradient averaging, applied in the ordered row sums
         with torch.no_grad():
             rows = ops.gather_rows(st.recv_local, shard.detach()) if len(st.recv_local) \
                 else shard.new_empty(0, shard.shape[1])
         # the compact table stays in send order; the ids are remapped to it (no row permutation)
-        compact = self.exchange.reply_rows(st, rows).requires_grad_(True)
-        inv_seq, inv_pos, inv_neg = (st.pos.index_select(0, req.inverse_of(x).reshape(-1)).view(x.shape)
-                                     for x in (input_seq, pos, neg))
+        compact = self.exchange.reply_rows(st, rows)
+        inv = [st.pos.index_select(0, req.inverse_of(x).reshape(-1)).view(x.shape) for x in id_sets]
         req.release()
+        return st, own, compact, inv
+
+    def training_step(self, batch, batch_idx):
+        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME))
+        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
+        pos, neg = batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]
+        st, own, compact, (inv_seq, inv_pos, inv_neg) = self._fetch([input_seq, pos, neg], train=True)
+        compact.requires_grad_(True)
+        U = compact.shape[0]
         # its gradient: the heads' contributions summed per compact row in a fixed order (no atomics, no zero fill)
         cplan = ops.SparseTablePlan.identity(U, [inv_seq, inv_pos, inv_neg], compact.shape[1])
         compact._asme_table_grad = ops.TableGrad()
@@ -230,6 +241,46 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
                 n = p.numel()
                 p.grad.copy_(flat[off:off + n].view_as(p.grad))
                 off += n
+
+
+    # ---------------------------------------------------------------- evaluation on the sharded table
+    @torch.no_grad()
+    def catalog_ranks(self, batch) -> torch.Tensor:
+        """1-based full-catalogue rank of every sequence's target over the GLOBAL item table: the input rows
+        come from their owners, each rank scores every rank's queries against its own shard
+        (sharded.catalog_ranks).  Collective: every rank must call it with the same batch size."""
+        self._flush_table()  # the shard's deferred Adam rows, before anyone reads them
+        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME, TARGET_ENTRY_NAME))
+        input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
+        _, _, compact, (inv_seq,) = self._fetch([input_seq], train=False)
+        emb = self.model._sequence_embedding_layer.item_embedding_layer
+        meta = get_additional_meta_data(self.model, batch)
+        padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
+        emb._table_override = compact
+        try:
+            q = self.model.catalog_query(InputSequence(inv_seq, padding_mask, meta))
+        finally:
+            emb._table_override = None
+        if q is None or q[2] is not None:
+            raise NotImplementedError("sharded evaluation needs the tied dot-product projection")
+        return catalog_ranks(self.exchange, q[0], targets, self.model.item_table().detach())
+
+    def validation_step(self, batch, batch_idx):
+        """NDCG / recall / MRR of the sharded model, identical to the unsharded model's (ranks over all |V|)"""
+        if self.metrics is None or not hasattr(self.metrics, "update_ranks"):
+            raise NotImplementedError("sharded validation needs a rank-based metrics container")
+        targets = batch[TARGET_ENTRY_NAME]
+        if targets.dim() != 1:
+            raise NotImplementedError("sharded validation takes one target per sequence")
+        self.metrics.update_ranks(self.catalog_ranks(batch))
+        return build_eval_step_return_dict(batch[ITEM_SEQ_ENTRY_NAME], None, targets)
+
+    def test_step(self, batch, batch_idx):
+        return self.validation_step(batch, batch_idx)
+
+    def predict_step(self, batch, batch_idx, dataloader_idx=None):
+        raise NotImplementedError("predict_step would score every item of the global table on one rank; use "
+                                  "catalog_ranks / sharded.catalog_topk")
 
 
 def train_step(module, optimizer, batch, batch_idx: int = 0):

@@ -115,9 +115,11 @@ def test_model_eval_outputs_match_reference(asme, dev, name):
             assert rel_err(pred.cpu().numpy(), z["eval_logits"]) < TOL
 
 
-def test_ml1m_anchor_ndcg(asme, dev):
+@pytest.mark.parametrize("fused_eval", [True, False])
+def test_ml1m_anchor_ndcg(asme, dev, fused_eval):
     """NDCG@10 of the reference-trained SASRec on the ml-1m-shaped synthetic eval set (6,040 users,
-    3,419-id vocabulary) within +-1e-4 of the reference's value (north_star)."""
+    3,419-id vocabulary) within +-1e-4 of the reference's value (north_star).  fused_eval: the targets are
+    ranked by asme_catalog_rank (the default) or from materialised (B, |V|) scores + asme_target_rank."""
     z = load("ml1m_anchor")
     n_users, L, d, h, N, V = (int(x) for x in z["cfg"])
     model = asme.SASRecModel(transformer_hidden_size=d, num_transformer_heads=h, num_transformer_layers=N,
@@ -130,7 +132,8 @@ def test_ml1m_anchor_ndcg(asme, dev):
     tok = asme.tokenization.Tokenizer(V - 3)
     ndcg = asme.metrics.NormalizedDiscountedCumulativeGainMetric(k=10)
     container = asme.metrics.RankingMetricsContainer([ndcg])
-    module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=container)
+    module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=container,
+                                                           fused_eval=fused_eval)
     module.eval()
     seqs = torch.from_numpy(z["eval_seq"].astype(np.int64))
     targets = torch.from_numpy(z["targets"])

@@ -1,0 +1,106 @@
+"""FusedAdam state handling with the lazily-updated item table (ops.LazyTableState):
+resume at a large step, optimizer state_dict round trips, and dataloader ids of other dtypes."""
+import copy
+
+import pytest
+import torch
+
+from helpers import build_model, load, state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _sasrec(asme, dev, table_grad):
+    z = load("sasrec_neg")
+    model = build_model(asme, "sasrec_neg", z)
+    model.load_state_dict(state_dict(z))
+    model.to(dev)
+    tok = asme.tokenization.Tokenizer(int(z["cfg"][5]) - 3)
+    module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
+                                                           table_grad=table_grad)
+    batch = {k: torch.from_numpy(z[s]).to(dev) for k, s in
+             (("item", "seq"), ("positive_samples", "pos"), ("negative_samples", "neg"))}
+    return model, module, batch
+
+
+def _params(model):
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}  # state_dict() flushes the table
+
+
+def test_default_table_grad_is_sparse_for_gather_only_tables(asme, dev):
+    _, module, _ = _sasrec(asme, dev, None)
+    assert module.table_grad == "sparse"
+
+
+def test_lazy_table_resumed_at_large_step(asme, dev):
+    """a run resumed at step 5000 (beyond the first history capacity) takes the same sparse/lazy step as the
+    eager row update (the history buffer must grow to step + 1 at once)"""
+    results = []
+    for lazy in (True, False):
+        model, module, batch = _sasrec(asme, dev, "sparse")
+        opt = asme.FusedAdam(module.parameters(), lr=1e-3, betas=(0.99, 0.998), weight_decay=1e-3, lazy_table=lazy)
+        for p in module.parameters():  # pretend 5000 steps were taken: moments and step counts of a checkpoint
+            st = opt._state(p)
+            st["step"] = 5000
+            st["exp_avg"].fill_(1e-4)
+            st["exp_avg_sq"].fill_(1e-6)
+        for i in range(2):
+            asme.modules.train_step(module, opt, None, batch, i)
+        opt.flush()
+        table = model.item_table()
+        assert opt.state[table]["step"] == 5002
+        results.append(_params(model))
+    for k in results[0]:
+        assert torch.equal(results[0][k], results[1][k]), k
+
+
+def test_optimizer_state_dict_round_trip(asme, dev):
+    """save -> load -> step reproduces the uninterrupted run bit for bit (the lazy table state is rebuilt
+    from the loaded moments; state_dict() flushes the deferred rows first)"""
+    model, module, batch = _sasrec(asme, dev, "sparse")
+    opt = module.configure_optimizers()
+    for i in range(3):
+        asme.modules.train_step(module, opt, None, batch, i)
+    saved_opt = copy.deepcopy(opt.state_dict())
+    saved_model = _params(model)
+    for i in range(2):
+        asme.modules.train_step(module, opt, None, batch, 3 + i)
+    straight = _params(model)
+    # rewind the same model and optimizer
+    model.load_state_dict(saved_model)
+    opt.load_state_dict(saved_opt)
+    assert all(getattr(p, "_asme_table_grad", None) is None or p._asme_table_grad.lazy is None
+               for p in module.parameters())
+    for i in range(2):
+        asme.modules.train_step(module, opt, None, batch, 3 + i)
+    resumed = _params(model)
+    for k in straight:
+        assert torch.equal(straight[k], resumed[k]), k
+
+
+def test_state_dict_moments_are_current(asme, dev):
+    """optimizer.state_dict() without a model.state_dict() first must not return stale table moments"""
+    res = {}
+    for mode in ("sparse", "dense"):
+        model, module, batch = _sasrec(asme, dev, mode)
+        opt = module.configure_optimizers()
+        for i in range(3):
+            asme.modules.train_step(module, opt, None, batch, i)
+        sd = opt.state_dict()
+        idx = [i for i, p in enumerate(module.parameters()) if p is model.item_table()][0]
+        res[mode] = sd["state"][idx]["exp_avg"].clone()
+    assert (res["sparse"] - res["dense"]).abs().max().item() <= 1e-5 * res["dense"].abs().max().item()
+
+
+def test_int32_batch_ids_with_sparse_table(asme, dev):
+    """int32 dataloader ids: the plan registers the normalised tensors the model reads"""
+    out = []
+    for dtype in (torch.int64, torch.int32):
+        model, module, batch = _sasrec(asme, dev, "sparse")
+        batch = {k: v.to(dtype) for k, v in batch.items()}
+        opt = module.configure_optimizers()
+        for i in range(2):
+            asme.modules.train_step(module, opt, None, batch, i)
+        out.append(_params(model))
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k

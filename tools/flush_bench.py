@@ -25,14 +25,14 @@ def main():
     v = torch.zeros(V, D, device=dev)
     hist = torch.zeros(1024, 8, device=dev)
     for t in range(1, a.k + 1):
-        call("asme_lazy_adam_record_step", ptr(hist), t, 1e-3, 0.9, 0.999, 1e-8, a.wd, st())
+        call("asme_lazy_adam_record_step", ptr(hist), hist.shape[0], t, 1e-3, 0.9, 0.999, 1e-8, a.wd, st())
     last = torch.zeros(V, dtype=torch.int32, device=dev)
     times = []
     for rep in range(4):
         last.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        call("asme_lazy_adam_catch_up", None, None, V, ptr(last), ptr(p), ptr(m), ptr(v), D, ptr(hist), a.k, st())
+        call("asme_lazy_adam_catch_up", None, None, V, ptr(last), ptr(p), ptr(m), ptr(v), D, ptr(hist), hist.shape[0], a.k, st())
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
