@@ -57,6 +57,14 @@ class TableGrad:
     def __init__(self):
         self.plan: Optional["SparseTablePlan"] = None
         self.lazy: Optional["LazyTableState"] = None
+        # the plan of the last optimizer step, kept like a .grad that was not zeroed: another step without a
+        # new backward applies the same rows again (torch.optim semantics); dropped by zero_grad / next plan
+        self.applied: Optional["SparseTablePlan"] = None
+
+    def drop_applied(self):
+        if self.applied is not None:
+            self.applied.release()
+            self.applied = None
 
 
 class LazyTableState:
@@ -107,6 +115,9 @@ class SparseTablePlan:
     def __init__(self, table: Optional[torch.Tensor], id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor,
                  vocab: Optional[int] = None, dim: int = 0):
         dev = slot_map.device
+        tg = getattr(table, "_asme_table_grad", None) if table is not None else None
+        if tg is not None:
+            tg.drop_applied()  # the previous step's plan still marks the shared slot map
         flat = torch.cat([_i64(x).reshape(-1) for x in id_sets])
         n = flat.numel()
         self.vocab, self.dim = table.shape if table is not None else (vocab, dim)
@@ -134,7 +145,6 @@ class SparseTablePlan:
             self._offset[key] = off
             off += k
         self.consumed = False
-        tg = getattr(table, "_asme_table_grad", None) if table is not None else None
         if tg is not None and tg.lazy is not None:
             # rows gathered by this step's forward must carry every earlier (zero-gradient) update
             tg.lazy.catch_up(self.unique, self.count, self.capacity)

@@ -32,6 +32,14 @@ class FusedAdam(torch.optim.Optimizer):
                 if tg is not None and tg.lazy is not None:
                     tg.lazy.flush()
 
+    def zero_grad(self, set_to_none: bool = True):
+        super().zero_grad(set_to_none=set_to_none)
+        for group in self.param_groups:
+            for p in group["params"]:
+                tg = getattr(p, "_asme_table_grad", None)
+                if tg is not None:
+                    tg.drop_applied()
+
     def state_dict(self):
         """flush first: lazily-deferred table rows must be current in the saved moments"""
         self.flush()
@@ -72,6 +80,9 @@ class FusedAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 tg = getattr(p, "_asme_table_grad", None)
                 plan = tg.plan if tg is not None else None
+                reapply = plan is None and tg is not None and tg.applied is not None and p.grad is None
+                if reapply:  # a step without a new backward: the last gradient again, like a kept .grad
+                    plan = tg.applied
                 if plan is not None:
                     if p.grad is not None:
                         raise RuntimeError("item table got a dense gradient while its sparse plan is active "
@@ -84,12 +95,14 @@ class FusedAdam(torch.optim.Optimizer):
                             tg.lazy = LazyTableState(p, st["exp_avg"], st["exp_avg_sq"])
                             tg.lazy.step = st["step"] - 1
                             tg.lazy.last_step.fill_(st["step"] - 1)  # every row is current up to now
+                        elif reapply:  # no forward caught these rows up this time
+                            tg.lazy.catch_up(plan.unique, plan.count, plan.capacity)
                         tg.lazy.record(st["step"], lr, b1, b2, eps, wd)
                         tg.lazy.apply(plan, st["step"])
                     else:
                         call("asme_adam_rows_step", ptr(p), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), V, D,
                              ptr(plan.slot_map), ptr(plan.grad_rows), lr, b1, b2, eps, wd, st["step"], stream())
-                    plan.release()
+                    tg.applied = plan
                     tg.plan = None
                     continue
                 if p.grad is None:

@@ -253,6 +253,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME, TARGET_ENTRY_NAME))
         input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
         _, _, compact, (inv_seq,) = self._fetch([input_seq], train=False)
+        compact._asme_table_grad = ops.TableGrad()  # no plan: the gather kernels read it like any table
         emb = self.model._sequence_embedding_layer.item_embedding_layer
         meta = get_additional_meta_data(self.model, batch)
         padding_mask = get_padding_mask(input_seq, self.item_tokenizer)

@@ -63,12 +63,11 @@ def _hook_outputs(model):
 
 
 # ----------------------------------------------------------------------------------
-def gen_sasrec_neg():
+def gen_sasrec_neg(B=4, L=12, d=32, h=2, N=2, NI=57, lengths=(12, 9, 5, 1), suffix=""):
     """sasrec-neg: SequenceNextItemPredictionTrainingModule + SASRecModel(mode=neg_sampling)
     core/modules/sequence_next_item_prediction_training_module.py:73-115,156-185
     core/models/sasrec/sasrec_model.py:29-108, core/models/sasrec/components.py:21-61
     core/losses/sasrec/sas_rec_losses.py:35-75"""
-    B, L, d, h, N, NI = 4, 12, 32, 2, 2, 57
     tok = S.make_tokenizer(NI)
     S.set_context({"item": tok})
     from asme.core.models.sasrec.sasrec_model import SASRecModel
@@ -81,7 +80,7 @@ def gen_sasrec_neg():
     module = SequenceNextItemPredictionTrainingModule(model=model, metrics=None)
     sd = _sd(model)
     g = torch.Generator().manual_seed(1)
-    lengths = [12, 9, 5, 1]
+    lengths = list(lengths)
     full = _ragged_batch(g, B, L + 1, V, [n + 1 for n in lengths])
     seq = full[:, :L].clone()
     pos = full[:, 1:].clone()
@@ -115,8 +114,8 @@ def gen_sasrec_neg():
                     eval_logits=pred.numpy(),
                     cfg=np.array([B, L, d, h, N, V]), lr=np.float32(1e-3), betas=np.array([0.99, 0.998], np.float32),
                     weight_decay=np.float32(1e-3)))
-    np.savez_compressed(os.path.join(HERE, "sasrec_neg.npz"), **out)
-    print("sasrec_neg", float(loss))
+    np.savez_compressed(os.path.join(HERE, f"sasrec_neg{suffix}.npz"), **out)
+    print("sasrec_neg" + suffix, float(loss))
 
 
 def gen_sasrec_cross():
@@ -178,11 +177,10 @@ def _cloze_batch(g, B, L, V, lengths):
     return seq, tgt
 
 
-def gen_bert4rec(kind: str):
+def gen_bert4rec(kind: str, B=4, L=10, d=32, h=2, N=2, NI=47, lengths=(10, 8, 4, 2), suffix="", adam2=True):
     """bert4rec: MaskedTrainingModule + BERT4RecModel(project_layer_type=kind)
     core/modules/masked_training_module.py:20-189, core/models/bert4rec/bert4rec_model.py:24-68
     core/models/common/layers/layers.py:112-157, ffn_modifier.py:8-26"""
-    B, L, d, h, N, NI = 4, 10, 32, 2, 2, 47
     tok = S.make_tokenizer(NI)
     S.set_context({"item": tok})
     from asme.core.models.bert4rec.bert4rec_model import BERT4RecModel
@@ -194,7 +192,7 @@ def gen_bert4rec(kind: str):
     module = MaskedTrainingModule(model=model, metrics=None, num_warmup_steps=10)
     sd = _sd(model)
     g = torch.Generator().manual_seed(5)
-    lengths = [10, 8, 4, 2]
+    lengths = list(lengths)
     seq, tgt = _cloze_batch(g, B, L, V, lengths)
     hooks = _hook_outputs(model)
     res = module.training_step({"item": seq, "item.target": tgt}, 0)
@@ -209,7 +207,7 @@ def gen_bert4rec(kind: str):
     after1 = _params(model, "adam1")
     opt.step()
     sched.step()
-    after2 = _params(model, "adam2")
+    after2 = _params(model, "adam2") if adam2 else {}
     model.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in sd.items()})
     # eval: one MASK at the last valid position (last_item_mask processor semantics)
     ev = seq.clone()
@@ -223,18 +221,19 @@ def gen_bert4rec(kind: str):
     out.update(grads)
     out.update(after1)
     out.update(after2)
-    out.update(dict(seq=seq.numpy(), target=tgt.numpy(), logits=logits.numpy(), loss=loss.detach().numpy(),
+    out.update(dict(seq=seq.numpy(), target=tgt.numpy(), logits=logits[:, :16 if suffix else L].numpy(), loss=loss.detach().numpy(),
                     emb_out=hooks["emb_out"].numpy(), enc_out=hooks["enc_out"].numpy(),
                     eval_seq=ev.numpy(), eval_logits=pred.numpy(), num_warmup_steps=np.int64(10),
+                    logits_head=np.int64(16 if suffix else L),
                     cfg=np.array([B, L, d, h, N, V]), lr=np.float32(1e-3), betas=np.array([0.99, 0.998], np.float32)))
-    np.savez_compressed(os.path.join(HERE, f"bert4rec_{kind}.npz"), **out)
-    print("bert4rec", kind, float(loss))
+    np.savez_compressed(os.path.join(HERE, f"bert4rec_{kind}{suffix}.npz"), **out)
+    print("bert4rec", kind + suffix, float(loss))
 
 
-def gen_kebert4rec(variant: str):
+def gen_kebert4rec(variant: str, B=4, L=10, d=32, h=2, N=2, NI=41, NG=7, NT=9, K=3, lengths=(10, 6, 5, 3),
+                   suffix=""):
     """kebert4rec: MaskedTrainingModule + KeBERT4RecModel with attribute side-embeddings
     core/models/kebert4rec/kebert4rec_model.py:24-89, components.py:15-115, layers.py:7-27"""
-    B, L, d, h, N, NI, NG, NT, K = 4, 10, 32, 2, 2, 41, 7, 9, 3
     tok = S.make_tokenizer(NI)
     gtok = S.make_tokenizer(NG, "Genre")
     ttok = S.make_tokenizer(NT, "Tag")
@@ -255,7 +254,7 @@ def gen_kebert4rec(variant: str):
     module = MaskedTrainingModule(model=model, metrics=None, num_warmup_steps=0)
     sd = _sd(model)
     g = torch.Generator().manual_seed(7)
-    lengths = [10, 6, 5, 3]
+    lengths = list(lengths)
     seq, tgt = _cloze_batch(g, B, L, V, lengths)
     genre = torch.randint(3, len(gtok), (B, L), generator=g)
     tags = torch.randint(3, len(ttok), (B, L, K), generator=g)
@@ -278,12 +277,13 @@ def gen_kebert4rec(variant: str):
     out.update(grads)
     out.update(after)
     out.update(dict(seq=seq.numpy(), target=tgt.numpy(), genre=genre.numpy(), tags=tags.numpy(),
-                    logits=logits.numpy(), loss=loss.detach().numpy(), emb_out=hooks["emb_out"].numpy(),
+                    logits=logits[:, :16 if suffix else L].numpy(), loss=loss.detach().numpy(), emb_out=hooks["emb_out"].numpy(),
                     enc_out=hooks["enc_out"].numpy(),
+                    logits_head=np.int64(16 if suffix else L),
                     cfg=np.array([B, L, d, h, N, V, len(gtok), len(ttok)]), lr=np.float32(1e-3),
                     betas=np.array([0.99, 0.998], np.float32)))
-    np.savez_compressed(os.path.join(HERE, f"kebert4rec_{variant}.npz"), **out)
-    print("kebert4rec", variant, float(loss))
+    np.savez_compressed(os.path.join(HERE, f"kebert4rec_{variant}{suffix}.npz"), **out)
+    print("kebert4rec", variant + suffix, float(loss))
 
 
 def gen_narm():
@@ -447,6 +447,14 @@ if __name__ == "__main__":
         gen_kebert4rec("pre")
         gen_kebert4rec("post")
         gen_narm()
+    if "d128" in which:
+        # the benchmarked composition: d = 128, h = 2, d_ff = 4d = 512, L = 200 -- every
+        # Linear on the weight-stationary GEMM, the fused FFN, the production weight-gradient shapes
+        big = dict(B=4, L=200, d=128, h=2, N=2, NI=1000, suffix="_d128")
+        gen_sasrec_neg(lengths=(200, 173, 61, 7), **big)
+        gen_bert4rec("linear", lengths=(200, 150, 37, 5), adam2=False, **big)
+        gen_bert4rec("transpose_embedding", lengths=(200, 150, 37, 5), adam2=False, **big)
+        gen_kebert4rec("post", lengths=(200, 120, 77, 9), NG=7, NT=9, K=3, **big)
     if "metrics" in which:
         gen_metrics()
     if "ml1m" in which:

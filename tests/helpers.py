@@ -30,8 +30,14 @@ class Tok:
         return self.n
 
 
+def base_name(name):
+    """fixture name without its shape suffix (sasrec_neg_d128 -> sasrec_neg)"""
+    return name[:-5] if name.endswith("_d128") else name
+
+
 def build_model(asme, name, z):
     cfg = [int(x) for x in z["cfg"]]
+    name = base_name(name)
     if name == "sasrec_neg" or name == "sasrec_cross":
         B, L, d, h, N, V = cfg
         return asme.SASRecModel(transformer_hidden_size=d, num_transformer_heads=h, num_transformer_layers=N,
@@ -65,6 +71,9 @@ def build_model(asme, name, z):
 
 MODEL_FIXTURES = ["sasrec_neg", "sasrec_cross", "bert4rec_transpose_embedding", "bert4rec_linear",
                   "kebert4rec_pre", "kebert4rec_post", "narm"]
+# the benchmarked composition: d = 128, h = 2, d_ff = 512, L = 200 (make_golden.py d128)
+D128_FIXTURES = ["sasrec_neg_d128", "bert4rec_linear_d128", "bert4rec_transpose_embedding_d128",
+                 "kebert4rec_post_d128"]
 
 
 def rel_err(a, b):

@@ -315,10 +315,14 @@ def test_sparse_table_plan_equals_dense(asme, dev):
     p_sparse._asme_table_grad.plan = plan
     p_dense = torch.nn.Parameter(table.clone())
     p_dense.grad = dense
-    for p in (p_sparse, p_dense):
-        asme.FusedAdam([p], lr=1e-2, betas=(0.99, 0.998), weight_decay=1e-3, lazy_table=False).step()
+    opts = [asme.FusedAdam([p], lr=1e-2, betas=(0.99, 0.998), weight_decay=1e-3, lazy_table=False)
+            for p in (p_sparse, p_dense)]
+    for o in opts:
+        o.step()
     assert _rel(p_sparse, p_dense) < 1e-5
-    assert int((slot_map != -1).sum()) == 0  # map reset after the update
+    assert int((slot_map != -1).sum()) > 0  # the applied plan is kept (a second step re-applies it) ...
+    opts[0].zero_grad()
+    assert int((slot_map != -1).sum()) == 0  # ... until zero_grad, which resets the map
 
 
 @pytest.mark.parametrize("D", [32, 64, 128, 192])

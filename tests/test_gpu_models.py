@@ -10,13 +10,14 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import MODEL_FIXTURES, build_model, close, load, prefixed, rel_err, state_dict
+from helpers import D128_FIXTURES, MODEL_FIXTURES, base_name, build_model, close, load, prefixed, rel_err, state_dict
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-3
 
 
 def _batch(name, z, dev):
+    name = base_name(name)
     t = lambda k: torch.from_numpy(z[k]).to(dev)  # noqa: E731
     if name == "sasrec_neg":
         return {"item": t("seq"), "positive_samples": t("pos"), "negative_samples": t("neg")}
@@ -27,6 +28,7 @@ def _batch(name, z, dev):
 
 
 def _module(asme, name, model, V):
+    name = base_name(name)
     tok = asme.tokenization.Tokenizer(V - 3)
     if name == "sasrec_neg":
         return asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None)
@@ -40,12 +42,34 @@ def _module(asme, name, model, V):
 
 
 @pytest.mark.parametrize("fused_xent", [True, False])
-@pytest.mark.parametrize("name", MODEL_FIXTURES)
+@pytest.mark.parametrize("name", MODEL_FIXTURES + D128_FIXTURES)
 def test_model_train_step_matches_reference(asme, dev, name, fused_xent, monkeypatch):
-    """fused_xent: the full-catalogue CE heads on asme_linear_xent_* (True) or materialised logits + CE kernel"""
-    if not fused_xent and name in ("sasrec_neg", "narm"):
+    """fused_xent: the full-catalogue CE heads on asme_linear_xent_* (True) or materialised logits + CE kernel.
+    The d = 128 fixtures run every transformer Linear on the weight-stationary bf16x6 GEMM (the fused FFN
+    included) and every weight gradient on asme_linear_weight_grad: checked by counting the launches and by
+    making any library Linear in the step an error."""
+    if not fused_xent and base_name(name) in ("sasrec_neg", "narm"):
         pytest.skip("no linear full-catalogue CE head")
     monkeypatch.setattr(asme.modules, "FUSED_XENT", fused_xent)
+    calls = {"ws": 0, "wgrad": 0, "ffn": 0}
+    if name.endswith("_d128"):
+        ws, wg, ffn_fwd = asme.ops._ws, asme.ops._weight_grad, asme.ops._FFNFn.forward
+
+        def count(key, fn):
+            def wrapped(*a, **k):
+                calls[key] += 1
+                return fn(*a, **k)
+            return wrapped
+
+        def no_library_linear(*a, **k):
+            raise AssertionError("library GEMM (F.linear) in the d=128 training step")
+
+        monkeypatch.setattr(asme.ops, "_ws", count("ws", ws))
+        monkeypatch.setattr(asme.ops, "_weight_grad", count("wgrad", wg))
+        monkeypatch.setattr(asme.ops._FFNFn, "forward", staticmethod(count("ffn", ffn_fwd)))
+        library_linear = torch.nn.functional.linear
+        if fused_xent:
+            monkeypatch.setattr(torch.nn.functional, "linear", no_library_linear)
     z = load(name)
     model = build_model(asme, name, z)
     model.load_state_dict(state_dict(z), strict=True)
@@ -57,16 +81,26 @@ def test_model_train_step_matches_reference(asme, dev, name, fused_xent, monkeyp
     loss = module.training_step(batch, 0)["loss"]
     assert rel_err(loss.item(), z["loss"]) < 1e-4, (loss.item(), float(z["loss"]))
     loss.backward()
+    if name.endswith("_d128"):
+        n_blocks = int(z["cfg"][4])
+        assert calls["ffn"] == n_blocks, calls        # fused GELU/dropout FFN per block
+        assert calls["ws"] >= 8 * n_blocks, calls     # QKV + O + FFN(2) forward + input-gradient GEMMs
+        assert calls["wgrad"] >= 4 * n_blocks, calls  # QKV, O, W1, W2 weight gradients
+        monkeypatch.setattr(torch.nn.functional, "linear", library_linear)
     grads = prefixed(z, "grad")
     named = dict(model.named_parameters())
     assert set(grads) == set(named), set(grads) ^ set(named)
+    dense_table = _sparse_table_grad(model)
     for k, g in grads.items():
         got = named[k].grad
+        if got is None and dense_table is not None and named[k] is model.item_table():
+            got = dense_table
         got = np.zeros_like(g) if got is None else got.detach().cpu().numpy()
         assert close(got, g, TOL), (k, rel_err(got, g))
 
     opt, sched = asme.modules.split_optimizers(module.configure_optimizers())
     opt.step()
+    opt.flush()  # a row-sparse table defers the zero-gradient rows' update (exact lazy Adam)
     if sched is not None:
         sched.step()
     for k, v in prefixed(z, "adam1").items():
@@ -75,10 +109,25 @@ def test_model_train_step_matches_reference(asme, dev, name, fused_xent, monkeyp
         assert close(named[k].detach().cpu().numpy(), v, TOL), (k, "adam step 1")
     if "adam2/" + next(iter(grads)) in z.files:
         opt.step()
+        opt.flush()
         for k, v in prefixed(z, "adam2").items():
             if _analytically_zero_grad(k):
                 continue
             assert close(named[k].detach().cpu().numpy(), v, TOL), (k, "adam step 2")
+
+
+def _sparse_table_grad(model):
+    """the item table's gradient as a dense (V, d) tensor when it is row-sparse (table_grad='sparse', the default
+    for gather-only tables): the step plan's ordered per-row sums scattered to their rows"""
+    table = model.item_table()
+    tg = getattr(table, "_asme_table_grad", None) if table is not None else None
+    if tg is None or tg.plan is None:
+        return None
+    plan = tg.plan
+    U = plan.n_unique()
+    dense = torch.zeros_like(table)
+    dense[plan.unique[:U]] = plan.grad_rows[:U] * plan.grad_scale
+    return dense
 
 
 def _analytically_zero_grad(name):
@@ -89,7 +138,7 @@ def _analytically_zero_grad(name):
     return name.endswith("attention.linear_layers.1.bias")
 
 
-@pytest.mark.parametrize("name", MODEL_FIXTURES)
+@pytest.mark.parametrize("name", MODEL_FIXTURES + D128_FIXTURES)
 def test_model_eval_outputs_match_reference(asme, dev, name):
     z = load(name)
     model = build_model(asme, name, z)
@@ -100,17 +149,19 @@ def test_model_eval_outputs_match_reference(asme, dev, name):
     module.eval()
     batch = _batch(name, z, dev)
     with torch.no_grad():
-        if name == "sasrec_neg":
+        if base_name(name) == "sasrec_neg":
             pred = module.predict_step({"item": batch["item"]}, 0)
             assert rel_err(pred.cpu().numpy(), z["eval_logits"]) < TOL
             return
         logits = module(batch, 0)
+        head = int(z["logits_head"]) if "logits_head" in z.files else logits.shape[1]
+        logits = logits[:, :head]  # the d = 128 fixtures keep the first 16 positions' logits
         assert logits.shape == z["logits"].shape
         assert rel_err(logits.cpu().numpy(), z["logits"]) < TOL
-        if name == "sasrec_cross":
+        if base_name(name) == "sasrec_cross":
             pred = module.predict_step({"item": batch["item"]}, 0)
             assert rel_err(pred.cpu().numpy(), z["eval_logits"]) < TOL
-        if name.startswith("bert4rec"):
+        if base_name(name).startswith("bert4rec"):
             pred = module.predict_step({"item": torch.from_numpy(z["eval_seq"]).to(dev)}, 0)
             assert rel_err(pred.cpu().numpy(), z["eval_logits"]) < TOL
 

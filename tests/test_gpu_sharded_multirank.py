@@ -106,7 +106,8 @@ def _worker(rank, world, port, cfg, q):
         module.validation_step(part, 0)
         want_part = want_ranks[rank * per:(rank + 1) * per]
         errs["eval/rank_mismatches"] = int((got_ranks != want_part).sum())
-        want_ndcg = float(asme.metrics.ndcg_from_ranks(want_part, 10).mean())
+        # compute() sums (value, count) over the ranks (torchmetrics dist_reduce_fx="sum"): the global NDCG
+        want_ndcg = float(asme.metrics.ndcg_from_ranks(want_ranks, 10).mean())
         errs["eval/ndcg"] = abs(float(ndcg.compute()) - want_ndcg)
         try:
             module.predict_step(part, 0)
