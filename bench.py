@@ -70,8 +70,11 @@ def parse():
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-sharded path even at N=1 (1-rank RCCL group): its overhead without the fabric")
-    ap.add_argument("--cpu-batch", type=int, default=256, help="sequences per CPU-baseline step")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=0, help="sequences per CPU-baseline step (0: --batch)")
+    ap.add_argument("--cpu-warmup", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-batch-1t", type=int, default=16, help="sequences of the single-thread CPU step")
+    ap.add_argument("--sampler-sessions", type=int, default=16, help="sessions for the CPU sampler rate")
     return ap.parse_args()
 
 
@@ -94,38 +97,75 @@ def synthetic_batch(B, L, V, seed, dev, kind="uniform"):
     return {"item": full[:, :L].contiguous(), "positive_samples": full[:, 1:].contiguous(), "negative_samples": neg}
 
 
+def cpu_share() -> int:
+    """host threads this job may use: the scheduler affinity, capped by OMP_NUM_THREADS when the pool sets it
+    (on the GPU box os.cpu_count() reports the whole machine, many times this job's share)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_model_name() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "cpu"
+
+
 def cpu_baseline(args, V):
-    """CPU oracle (oracle/asme_oracle.py) on the host cores: the same step (fwd+bwd+dense Adam over the
-    full 10M-row table) on a bounded batch sample."""
+    """CPU restatement (oracle/asme_oracle.py, reference op order) timed on the host cores, SURVEY §8(d): the same
+    step (fwd + bwd + dense torch Adam over the full 10M-row table) on the same B = 1024 batch shape, all of this
+    job's threads, --cpu-warmup warm-up + --cpu-steps timed steps; then the single-thread rate (same model and
+    optimizer state, a --cpu-batch-1t batch) and the reference CPU input pipeline's rate (the pos/neg sampler's
+    0/1-weight multinomial over |V| per session, pos_neg_sampler.py:41-106)."""
     from oracle import asme_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_share()
     torch.set_num_threads(threads)
     d, L, N, h = args.dim, args.seq_len, args.layers, args.heads
     sd = O.init_sasrec_state(V, L, d, N, seed=0)
     params = [p.requires_grad_(True) for p in sd.values()]
     opt = torch.optim.Adam(params, lr=1e-3, betas=(0.99, 0.998), weight_decay=1e-3, foreach=False)
-    B = args.cpu_batch
-    batch = synthetic_batch(B, L, V, 1234, torch.device("cpu"))
-    times = []
-    for i in range(1 + args.cpu_steps):
-        t0 = time.perf_counter()
-        O.sasrec_neg_train_step(sd, opt, batch["item"], batch["positive_samples"], batch["negative_samples"], h,
-                                dropout=args.dropout)
-        times.append(time.perf_counter() - t0)
-    per_step = sum(times[1:]) / len(times[1:])
-    cpu_name = platform.processor() or "cpu"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_name = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
+    B = args.cpu_batch or args.batch
+
+    def run(batch_size, n_warm, n_timed, tag):
+        batch = synthetic_batch(batch_size, L, V, 1234, torch.device("cpu"))
+        times = []
+        for i in range(n_warm + n_timed):
+            t0 = time.perf_counter()
+            O.sasrec_neg_train_step(sd, opt, batch["item"], batch["positive_samples"], batch["negative_samples"], h,
+                                    dropout=args.dropout)
+            times.append(time.perf_counter() - t0)
+            print(f"[cpu_baseline] {tag} step {i + 1}/{n_warm + n_timed}: {times[-1]:.2f} s", file=sys.stderr,
+                  flush=True)
+        return sum(times[n_warm:]) / n_timed
+
+    per_step = run(B, args.cpu_warmup, args.cpu_steps, f"B={B} x{threads} threads")
+    torch.set_num_threads(1)
+    B1 = args.cpu_batch_1t
+    per_step_1t = run(B1, 0, 1, f"B={B1} x1 thread")
+    torch.set_num_threads(threads)
+    # the reference's CPU negative sampler at this |V| (one DataLoader worker = one core)
+    g = torch.Generator().manual_seed(1235)
+    sessions = torch.randint(3, V, (args.sampler_sessions, L + 1), generator=g).tolist()
+    torch.set_num_threads(1)
+    t0 = time.perf_counter()
+    for sess in sessions:
+        O.pos_neg(sess, V, (0, 1, 2))
+    sampler = len(sessions) / (time.perf_counter() - t0)
+    torch.set_num_threads(threads)
     return {"value": round(B / per_step, 3), "unit": "sequences/s", "cores": threads, "kind": "port",
-            "sample": f"SASRec-neg fwd+bwd+dense Adam, B={B} L={L} d={d} |V|={V} (full table), "
-                      f"{args.cpu_steps} timed steps after 1 warm-up, {per_step:.2f} s/step, torch CPU fp32, "
-                      f"{cpu_name}"}
+            "batch": B, "s_per_step": round(per_step, 3),
+            "single_thread": {"value": round(B1 / per_step_1t, 3), "batch": B1, "s_per_step": round(per_step_1t, 3)},
+            "input_pipeline": {"value": round(sampler, 2), "unit": "sessions/s per core",
+                               "what": f"reference pos/neg sampler (torch.multinomial over |V|={V}), L={L}"},
+            "machine_cpus": os.cpu_count(),
+            "sample": f"SASRec-neg fwd+bwd+dense Adam, B={B} L={L} d={d} |V|={V} (full table), {args.cpu_steps} "
+                      f"timed steps after {args.cpu_warmup} warm-up, {per_step:.2f} s/step on {threads} threads "
+                      f"(this job's CPU share; the machine has {os.cpu_count()}), torch CPU fp32, {cpu_model_name()}"}
 
 
 def bench_bert4rec(args, asme, dev, world, rank):

@@ -534,6 +534,42 @@ def test_catalog_rank_and_topk(asme, dev, d, nq, V, with_bias):
     assert torch.allclose(vals, logits.gather(1, idx), rtol=1e-5, atol=1e-4)
 
 
+def _tie_free_scores(nq, V, d, with_bias, dev, seed):
+    """integer-valued queries / items whose scores are exact in fp32 (and in every split-bf16 product) and
+    pairwise distinct: a distinct multiple of 2^-12 per item comes from the bias or from item column 0
+    (query column 0 = 1); |score| < 2^11, so integer + fraction fit fp32's 24 bits"""
+    g = torch.Generator().manual_seed(seed)
+    H = torch.randint(-3, 4, (nq, d), generator=g).float()
+    E = torch.randint(-3, 4, (V, d), generator=g).float()
+    frac = torch.randperm(V, generator=g).float() * 2.0 ** -12
+    bias = None
+    if with_bias:
+        bias = torch.randint(-8, 8, (V,), generator=g).float() + frac
+    else:
+        H[:, 0] = 1.0
+        E[:, 0] += frac
+    s = H.double() @ E.double().t() + (bias.double() if bias is not None else 0)
+    return H.to(dev), E.to(dev), (bias.to(dev) if bias is not None else None), s
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("nq,V", [(5, 37), (130, 1000), (300, 4099)])
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_catalog_rank_and_topk_exact(asme, dev, d, nq, V, with_bias):
+    """Exact ranks and top-k on tie-free data with exactly representable scores: the fused kernels equal the
+    float64 reference rank rule (1 + #items scored above the target) and topk bit for bit."""
+    H, E, bias, s = _tie_free_scores(nq, V, d, with_bias, dev, d * 7 + nq + V)
+    targets = torch.randint(0, V, (nq,), generator=torch.Generator().manual_seed(V)).to(dev)
+    t = s.gather(1, targets.cpu()[:, None])
+    ref_rank = 1 + (s > t).sum(1)
+    assert torch.equal(asme.ops.catalog_rank(H, E, targets, bias).cpu(), ref_rank)
+    k = min(10, V)
+    vals, idx = asme.ops.catalog_topk(H, E, k, bias)
+    ref_v, ref_i = torch.topk(s, k, dim=1)
+    assert torch.equal(idx.cpu(), ref_i)
+    assert torch.equal(vals.cpu().double(), ref_v)
+
+
 @pytest.mark.parametrize("world", [1, 3, 8])
 @pytest.mark.parametrize("n", [1, 1023, 1025, 300001])
 def test_bucket_by_owner_matches_stable_argsort(asme, dev, world, n):
