@@ -158,7 +158,8 @@ int asme_cross_entropy_bwd(const float* logits, int64_t ld, const float* lse, co
                            const float* stats, float* dlogits, int64_t ld_dlogits, void* stream);
 /* Full-catalogue logits head fused with CrossEntropyLoss(ignore_index), logits never materialised
  * (layers.py:105-109,138-143 + masked_training_module.py:93-111 / losses.py:77-115; SURVEY A14+A17).
- * s = H W^T + bias (H: n x dim, W: V x dim, dim in {32, 64, 128}, rows 16-B aligned); lse (n);
+ * s = H W^T + bias (H: n x dim, W: V x dim, dim a multiple of 4 in [4, 128], rows 16-B aligned); lse (n);
+ * products at fp32 level on the bf16 matrix cores (bf16x6 split operands, csrc/logits.hip);
  * out[0] = mean over rows with a valid target of lse - s[t] (NaN if none), out[1] = that count.
  * The backward overwrites dH (n x dim), dW (V x dim) and db (V, nullable) with the gradients of
  * dloss[0] * out[0].  Workspaces are caller-owned, sized by the *_workspace functions (bytes). */
@@ -171,6 +172,12 @@ int asme_linear_xent_bwd(const float* H, int64_t ld_h, int64_t n, int64_t dim, c
                          const float* bias, const int64_t* targets, int64_t ignore_index, const float* lse,
                          const float* stats, const float* dloss, float* dH, float* dW, float* db, float* workspace,
                          int64_t ws_bytes, void* stream);
+/* Materialised full-catalogue scores (evaluation / predict_step: layers.py:105-109,138-143,
+ * sasrec/components.py:46-61): out (n x V, row stride ld_out) = H (n x dim) W^T (V x dim) + bias (nullable),
+ * same products as the fused head.  Workspace (bytes) from asme_logits_workspace. */
+int64_t asme_logits_workspace(int64_t n, int64_t V, int64_t dim);
+int asme_logits(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w, int64_t V,
+                const float* bias, float* out, int64_t ld_out, float* workspace, int64_t ws_bytes, void* stream);
 /* ranking (core/metrics/common.py:4-27 get_true_positives): 1-based rank of targets[r] in row r of
  * scores, descending, ties broken by lower item id */
 int asme_target_rank(const float* scores, int64_t ld, const int64_t* targets, int64_t n_rows, int64_t n_items,

@@ -1,0 +1,751 @@
+// Full-catalogue logits head on gfx950's bf16 matrix cores with fp32-level products (bf16x6, common.h):
+// fused logits + CrossEntropyLoss(ignore_index) for training (the (n x |V|) logits never reach HBM) and the
+// materialised (n x |V|) scores for evaluation / predict.
+//
+// Reference semantics (paths relative to /root/reference/src/asme):
+//   LinearProjectionLayer / ItemEmbeddingProjectionLayer (tied h E^T + b)   core/models/common/layers/layers.py:105-109,138-143
+//   MaskedTrainingModule._calc_loss, CrossEntropyLoss(ignore_index=pad)      core/modules/masked_training_module.py:93-111
+//   SingleTargetCrossEntropyLoss / SASRecFullSequenceCrossEntropyLoss       core/losses/losses.py:77-115
+//   SASRecProjectionComponent inference (last position . E^T)               core/models/sasrec/components.py:46-61
+//
+//   s[q][i] = H[q] . W[i] + b[i],  lse[q] = log sum_i exp s[q][i],  loss = mean_{valid q} (lse[q] - s[q][t_q])
+//   dS = (softmax(s) - onehot(t)) * dloss / count;  dH = dS W;  dW = dS^T H;  db = colsum(dS)
+//
+// Operands.  H (n x d) and W (|V| x d) are split once per call into three bf16 planes each (x = h + m + l exactly,
+// rows zero-padded to 128 features and to a multiple of 128 rows): the hot loops then run only MFMAs and LDS
+// reads -- no VALU split of a reused operand.  Every pass is one kernel template over a (stationary, streamed)
+// pair of those planes:
+//   stationary rows: 16 per wave, their three planes held as MFMA B fragments in registers for the whole kernel
+//   streamed rows:   64-row tiles of the three planes through a double-buffered LDS image (one barrier per tile)
+//                    in the T10 swizzle (plain 256-B rows, chunk ^ ((r&3)<<2 | (r>>2)&3)): ds_read_b128 row
+//                    reads for the score product, ds_read_b64_tr_b16 transposed reads for the gradient product
+//   X = A_streamed . B_stationary^T (v_mfma_f32_16x16x32_bf16 x 6): lane (stationary row c, group g) holds
+//   streamed rows 4g..4g+3 of each 16-row sub-tile, so a pair of sub-tiles gives the 8 values the lane supplies
+//   as the B fragment of the NEXT product, which sums over the streamed rows with no lane movement:
+//   Y^T[f][c] += (streamed^T)[f][rows] . P[rows][c]   (the streamed operand read back transposed)
+// Passes (n queries, V items; the streamed operand is split into 8k chunks, chunk = workgroup % nchunks, so the
+// workgroups of one XCD share one chunk in their L2):
+//   stats   stationary = queries, streamed = items: online (max, sum exp) per query per chunk + target logit
+//   dH      stationary = queries, streamed = items: P = exp(s + b - lse) - onehot; dH^T += W^T P^T
+//   dW, db  stationary = items, streamed = queries: P^T the same way;            dW^T += H^T P
+//   logits  stationary = queries, streamed = items: out = s + b
+// Work: 2 (stats) + 4 (dH) + 4 (dW) n|V|d FLOP executed for the 6 of a materialised head; HBM bytes O((n+V)d).
+// Partial slabs of the chunks are summed in a fixed order: deterministic.
+#include "common.h"
+#include <algorithm>
+
+#ifndef ASME_LOGITS_PIPE
+#define ASME_LOGITS_PIPE 0
+#endif
+
+using namespace asme;
+
+namespace {
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4;
+
+constexpr int kDP = 128;                 // padded feature width of a plane row (256 B)
+constexpr int kRowB = kDP * 2;           // bytes per plane row
+constexpr int kTS = 64;                  // streamed rows per LDS tile
+// workgroup = W waves x 32 stationary rows: W = 8 (two waves per SIMD, 256 registers each: the partner wave's
+// MFMAs fill this wave's softmax VALU) where the pass fits that budget (stats, logits); W = 4 (one wave per SIMD,
+// 512 registers) for the gradient passes, whose stationary fragments + 128-feature accumulators need more
+constexpr int kRowPad = 256;             // plane rows are padded to a multiple of this (>= 32 W, kTS)
+template <int MODE> struct EngineWaves { static constexpr int W = (MODE == 1 || MODE == 2) ? 4 : 8; };
+constexpr int kPlaneTile = kTS * kRowB;  // 16 KiB: one plane of one tile
+constexpr int kTile = 3 * kPlaneTile;    // 48 KiB
+
+enum { M_STATS = 0, M_DH = 1, M_DW = 2, M_LOGITS = 3 };
+
+__host__ __device__ constexpr int64_t pad_rows(int64_t r) { return (r + kRowPad - 1) / kRowPad * kRowPad; }
+
+// byte offset of 16-B chunk ch of row r in a plane image of 256-B rows (cdna_hip_programming.md T10, image (b)):
+// conflict-free ds_read_b64_tr_b16 reads, 2-way ds_read_b128 row reads of the 16x16x32 operand
+__device__ __forceinline__ int swz(int r, int ch) { return r * kRowB + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+__device__ __forceinline__ bf16x8 lds_b128(const char* base, int off) {
+    return *reinterpret_cast<const bf16x8*>(base + off);
+}
+__device__ __forceinline__ short4v lds_tr(const char* base, int off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(base + off));
+}
+__device__ __forceinline__ bf16x8 cat8(short4v lo, short4v hi) {
+    typedef short short8v __attribute__((ext_vector_type(8)));
+    const short8v v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// ------------------------------------------------------------------------------------------------ split
+// planes[p][r][0..127] (bf16) = plane p of X[r][0..d) (zero beyond d and for r >= rows), r < rows_pad
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ X, int64_t ld, int64_t rows,
+                                                           int d, int64_t rows_pad, __bf16* __restrict__ planes) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per 8 features
+    if (t >= rows_pad * (kDP / 8)) return;
+    const int64_t r = t / (kDP / 8);
+    const int c = (int)(t % (kDP / 8)) * 8;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (r < rows) {
+        const float* x = X + r * ld;
+        if (c + 8 <= d) {
+            a = *reinterpret_cast<const float4*>(x + c);
+            b = *reinterpret_cast<const float4*>(x + c + 4);
+        } else if (c < d) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = c + j < d ? x[c + j] : 0.f;
+            a = make_float4(v[0], v[1], v[2], v[3]);
+            b = make_float4(v[4], v[5], v[6], v[7]);
+        }
+    }
+    const Bf3 s = split_bf3(a, b);
+    const int64_t o = r * kDP + c, P = rows_pad * kDP;
+    *reinterpret_cast<bf16x8*>(planes + o) = s.h;
+    *reinterpret_cast<bf16x8*>(planes + P + o) = s.m;
+    *reinterpret_cast<bf16x8*>(planes + 2 * P + o) = s.l;
+}
+
+// ------------------------------------------------------------------------------------------------ engine
+struct LogitsArgs {
+    const __bf16* stat;     // stationary planes (3 x stat_pad x 128)
+    const __bf16* strm;     // streamed planes (3 x strm_pad x 128)
+    int64_t stat_pad, strm_pad;
+    int64_t n_stat, n_strm;  // real rows
+    int64_t chunk;           // streamed rows per chunk (multiple of kTS)
+    int nchunks;
+    int d;
+    const float* bias;       // [V] or null
+    const int64_t* targets;  // [n]
+    int64_t ignore;
+    int64_t V;               // = the item count (n_strm in stats / dH / logits, n_stat in dW)
+    const float* lse;        // [n] (dH, dW)
+    const float* dloss;      // dH, dW: scale = dloss[0] / stats[1]
+    const float* stats;
+    float* part;             // stats: (nchunks, n, 2); dH: (nchunks, n, d) or dH; dW: (nchunks, V, d) or dW
+    float* part2;            // stats: target logits [n]; dW: db partials (nchunks, V) or db (nullable)
+    float* out;              // logits: (n, ld_out)
+    int64_t ld_out;
+};
+
+__device__ __forceinline__ bool valid_target(int64_t t, int64_t ignore, int64_t V) {
+    return t != ignore && t >= 0 && t < V;
+}
+
+// One streamed tile (3 planes x kTS rows x 256 B) straight from HBM/L2 into an LDS buffer by LDS-DMA
+// (global_load_lds_dwordx4: 1 KiB = 4 image rows per wave-instruction, lane L -> bytes 16L..16L+15): each lane
+// fetches the source chunk that the swizzle puts at its destination slot, so the image is written in place
+// without registers or ds_write.  Completion: the issuing wave's vmcnt, then the workgroup barrier.
+template <int W>
+__device__ __forceinline__ void dma_tile(const __bf16* __restrict__ planes, int64_t pad, int64_t row0, char* buf) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < kTile / 1024 / W; ++i) {
+        const int w = wave + W * i;                     // wave-instruction: plane w / 16, image rows 4 (w % 16) ..
+        const int p = w / (kTS / 4), R = 4 * (w % (kTS / 4));
+        const int row = R + (lane >> 4);
+        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));  // swz(): slot lane & 15 holds chunk ch
+        const __bf16* src = planes + (int64_t)p * pad * kDP + (row0 + row) * kDP + ch * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(buf + p * kPlaneTile + R * kRowB),
+                                         16, 0, 0);
+    }
+}
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// per-streamed-row metadata staged next to the tile: M_STATS / M_DH / M_LOGITS: item bias (-inf beyond V);
+// M_DW: query lse (+inf for ignored / padding queries) and target (-1 for them)
+struct TileMeta {
+    float f;
+    int t;
+    __device__ __forceinline__ void load(int mode, const LogitsArgs& a, int64_t row) {
+        if (mode == M_DW) {
+            const int64_t tg = row < a.n_strm ? a.targets[row] : -1;
+            const bool ok = row < a.n_strm && valid_target(tg, a.ignore, a.V);
+            f = ok ? a.lse[row] : INFINITY;
+            t = ok ? (int)tg : -1;
+        } else {
+            f = row < a.n_strm ? (a.bias ? a.bias[row] : 0.f) : -INFINITY;
+            t = 0;
+        }
+    }
+};
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// acc += a . b over one 16-k step of v_mfma_f32_32x32x16_bf16, the six bf16x6 terms smallest first
+__device__ __forceinline__ floatx16 mfma32_bf3(const Bf3& a, const Bf3& b, floatx16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
+}
+
+// 32x32x16 fragment maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) supplies A[row r][k 8h..8h+7]
+// and B[k 8h..8h+7][col r]; accumulator register i holds C[row (i & 3) + 8 (i >> 2) + 4h][col r].
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+template <int MODE, int KB, int W>
+__global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* bufs = smem;                                                  // 2 x kTile
+    float* mf = reinterpret_cast<float*>(smem + 2 * kTile);            // 2 x kTS
+    int* mt = reinterpret_cast<int*>(smem + 2 * kTile + 2 * kTS * 4);  // 2 x kTS
+    constexpr int KS = 2 * KB;  // 16-k steps of the score product
+    constexpr int NFT = KB;     // 32-feature tiles of the gradient product
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r32 = lane & 31;
+    const int chunk_id = (int)(blockIdx.x % (unsigned)a.nchunks);
+    const int64_t sblock = blockIdx.x / (unsigned)a.nchunks;
+    const int64_t srow = sblock * (32 * W) + wave * 32 + r32;  // this lane's stationary row (MFMA column)
+    const int64_t s_begin = (int64_t)chunk_id * a.chunk;
+    const int64_t s_end = std::min(a.strm_pad, s_begin + a.chunk);  // tiles past n_strm read zero planes
+
+    // stationary fragments (B operand): row srow, k = 16 ks + 8 h .. +7, three planes
+    Bf3 st[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int64_t o = srow * kDP + 16 * ks + 8 * h;
+        st[ks].h = *reinterpret_cast<const bf16x8*>(a.stat + o);
+        st[ks].m = *reinterpret_cast<const bf16x8*>(a.stat + a.stat_pad * kDP + o);
+        st[ks].l = *reinterpret_cast<const bf16x8*>(a.stat + 2 * a.stat_pad * kDP + o);
+    }
+    // stationary-row metadata
+    float s_lse = 0.f, s_bias = 0.f;
+    int s_tgt = -1;
+    if (MODE == M_DH || MODE == M_STATS) {
+        const int64_t tg = srow < a.n_stat ? a.targets[srow] : -1;
+        const bool ok = srow < a.n_stat && valid_target(tg, a.ignore, a.V);
+        s_tgt = ok ? (int)tg : -1;
+        if (MODE == M_DH) s_lse = ok ? a.lse[srow] : INFINITY;  // ignored / padding queries: P = 0
+    } else if (MODE == M_DW) {
+        s_bias = srow < a.n_stat ? (a.bias ? a.bias[srow] : 0.f) : -INFINITY;
+        s_tgt = (int)srow;  // compare the streamed query's target against this item
+    }
+    float run_max = -INFINITY, run_sum = 0.f, t_logit = 0.f;
+    bool have_t = false;
+    floatx16 y[NFT];  // gradient product: Y^T[feature 32 ft + acc_row(i, h)][stationary row r32]
+#pragma unroll
+    for (int f = 0; f < NFT; ++f)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) y[f][i] = 0.f;
+    float db = 0.f;
+
+    TileMeta tm;
+    if (s_begin < s_end) {
+        dma_tile<W>(a.strm, a.strm_pad, s_begin, bufs);
+        if (threadIdx.x < kTS) {
+            tm.load(MODE, a, s_begin + threadIdx.x);
+            mf[threadIdx.x] = tm.f;
+            mt[threadIdx.x] = tm.t;
+        }
+        wait_dma();
+    }
+    __syncthreads();
+    int it = 0;
+    for (int64_t r0 = s_begin; r0 < s_end; r0 += kTS, ++it) {
+        const int cur = it & 1;
+        const bool more = r0 + kTS < s_end;
+        if (more) {  // the next tile flies into the other buffer during this tile's MFMAs
+            dma_tile<W>(a.strm, a.strm_pad, r0 + kTS, bufs + (cur ^ 1) * kTile);
+            if (threadIdx.x < kTS) tm.load(MODE, a, r0 + kTS + threadIdx.x);
+        }
+        const char* buf = bufs + cur * kTile;
+        const float* tf = mf + cur * kTS;
+        const int* tt = mt + cur * kTS;
+        // X = streamed rows 32 sub .. +31 (MFMA rows) x stationary rows (columns): row reads of the tile
+        auto score = [&](int sub) {
+            floatx16 x;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int off = swz(32 * sub + r32, 2 * ks + h);
+                Bf3 A;
+                A.h = lds_b128(buf, off);
+                A.m = lds_b128(buf + kPlaneTile, off);
+                A.l = lds_b128(buf + 2 * kPlaneTile, off);
+                x = mfma32_bf3(A, st[ks], x);
+            }
+            return x;
+        };
+        // P (unscaled) as the split B fragments of the two 16-row k steps:
+        //   dH: streamed = items (bias tf, id r0 + lr), stationary = query (s_lse, s_tgt)
+        //   dW: streamed = queries (lse tf, target tt), stationary = item (s_bias, id srow)
+        auto probs = [&](floatx16 x, int sub, Bf3 (&P)[2]) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int lr = 32 * sub + acc_row(i, h);
+                if (MODE == M_DH) {
+                    x[i] = __expf(x[i] + tf[lr] - s_lse) - ((int64_t)s_tgt == r0 + lr ? 1.f : 0.f);
+                } else {
+                    x[i] = __expf(x[i] + s_bias - tf[lr]) - (tt[lr] == s_tgt ? 1.f : 0.f);
+                    db += x[i];
+                }
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                P[s2] = split_bf3(make_float4(x[8 * s2], x[8 * s2 + 1], x[8 * s2 + 2], x[8 * s2 + 3]),
+                                  make_float4(x[8 * s2 + 4], x[8 * s2 + 5], x[8 * s2 + 6], x[8 * s2 + 7]));
+        };
+        // Y^T[f][r32] += streamed^T[f][rows] . P[rows][r32], k step s2 = rows 16 s2 .. +15 of the sub-tile: the
+        // B fragment is P registers 8 s2 .. 8 s2 + 7 (element j = row 16 s2 + 8 (j >> 2) + 4 h + (j & 3)); the A
+        // fragment comes from two transposed reads: 16-lane group (h, fh) reads rows 16 s2 + 4 h + q (+8) x
+        // features 32 ft + 16 fh + 4 p4 .. +3 (lane 4q + p4 addresses one row), lane receives its feature
+        auto grad = [&](int sub, const Bf3 (&P)[2]) {
+            const int fh = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int rlo = 32 * sub + 16 * s2 + 4 * h + q, rhi = rlo + 8;
+#pragma unroll
+                for (int ft = 0; ft < NFT; ++ft) {
+                    const int ch = 4 * ft + 2 * fh + (p4 >> 1);
+                    const int olo = swz(rlo, ch) + 8 * (p4 & 1), ohi = swz(rhi, ch) + 8 * (p4 & 1);
+                    Bf3 A;
+                    A.h = cat8(lds_tr(buf, olo), lds_tr(buf, ohi));
+                    A.m = cat8(lds_tr(buf + kPlaneTile, olo), lds_tr(buf + kPlaneTile, ohi));
+                    A.l = cat8(lds_tr(buf + 2 * kPlaneTile, olo), lds_tr(buf + 2 * kPlaneTile, ohi));
+                    y[ft] = mfma32_bf3(A, P[s2], y[ft]);
+                }
+            }
+        };
+        if constexpr (MODE == M_DH || MODE == M_DW) {
+#if ASME_LOGITS_PIPE
+            // one wave per SIMD: software-pipeline the tile's two sub-tiles so the softmax VALU of one runs in the
+            // MFMA shadow of the other's products: [S0] [P0 | S1] [G0 | P1] [G1], interleaved by the scheduler
+            // directives (per MFMA: at most one LDS read and five vector instructions, MI355X guide T19)
+            const floatx16 x0 = score(0);
+            __builtin_amdgcn_sched_barrier(0);
+            Bf3 P0[2], P1[2];
+            probs(x0, 0, P0);
+            const floatx16 x1 = score(1);
+#pragma unroll
+            for (int i = 0; i < 6 * KS / 2; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            grad(0, P0);
+            probs(x1, 1, P1);
+#pragma unroll
+            for (int i = 0; i < 12 * NFT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            grad(1, P1);
+#else
+#pragma unroll
+            for (int sub = 0; sub < kTS / 32; ++sub) {
+                Bf3 P[2];
+                probs(score(sub), sub, P);
+                grad(sub, P);
+            }
+#endif
+        } else {
+#pragma unroll
+            for (int sub = 0; sub < kTS / 32; ++sub) {
+                floatx16 x = score(sub);
+                if (MODE == M_LOGITS) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int lr = 32 * sub + acc_row(i, h);
+                        const int64_t item = r0 + lr;
+                        if (item < a.n_strm && srow < a.n_stat) a.out[srow * a.ld_out + item] = x[i] + tf[lr];
+                    }
+                    continue;
+                }
+                // M_STATS: online (max, sum exp) over the lane's streamed rows + the target logit
+                float tmax = -INFINITY;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    x[i] += tf[32 * sub + acc_row(i, h)];
+                    tmax = fmaxf(tmax, x[i]);
+                }
+                const int rel = s_tgt - (int)(r0 + 32 * sub);  // target in this sub-tile and lane half?
+                if ((unsigned)rel < 32u && ((rel >> 2) & 1) == h) {
+                    const int ri = (rel & 3) + 4 * (rel >> 3);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (i == ri) t_logit = x[i];
+                    have_t = true;
+                }
+                const float nm = fmaxf(run_max, tmax);
+                if (nm != -INFINITY) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) sum += __expf(x[i] - nm);
+                    run_sum = run_sum * __expf(run_max - nm) + sum;
+                    run_max = nm;
+                }
+            }
+        }
+        if (more) {
+            if (threadIdx.x < kTS) {
+                mf[(cur ^ 1) * kTS + threadIdx.x] = tm.f;
+                mt[(cur ^ 1) * kTS + threadIdx.x] = tm.t;
+            }
+            wait_dma();
+        }
+        __syncthreads();
+    }
+
+    if (MODE == M_LOGITS) return;
+    if (MODE == M_STATS) {
+        // merge the two lane halves of each query (each holds its own streamed rows)
+        const float m2 = __shfl_xor(run_max, 32, 64), s2 = __shfl_xor(run_sum, 32, 64);
+        const float nm = fmaxf(run_max, m2);
+        if (nm != -INFINITY) {
+            run_sum = run_sum * __expf(run_max - nm) + s2 * __expf(m2 - nm);
+            run_max = nm;
+        }
+        if (srow < a.n_stat) {
+            if (h == 0) {
+                a.part[((int64_t)chunk_id * a.n_stat + srow) * 2] = run_max;
+                a.part[((int64_t)chunk_id * a.n_stat + srow) * 2 + 1] = run_sum;
+            }
+            if (have_t) a.part2[srow] = t_logit;
+        }
+        return;
+    }
+    const float scale = a.dloss[0] / a.stats[1];
+    // lane (r32, h) holds Y^T[32 ft + 8 u + 4 h + (0..3)][r32] = gradient[srow][that feature], u = reg >> 2
+    if (srow < a.n_stat) {
+        float* dst = a.part + ((a.nchunks > 1 ? (int64_t)chunk_id * a.n_stat : 0) + srow) * a.d;
+#pragma unroll
+        for (int ft = 0; ft < NFT; ++ft)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int f = 32 * ft + 8 * u + 4 * h;
+                if (f < a.d)
+                    *reinterpret_cast<float4*>(dst + f) =
+                        make_float4(y[ft][4 * u] * scale, y[ft][4 * u + 1] * scale, y[ft][4 * u + 2] * scale,
+                                    y[ft][4 * u + 3] * scale);
+            }
+    }
+    if (MODE == M_DW && a.part2) {
+        db += __shfl_xor(db, 32, 64);
+        if (h == 0 && srow < a.n_stat) a.part2[(a.nchunks > 1 ? (int64_t)chunk_id * a.n_stat : 0) + srow] = db * scale;
+    }
+}
+
+// one block: lse[q] = merge of the chunks; out[0] = mean over valid rows of lse - s_t (NaN if none), out[1] = count
+__global__ __launch_bounds__(1024) void lce_finish_kernel(const float* __restrict__ part, int64_t n, int nchunks,
+                                                          const int64_t* __restrict__ targets, int64_t ignore,
+                                                          int64_t V, const float* __restrict__ tlogit,
+                                                          float* __restrict__ lse, float* __restrict__ out) {
+    __shared__ float sa[1024], sc[1024];
+    float acc = 0.f, cnt = 0.f;
+    for (int64_t q = threadIdx.x; q < n; q += blockDim.x) {
+        float m = -INFINITY, s = 0.f;
+        for (int k = 0; k < nchunks; ++k) {
+            const float m2 = part[((int64_t)k * n + q) * 2], s2 = part[((int64_t)k * n + q) * 2 + 1];
+            const float nm = fmaxf(m, m2);
+            if (nm == -INFINITY) continue;
+            s = s * __expf(m - nm) + s2 * __expf(m2 - nm);
+            m = nm;
+        }
+        const float l = m + logf(s);
+        lse[q] = l;
+        if (valid_target(targets[q], ignore, V)) {
+            acc += l - tlogit[q];
+            cnt += 1.f;
+        }
+    }
+    sa[threadIdx.x] = acc;
+    sc[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            sa[threadIdx.x] += sa[threadIdx.x + s];
+            sc[threadIdx.x] += sc[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = sa[0] / sc[0];
+        out[1] = sc[0];
+    }
+}
+
+// out[i] = sum_{c < nparts} part[c * stride + i] (fixed order)
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int64_t stride, int nparts,
+                                                        int64_t count, float* __restrict__ out) {
+    const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i4 >= count) return;
+    if (i4 + 4 <= count) {
+        float4 s = *reinterpret_cast<const float4*>(part + i4);
+        for (int c = 1; c < nparts; ++c) {
+            const float4 v = *reinterpret_cast<const float4*>(part + c * stride + i4);
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        *reinterpret_cast<float4*>(out + i4) = s;
+    } else {
+        for (int64_t i = i4; i < count; ++i) {
+            float s = part[i];
+            for (int c = 1; c < nparts; ++c) s += part[c * stride + i];
+            out[i] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ host
+constexpr size_t kSmem = 2 * kTile + 2 * kTS * 8;
+
+// chunks of the streamed operand: a multiple of 8 (one set per XCD) when there is enough work, each a whole
+// number of tiles; the stationary blocks times the chunks give the grid
+struct Plan {
+    int64_t stat_pad, strm_pad, sblocks, chunk;
+    int nchunks;
+};
+template <int MODE>
+Plan make_plan(int64_t n_stat, int64_t n_strm, int cus) {
+    Plan p;
+    p.stat_pad = pad_rows(std::max<int64_t>(n_stat, 1));
+    p.strm_pad = pad_rows(std::max<int64_t>(n_strm, 1));
+    p.sblocks = p.stat_pad / (32 * EngineWaves<MODE>::W);
+    const int64_t tiles = p.strm_pad / kTS;
+    // enough workgroups to cover the CUs ~4 times, chunks of at least 4 tiles
+    int64_t want = std::max<int64_t>(1, (4 * (int64_t)cus + p.sblocks - 1) / p.sblocks);
+    if (want >= 8) want = (want + 7) / 8 * 8;
+    want = std::min<int64_t>(want, std::max<int64_t>(1, tiles / 4));
+    p.chunk = (tiles + want - 1) / want * kTS;
+    p.nchunks = (int)((p.strm_pad + p.chunk - 1) / p.chunk);
+    return p;
+}
+
+int device_cus() {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus;
+}
+
+int64_t planes_bytes(int64_t rows) { return 3 * pad_rows(std::max<int64_t>(rows, 1)) * kDP * 2; }
+
+int split(const float* X, int64_t ld, int64_t rows, int d, __bf16* planes, hipStream_t s) {
+    const int64_t pad = pad_rows(std::max<int64_t>(rows, 1));
+    const int64_t threads = pad * (kDP / 8);
+    hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, X, ld, rows, d,
+                       pad, planes);
+    return hip_status(hipGetLastError(), "logits: split");
+}
+
+template <int MODE, int KB>
+int launch_engine(const LogitsArgs& a, int64_t sblocks, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)logits_engine_kernel<MODE, KB, EngineWaves<MODE>::W>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmem);
+        if (e != hipSuccess) return hip_status(e, "logits: LDS opt-in");
+        attr = true;
+    }
+    constexpr int W = EngineWaves<MODE>::W;
+    hipLaunchKernelGGL((logits_engine_kernel<MODE, KB, W>), dim3((unsigned)(sblocks * a.nchunks)), dim3(W * 64), kSmem,
+                       s, a);
+    return hip_status(hipGetLastError(), "logits: engine");
+}
+
+template <int MODE>
+int launch_kb(const LogitsArgs& a, int64_t sblocks, hipStream_t s) {
+    switch ((a.d + 31) / 32) {
+        case 1: return launch_engine<MODE, 1>(a, sblocks, s);
+        case 2: return launch_engine<MODE, 2>(a, sblocks, s);
+        case 3: return launch_engine<MODE, 3>(a, sblocks, s);
+        default: return launch_engine<MODE, 4>(a, sblocks, s);
+    }
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------- fused CE, forward
+ASME_API int64_t asme_linear_xent_fwd_workspace(int64_t n, int64_t V, int64_t dim) {
+    (void)dim;
+    const Plan p = make_plan<M_STATS>(n, V, device_cus());
+    return align256(planes_bytes(n)) + align256(planes_bytes(V)) + align256(p.nchunks * n * 2 * 4) + align256(n * 4);
+}
+
+// lse[q] (n) and out = {mean loss over the valid rows, their count}; H (n x dim), W (V x dim), dim <= 128
+ASME_API int asme_linear_xent_fwd(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
+                                  int64_t V, const float* bias, const int64_t* targets, int64_t ignore_index,
+                                  float* lse, float* workspace, int64_t ws_bytes, float* out, void* stream) {
+    ASME_CHECK_ARG(H && W && targets && lse && workspace && out, "asme_linear_xent_fwd: null pointer");
+    ASME_CHECK_ARG(dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && ld_w % 4 == 0 && aligned16(H) &&
+                       aligned16(W),
+                   "asme_linear_xent_fwd: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    ASME_CHECK_ARG(n >= 0 && V >= 1 && V < (1LL << 31), "asme_linear_xent_fwd: bad shape");
+    ASME_CHECK_ARG(ws_bytes >= asme_linear_xent_fwd_workspace(n, V, dim), "asme_linear_xent_fwd: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const Plan p = make_plan<M_STATS>(n, V, device_cus());
+    char* w = reinterpret_cast<char*>(workspace);
+    __bf16* hp = reinterpret_cast<__bf16*>(w);
+    __bf16* wp = reinterpret_cast<__bf16*>(w + align256(planes_bytes(n)));
+    float* part = reinterpret_cast<float*>(w + align256(planes_bytes(n)) + align256(planes_bytes(V)));
+    float* tlogit = part + align256(p.nchunks * n * 2 * 4) / 4;
+    if (n > 0) {
+        int rc = split(H, ld_h, n, (int)dim, hp, s);
+        if (rc == 0) rc = split(W, ld_w, V, (int)dim, wp, s);
+        if (rc != 0) return rc;
+        LogitsArgs a{};
+        a.stat = hp;
+        a.strm = wp;
+        a.stat_pad = p.stat_pad;
+        a.strm_pad = p.strm_pad;
+        a.n_stat = n;
+        a.n_strm = V;
+        a.chunk = p.chunk;
+        a.nchunks = p.nchunks;
+        a.d = (int)dim;
+        a.bias = bias;
+        a.targets = targets;
+        a.ignore = ignore_index;
+        a.V = V;
+        a.part = part;
+        a.part2 = tlogit;
+        rc = launch_kb<M_STATS>(a, p.sblocks, s);
+        if (rc != 0) return rc;
+    }
+    hipLaunchKernelGGL(lce_finish_kernel, dim3(1), dim3(1024), 0, s, part, n, p.nchunks, targets, ignore_index, V,
+                       tlogit, lse, out);
+    ASME_LAUNCH_CHECK("asme_linear_xent_fwd");
+}
+
+// --------------------------------------------------------------------------------------- fused CE, backward
+ASME_API int64_t asme_linear_xent_bwd_workspace(int64_t n, int64_t V, int64_t dim) {
+    const int cus = device_cus();
+    const Plan ph = make_plan<M_DH>(n, V, cus), pw = make_plan<M_DW>(V, n, cus);
+    const int64_t dh = ph.nchunks > 1 ? ph.nchunks * n * dim : 0;
+    const int64_t dw = pw.nchunks > 1 ? pw.nchunks * V * (dim + 1) : 0;
+    return align256(planes_bytes(n)) + align256(planes_bytes(V)) + align256(dh * 4) + align256(dw * 4);
+}
+
+// dH (n x dim), dW (V x dim), db (V, nullable) are overwritten (not accumulated)
+ASME_API int asme_linear_xent_bwd(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
+                                  int64_t V, const float* bias, const int64_t* targets, int64_t ignore_index,
+                                  const float* lse, const float* stats, const float* dloss, float* dH, float* dW,
+                                  float* db, float* workspace, int64_t ws_bytes, void* stream) {
+    ASME_CHECK_ARG(H && W && targets && lse && stats && dloss && dH && dW, "asme_linear_xent_bwd: null pointer");
+    ASME_CHECK_ARG(dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && ld_w % 4 == 0 && aligned16(H) &&
+                       aligned16(W) && aligned16(dH) && aligned16(dW),
+                   "asme_linear_xent_bwd: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    ASME_CHECK_ARG(V >= 1 && V < (1LL << 31), "asme_linear_xent_bwd: bad shape");
+    ASME_CHECK_ARG(ws_bytes >= asme_linear_xent_bwd_workspace(n, V, dim), "asme_linear_xent_bwd: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (hipMemsetAsync(dW, 0, V * dim * sizeof(float), s) != hipSuccess ||
+            (db && hipMemsetAsync(db, 0, V * sizeof(float), s) != hipSuccess))
+            return hip_status(hipGetLastError(), "asme_linear_xent_bwd");
+        return 0;
+    }
+    const int cus = device_cus();
+    const Plan ph = make_plan<M_DH>(n, V, cus), pw = make_plan<M_DW>(V, n, cus);
+    char* w = reinterpret_cast<char*>(workspace);
+    __bf16* hp = reinterpret_cast<__bf16*>(w);
+    __bf16* wp = reinterpret_cast<__bf16*>(w + align256(planes_bytes(n)));
+    float* dh_part = reinterpret_cast<float*>(w + align256(planes_bytes(n)) + align256(planes_bytes(V)));
+    const int64_t dh_elems = ph.nchunks > 1 ? ph.nchunks * n * dim : 0;
+    float* dw_part = dh_part + align256(dh_elems * 4) / 4;
+    float* db_part = dw_part + (pw.nchunks > 1 ? pw.nchunks * V * dim : 0);
+    int rc = split(H, ld_h, n, (int)dim, hp, s);
+    if (rc == 0) rc = split(W, ld_w, V, (int)dim, wp, s);
+    if (rc != 0) return rc;
+    LogitsArgs a{};
+    a.d = (int)dim;
+    a.bias = bias;
+    a.targets = targets;
+    a.ignore = ignore_index;
+    a.V = V;
+    a.lse = lse;
+    a.dloss = dloss;
+    a.stats = stats;
+    // dH: queries stationary, items streamed
+    a.stat = hp;
+    a.strm = wp;
+    a.stat_pad = ph.stat_pad;
+    a.strm_pad = ph.strm_pad;
+    a.n_stat = n;
+    a.n_strm = V;
+    a.chunk = ph.chunk;
+    a.nchunks = ph.nchunks;
+    a.part = ph.nchunks > 1 ? dh_part : dH;
+    a.part2 = nullptr;
+    rc = launch_kb<M_DH>(a, ph.sblocks, s);
+    if (rc != 0) return rc;
+    // dW, db: items stationary, queries streamed
+    a.stat = wp;
+    a.strm = hp;
+    a.stat_pad = pw.stat_pad;
+    a.strm_pad = pw.strm_pad;
+    a.n_stat = V;
+    a.n_strm = n;
+    a.chunk = pw.chunk;
+    a.nchunks = pw.nchunks;
+    a.part = pw.nchunks > 1 ? dw_part : dW;
+    a.part2 = pw.nchunks > 1 ? (db ? db_part : nullptr) : db;
+    rc = launch_kb<M_DW>(a, pw.sblocks, s);
+    if (rc != 0) return rc;
+    auto sum = [&](const float* part, int64_t stride, int64_t nparts, int64_t count, float* out) {
+        const int64_t thr = (count + 3) / 4;
+        hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, part, stride,
+                           (int)nparts, count, out);
+    };
+    if (ph.nchunks > 1) sum(dh_part, n * dim, ph.nchunks, n * dim, dH);
+    if (pw.nchunks > 1) {
+        sum(dw_part, V * dim, pw.nchunks, V * dim, dW);
+        if (db) sum(db_part, V, pw.nchunks, V, db);
+    }
+    ASME_LAUNCH_CHECK("asme_linear_xent_bwd");
+}
+
+// ------------------------------------------------------------------------------------ materialised scores
+ASME_API int64_t asme_logits_workspace(int64_t n, int64_t V, int64_t dim) {
+    (void)dim;
+    return align256(planes_bytes(n)) + align256(planes_bytes(V));
+}
+
+// out (n x V, row stride ld_out) = H (n x dim) . W^T (V x dim) + bias (nullable), fp32-level products (bf16x6)
+ASME_API int asme_logits(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
+                         int64_t V, const float* bias, float* out, int64_t ld_out, float* workspace, int64_t ws_bytes,
+                         void* stream) {
+    ASME_CHECK_ARG(H && W && out && workspace, "asme_logits: null pointer");
+    ASME_CHECK_ARG(dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && ld_w % 4 == 0 && aligned16(H) &&
+                       aligned16(W) && ld_out >= V,
+                   "asme_logits: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    ASME_CHECK_ARG(n >= 0 && V >= 1 && V < (1LL << 31), "asme_logits: bad shape");
+    ASME_CHECK_ARG(ws_bytes >= asme_logits_workspace(n, V, dim), "asme_logits: workspace too small");
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const Plan p = make_plan<M_LOGITS>(n, V, device_cus());
+    char* w = reinterpret_cast<char*>(workspace);
+    __bf16* hp = reinterpret_cast<__bf16*>(w);
+    __bf16* wp = reinterpret_cast<__bf16*>(w + align256(planes_bytes(n)));
+    int rc = split(H, ld_h, n, (int)dim, hp, s);
+    if (rc == 0) rc = split(W, ld_w, V, (int)dim, wp, s);
+    if (rc != 0) return rc;
+    LogitsArgs a{};
+    a.stat = hp;
+    a.strm = wp;
+    a.stat_pad = p.stat_pad;
+    a.strm_pad = p.strm_pad;
+    a.n_stat = n;
+    a.n_strm = V;
+    a.chunk = p.chunk;
+    a.nchunks = p.nchunks;
+    a.d = (int)dim;
+    a.bias = bias;
+    a.V = V;
+    a.out = out;
+    a.ld_out = ld_out;
+    return launch_kb<M_LOGITS>(a, p.sblocks, s);
+}

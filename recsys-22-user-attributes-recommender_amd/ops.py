@@ -882,18 +882,55 @@ def cross_entropy(logits, targets, ignore_index: int):
     return _CrossEntropyFn.apply(logits, targets, ignore_index)
 
 
-_XENT_DIMS = (32, 64, 128)
-
-
 def linear_xent_ok(hidden: torch.Tensor, weight: torch.Tensor) -> bool:
-    """shapes the fused logits + cross-entropy kernels take (asme_linear_xent_*)"""
-    return (hidden.shape[-1] in _XENT_DIMS and weight.dim() == 2 and weight.shape[1] == hidden.shape[-1]
+    """shapes the logits kernels take (asme_linear_xent_*, asme_logits; csrc/logits.hip): hidden width a multiple of
+    4 up to 128, weight rows contiguous and 16-B aligned"""
+    d = hidden.shape[-1]
+    return (4 <= d <= 128 and d % 4 == 0 and weight.dim() == 2 and weight.shape[1] == d
             and weight.stride(1) == 1 and weight.stride(0) % 4 == 0 and weight.data_ptr() % 16 == 0)
+
+
+class _LogitsFn(torch.autograd.Function):
+    """H W^T + b materialised on asme_logits (evaluation / predict scores).  Its backward (only for callers that
+    differentiate through materialised logits with a loss other than the fused cross-entropy) uses library
+    GEMMs: dH = dS W, dW = dS^T H."""
+
+    @staticmethod
+    def forward(ctx, hidden, weight, bias):
+        h = _f32(hidden).reshape(-1, hidden.shape[-1])
+        n, d = h.shape
+        V = weight.shape[0]
+        out = torch.empty(n, V, device=h.device, dtype=torch.float32)
+        nb = int(_lib.load().asme_logits_workspace(n, V, d))
+        ws = torch.empty(max(4, nb // 4 + 1), device=h.device, dtype=torch.float32)
+        call("asme_logits", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(_f32(bias)) if bias is not None
+             else None, ptr(out), V, ptr(ws), ws.numel() * 4, stream())
+        ctx.save_for_backward(h, weight)
+        ctx.meta = (bias is not None, hidden.shape)
+        return out.view(*hidden.shape[:-1], V)
+
+    @staticmethod
+    def backward(ctx, ds):
+        h, weight = ctx.saved_tensors
+        has_bias, shape = ctx.meta
+        ds2 = ds.reshape(-1, weight.shape[0])
+        dh = (ds2 @ weight).view(shape) if ctx.needs_input_grad[0] else None
+        dw = ds2.t() @ h if ctx.needs_input_grad[1] else None
+        db = ds2.sum(0) if has_bias and ctx.needs_input_grad[2] else None
+        return dh, dw, db
+
+
+def logits(hidden, weight, bias=None):
+    """full-catalogue scores hidden . weight^T (+ bias) on the bf16x6 logits kernel (library GEMM only for widths
+    it does not take)"""
+    if linear_xent_ok(hidden, weight) and hidden.is_cuda:
+        return _LogitsFn.apply(hidden, weight, bias)
+    return torch.nn.functional.linear(hidden, weight, bias)
 
 
 class _LinearXentFn(torch.autograd.Function):
     """CrossEntropyLoss(ignore_index)(H W^T + b, targets), mean over non-ignored rows, without the (n, |V|)
-    logits (csrc/xent.hip; layers.py:105-109,138-143 + losses.py:77-115)."""
+    logits (csrc/logits.hip; layers.py:105-109,138-143 + losses.py:77-115)."""
 
     @staticmethod
     def forward(ctx, hidden, weight, bias, targets, ignore_index: int):

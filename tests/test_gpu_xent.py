@@ -1,4 +1,4 @@
-"""Fused full-catalogue logits head + CrossEntropyLoss (csrc/xent.hip, ops.linear_cross_entropy) against the
+"""Fused full-catalogue logits head + CrossEntropyLoss (csrc/logits.hip, ops.linear_cross_entropy) against the
 plain PyTorch fp64 CPU computation F.cross_entropy(F.linear(h, W, b), t, ignore_index) (layers.py:105-109,
 138-143; losses.py:77-115): loss, dH, dW, db; ignored rows, out-of-range targets, all rows ignored (NaN,
 like torch), ragged n / |V| (not multiples of the 64-row tiles), every supported width."""
@@ -16,7 +16,7 @@ def _rel(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-30))
 
 
-@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("d", [32, 36, 64, 100, 128])
 @pytest.mark.parametrize("n,V", [(1, 5), (37, 67), (300, 1000), (2051, 4099), (513, 27003)])
 @pytest.mark.parametrize("with_bias", [True, False])
 def test_linear_xent_matches_reference(asme, dev, d, n, V, with_bias):
@@ -60,6 +60,32 @@ def test_linear_xent_all_ignored_and_out_of_range(asme, dev):
     loss2 = asme.ops.linear_cross_entropy(h, W, b, t2, 0)
     ref = F.cross_entropy(F.linear(h[keep].double(), W.double(), b.double()), t2[keep])
     assert abs(loss2.item() - ref.item()) / abs(ref.item()) < 1e-5
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("n,V", [(1, 3), (129, 257), (700, 27003)])
+def test_logits_exact_on_integer_data(asme, dev, d, n, V):
+    """asme_logits on integer-valued operands (every product and sum exact in fp32 and in the split bf16 terms):
+    bit-exact against float64, which pins the operand / fragment layouts of the engine"""
+    g = torch.Generator().manual_seed(d + n + V)
+    h = torch.randint(-4, 5, (n, d), generator=g).float()
+    W = torch.randint(-4, 5, (V, d), generator=g).float()
+    b = torch.randint(-9, 10, (V,), generator=g).float()
+    want = h.double() @ W.double().t() + b.double()
+    got = asme.ops.logits(h.to(dev), W.to(dev), b.to(dev))
+    assert torch.equal(got.cpu().double(), want)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_logits_random_vs_fp64(asme, dev, d):
+    """fp32-level accuracy of the split-bf16 products: error vs float64 within fp32 GEMM rounding"""
+    torch.manual_seed(d)
+    n, V = 333, 5001
+    h, W, b = torch.randn(n, d), torch.randn(V, d), torch.randn(V)
+    want = h.double() @ W.double().t() + b.double()
+    got = asme.ops.logits(h.to(dev), W.to(dev), b.to(dev)).cpu().double()
+    scale = h.double().abs() @ W.double().abs().t() + b.double().abs()
+    assert ((got - want).abs() / scale).max().item() < 2e-6
 
 
 def test_linear_xent_vs_materialised_kernels(asme, dev):

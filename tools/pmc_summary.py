@@ -1,24 +1,30 @@
-"""Summarise tools/pmc_generic.sh output: python tools/pmc_summary.py gpurun_out/pmc_TAG"""
+"""Summarise tools/pmc_kernel.sh CSVs: per kernel (name filter), counters averaged over its dispatches, and
+derived fractions (MFMA busy of all SIMD cycles, wave-cycle split)."""
 import collections
 import csv
+import glob
 import sys
 
 d = sys.argv[1]
-agg = collections.defaultdict(lambda: collections.defaultdict(float))
-n = collections.Counter()
-for p in ("p1", "p2"):
-    for r in csv.DictReader(open(f"{d}/{p}/run_counter_collection.csv")):
-        nm = r["Kernel_Name"]
-        k = (nm.split("::")[1] if "::" in nm else nm).split("(")[0][:60] + "|" + r.get("Grid_Size", "")
-        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        if r["Counter_Name"] in ("GRBM_GUI_ACTIVE", "SQ_INSTS_LDS"):
-            n[(k, p)] += 1
-for k, v in agg.items():
-    c1, c2 = max(n[(k, "p1")], 1), max(n[(k, "p2")], 1)
-    wc = v["SQ_WAVE_CYCLES"] or 1
-    gui = v["GRBM_GUI_ACTIVE"] / c1 / 8
-    print(f"{k}: launches {c1}/{c2}  cycles/launch {gui:.3g}  waves/SIMD {4 * v['SQ_WAVE_CYCLES'] / c1 / 1024 / max(gui, 1):.2f}")
-    print(f"   wait_any {v['SQ_WAIT_ANY'] / wc:.2f} wait_inst {v['SQ_WAIT_INST_ANY'] / wc:.2f} active {v['SQ_ACTIVE_INST_ANY'] / wc:.2f}"
-          f"  mfma_util {v['SQ_VALU_MFMA_BUSY_CYCLES'] / c2 / 1024 / max(gui, 1):.2f}  valu/launch {v['SQ_INSTS_VALU'] / c2:.3g}"
-          f"  lds {v['SQ_INSTS_LDS'] / c2:.3g} salu {v['SQ_INSTS_SALU'] / c2:.3g} ldsconf {v['SQ_LDS_BANK_CONFLICT'] / c2:.3g}"
-          f" waitinstlds {v['SQ_WAIT_INST_LDS'] / c2:.3g}")
+pat = sys.argv[2] if len(sys.argv) > 2 else ""
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{d}/*counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        if pat not in k:
+            continue
+        agg[k[:90]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, c in agg.items():
+    v = {n: sum(x) / len(x) for n, x in c.items()}
+    out = {n: f"{x:.4g}" for n, x in sorted(v.items())}
+    if "GRBM_GUI_ACTIVE" in v and "SQ_VALU_MFMA_BUSY_CYCLES" in v:
+        simd_cycles = v["GRBM_GUI_ACTIVE"] / 8 * 1024
+        out["mfma_busy_frac"] = f"{v['SQ_VALU_MFMA_BUSY_CYCLES'] / simd_cycles:.3f}"
+    if "SQ_WAVE_CYCLES" in v:
+        for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                  "SQ_WAIT_INST_LDS"):
+            if n in v:
+                out[n + "_frac"] = f"{v[n] / v['SQ_WAVE_CYCLES']:.3f}"
+    print(k)
+    for n, x in out.items():
+        print(f"   {n} = {x}")
