@@ -28,7 +28,7 @@ PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
 # kernels that compute their fp32 products as six bf16 MFMAs of split operands (csrc/common.h, bf16x6): their
 # ceiling is the dense bf16 MFMA peak (2516.6 TF/s = 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz) over 6
 PEAK_BF16X6_TFS = 2516.6 / 6
-BF16X6_KERNELS = {"asme_ws_linear", "asme_linear_weight_grad"}
+BF16X6_KERNELS = {"asme_ws_linear", "asme_linear_weight_grad", "asme_linear_xent_fwd", "asme_linear_xent_bwd", "asme_logits"}
 
 
 def instrumented_steps(steps):

@@ -256,35 +256,16 @@ int asme_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t 
                      void* stream);
 
 
-/* ---- Fused Linear layers (csrc/linear.hip): fp32 MFMA GEMMs with the block's elementwise passes as
- * epilogues.  w is nn.Linear.weight (out_f x in_f, row-major).  Reference: transformer_layers.py:120-130
- * (SublayerConnection), 175-199 (projections), 212-220 (PositionwiseFeedForward), 251-258 (TransformerBlock). */
+/* ---- General Linear GEMMs (csrc/linear.hip), fp32 MFMA: the widths asme_ws_linear does not tile (e.g. the
+ * reference's d = 32 / 64 configurations; in_f, out_f multiples of 4, rows 16-B aligned).  w is nn.Linear.weight
+ * (out_f x in_f, row-major).  Reference: transformer_layers.py:175-199 (projections), 212-220
+ * (PositionwiseFeedForward), ffn_modifier.py:24-26. */
 /* y = x . w^T + b */
 int asme_linear_fwd(const float* x, int64_t ld_x, int64_t n_rows, int64_t in_f, const float* w, const float* b,
                     int64_t out_f, float* y, int64_t ld_y, void* stream);
 /* dx (+)= dy . w */
 int asme_linear_dx(const float* dy, int64_t ld_dy, int64_t n_rows, int64_t out_f, const float* w, int64_t in_f,
                    float* dx, int64_t ld_dx, int accumulate, void* stream);
-/* pre = x . w^T + b;  y = dropout_p(GELU_erf(pre))   (PositionwiseFeedForward inner layer) */
-int asme_linear_gelu_dropout_fwd(const float* x, int64_t ld_x, int64_t n_rows, int64_t in_f, const float* w,
-                                 const float* b, int64_t out_f, float p, uint64_t seed, float* pre, float* y,
-                                 int64_t ld_y, void* stream);
-/* dx = (dy . w) * keep_p * GELU'(pre) */
-int asme_linear_dx_gelu_bwd(const float* dy, int64_t ld_dy, int64_t n_rows, int64_t out_f, const float* w,
-                            int64_t in_f, const float* pre, float p, uint64_t seed, float* dx, int64_t ld_dx,
-                            void* stream);
-/* out_f == 128: s_out = drop_b(res + drop_a(x . w^T + b)); ln_out = LN(s_out) (ln_w nullable); stats = (mean, rstd) */
-int asme_linear_residual_ln_fwd(const float* x, int64_t ld_x, int64_t n_rows, int64_t in_f, const float* w,
-                                const float* b, int64_t out_f, const float* res, float p_a, uint64_t seed_a, float p_b,
-                                uint64_t seed_b, const float* ln_w, const float* ln_b, float eps, float* s_out,
-                                float* ln_out, float* stats, void* stream);
-/* rows of LN-parameter partials (2 x 128 floats each) written by asme_linear_dx_residual_ln_bwd */
-int64_t asme_linear_partials_rows(int64_t n_rows);
-/* in_f == 128: C = dy . w (= dL/dLN-output); d_s = d_in + LN_bwd(C); d_res = d_s*keep_b; d_y = d_res*keep_a */
-int asme_linear_dx_residual_ln_bwd(const float* dy, int64_t ld_dy, int64_t n_rows, int64_t out_f, const float* w,
-                                   int64_t in_f, const float* s, const float* stats, const float* ln_w,
-                                   const float* d_in, float p_a, uint64_t seed_a, float p_b, uint64_t seed_b,
-                                   float* d_res, float* d_y, float* partials, void* stream);
 
 
 /* ---- Full-catalogue evaluation (csrc/catalog.hip), no (queries x |V|) logits.  Reference:

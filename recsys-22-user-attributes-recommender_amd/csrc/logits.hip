@@ -512,11 +512,25 @@ Plan make_plan(int64_t n_stat, int64_t n_strm, int cus) {
     p.strm_pad = pad_rows(std::max<int64_t>(n_strm, 1));
     p.sblocks = p.stat_pad / (32 * EngineWaves<MODE>::W);
     const int64_t tiles = p.strm_pad / kTS;
-    // enough workgroups to cover the CUs ~4 times, chunks of at least 4 tiles
-    int64_t want = std::max<int64_t>(1, (4 * (int64_t)cus + p.sblocks - 1) / p.sblocks);
-    if (want >= 8) want = (want + 7) / 8 * 8;
-    want = std::min<int64_t>(want, std::max<int64_t>(1, tiles / 4));
-    p.chunk = (tiles + want - 1) / want * kTS;
+    // one workgroup per CU at a time (96 KiB of LDS): pick the chunk count whose grid fills its last round best
+    // (the workgroups of a round take about equally long), preferring multiples of 8 (a chunk per XCD, its tiles
+    // shared in that XCD's L2) at equal fill; chunks of at least 4 tiles
+    const int64_t max_chunks = std::max<int64_t>(1, std::min<int64_t>(tiles / 4, 64));
+    double best = -1.0;
+    p.chunk = tiles * kTS;
+    for (int64_t want = 1; want <= max_chunks; ++want) {
+        const int64_t chunk = (tiles + want - 1) / want;
+        const int64_t nch = (tiles + chunk - 1) / chunk;
+        const int64_t wgs = p.sblocks * nch;
+        if (wgs < cus && want < max_chunks) continue;  // fewer workgroups than CUs: keep splitting
+        const int64_t rounds = (wgs + cus - 1) / cus;
+        // fill of the CU-rounds, minus a small cost per round (per-workgroup prologue / epilogue, partial slabs)
+        const double score = (double)wgs / (double)(rounds * cus) + (nch % 8 == 0 ? 0.02 : 0.0) - 0.002 * rounds;
+        if (score > best) {
+            best = score;
+            p.chunk = chunk * kTS;
+        }
+    }
     p.nchunks = (int)((p.strm_pad + p.chunk - 1) / p.chunk);
     return p;
 }

@@ -5,8 +5,8 @@ fixtures) are interchangeable, e.g.
   _sequence_embedding_layer.item_embedding_layer.item_embedding.embedding.weight
   _sequence_representation_layer.transformer_layer.transformer_blocks.0.attention.linear_layers.0.weight
 The forward passes do not call the sub-modules one by one: they hand the parameters to the fused
-gfx950 kernels in `ops` (embedding+LN+dropout, attention, residual+dropout+LN, GELU+dropout) and
-use PyTorch (hipBLASLt) only for the plain Linear GEMMs.
+gfx950 kernels in `ops` (embedding+LN+dropout, attention, residual+dropout+LN, the weight-stationary
+bf16x6 Linear GEMMs with the FFN's GELU+dropout epilogues, the full-catalogue logits head).
 
 Reference classes (paths relative to /root/reference/src/asme):
   SequenceElementsEmbeddingLayer    core/models/common/layers/sequence_embedding.py:47-93
@@ -28,15 +28,10 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import fused, ops
+from . import ops
 from .sequence import get_attribute
 
 
-# Run the transformer stack as one fused autograd function (fused.py: GEMM epilogues) when its shapes
-# allow.  Off by default: measured at the bench shape the epilogue-fused GEMMs (csrc/linear.hip) are
-# slower than library GEMMs + the standalone HBM-bound row kernels; kept tested and
-# opt-in (tests/test_gpu_fused.py flips it).
-FUSED_STACK = False
 
 
 def _p(module: nn.Module, training: bool) -> float:
@@ -249,9 +244,6 @@ class TransformerLayer(nn.Module):
         if len(blocks) == 0:
             return x
         tr = self.training
-        b0 = blocks[0]
-        if FUSED_STACK and fused.fusable(x.shape[-1], b0.feed_forward.w_1.weight.shape[0], b0.attention.heads, x):
-            return fused.transformer_stack(x, key_valid, blocks, causal, tr)
         x, ln = ops.layer_norm_pass(x, blocks[0].input_sublayer.norm)
         for i, blk in enumerate(blocks):
             att, ff = blk.attention, blk.feed_forward
@@ -353,7 +345,7 @@ class LinearProjectionLayer(nn.Module):
         return self.linear.weight, self.linear.bias
 
     def forward(self, representation: torch.Tensor, sequence=None) -> torch.Tensor:
-        return F.linear(representation, self.linear.weight, self.linear.bias)
+        return ops.logits(representation, self.linear.weight, self.linear.bias)
 
 
 class ItemEmbeddingProjectionLayer(nn.Module):
@@ -371,7 +363,7 @@ class ItemEmbeddingProjectionLayer(nn.Module):
         return self.embedding.weight, self.output_bias
 
     def forward(self, representation: torch.Tensor, sequence=None) -> torch.Tensor:
-        return F.linear(representation, self.embedding.weight, self.output_bias)
+        return ops.logits(representation, self.embedding.weight, self.output_bias)
 
 
 def build_projection_layer(project_type: str, transformer_hidden_size: int, item_voc_size: int,
@@ -403,6 +395,6 @@ class SASRecProjectionComponent(nn.Module):
         last = representation[torch.arange(representation.shape[0], device=representation.device), idx]
         if pos.dim() == 2 and pos.shape[1] == table.shape[0] and bool(
                 (pos[0] == torch.arange(table.shape[0], device=pos.device)).all()) and bool((pos == pos[0]).all()):
-            return last @ table.t()  # all items, in id order (predict_step's items_to_rank)
+            return ops.logits(last, table)  # all items, in id order (predict_step's items_to_rank)
         rows = F.embedding(pos, table)  # (N, I, d)
         return torch.bmm(rows, last.unsqueeze(-1)).squeeze(-1)

@@ -223,25 +223,22 @@ def _instantiate_loss(loss_function, item_tokenizer):
     return loss_function
 
 
-# Full-catalogue CE heads: True = asme_linear_xent_* (logits never stored; 10 n|V|d MFMA FLOP), False = library
-# GEMM logits (n, |V|) + CE kernels (6 n|V|d FLOP, 2 x 4 n|V| bytes of logits and their gradient), None = fused
-# only when those logits would exceed XENT_MATERIALISE_MAX_BYTES (at BERT4Rec C3, 37k x 27k, the materialised
-# path is faster: 10.9 vs 14.4 ms, tools/xent_bench.py).
-FUSED_XENT: Optional[bool] = None
-XENT_MATERIALISE_MAX_BYTES = 16 << 30
+# Full-catalogue CE heads (linear / tied): True (default) = asme_linear_xent_* (csrc/logits.hip: bf16x6 MFMA logits +
+# online LSE + dH/dW passes, the (n, |V|) logits never stored; at BERT4Rec C3, 37k x 27k, 7.2 ms against 10.0 ms for
+# library-GEMM logits + CE, tools/xent_bench.py); False = materialised logits on asme_logits + the CE kernels.
+FUSED_XENT: bool = True
 
 
 def _rows_cross_entropy(model, sequence, rows, targets, pad: int) -> torch.Tensor:
     """CrossEntropyLoss(ignore_index=pad) of the full-catalogue logits at the flattened positions `rows`
     (masked_training_module.py:93-111 / losses.py:77-115).  With a linear or tied head the logits are never
     materialised (ops.linear_cross_entropy); otherwise they are, for the selected rows only."""
-    wb = model.head_weight_bias() if FUSED_XENT is not False and hasattr(model, "head_weight_bias") else None
+    wb = model.head_weight_bias() if hasattr(model, "head_weight_bias") else None
     if wb is not None:
         h = model.encode_rows(sequence, rows)
-        big = 8 * h.shape[0] * wb[0].shape[0] > XENT_MATERIALISE_MAX_BYTES
-        if (FUSED_XENT or big) and ops.linear_xent_ok(h, wb[0]):
+        if FUSED_XENT and ops.linear_xent_ok(h, wb[0]):
             return ops.linear_cross_entropy(h, wb[0], wb[1], targets, pad)
-        return ops.cross_entropy(F.linear(h, wb[0], wb[1]), targets, pad)
+        return ops.cross_entropy(ops.logits(h, wb[0], wb[1]), targets, pad)
     return ops.cross_entropy(model.forward_rows(sequence, rows), targets, pad)
 
 
