@@ -198,7 +198,13 @@ def bench_bert4rec(args, asme, dev, world, rank):
     store = asme.batches.SessionStore(flat, torch.arange(n_sess + 1, device=dev) * L)
     cloze = asme.batches.ClozeMaskProcessor(tok, 0.2, 0.1)
     order = torch.randperm(n_sess, device=dev, generator=g)
-    params = [p for p in model.parameters() if p.requires_grad]
+
+    # N > 1: data parallel with DDP semantics (dataparallel.GradientAllReduce: bucketed RCCL all-reduce launched
+    # from the backward hooks, the row-sparse item table reduced last)
+    reducer = None
+    if world > 1:
+        reducer = asme.dataparallel.GradientAllReduce(module)
+        reducer.broadcast_parameters(module)
 
     def step(i):
         idx = order[(i * B) % (n_sess - B + 1):][:B]
@@ -206,19 +212,10 @@ def bench_bert4rec(args, asme, dev, world, rank):
         batch = cloze.process_batch(items, lengths, seed=1000 + i)
         if kebert:
             batch["genre"] = torch.where(items > 0, items % (n_genre - 1) + 1, 0)
-        loss = module.training_step(batch, i)["loss"]
-        loss.backward()
-        if world > 1:
-            flat_g = torch.cat([p.grad.reshape(-1) for p in params])
-            dist.all_reduce(flat_g)
-            flat_g.mul_(1.0 / world)
-            off = 0
-            for p in params:
-                p.grad.copy_(flat_g[off:off + p.numel()].view_as(p.grad))
-                off += p.numel()
-        opt.step()
-        sched.step()
-        opt.zero_grad(set_to_none=True)
+        if reducer is not None:
+            asme.dataparallel.train_step(module, opt, sched, reducer, batch, i)
+        else:
+            asme.modules.train_step(module, opt, sched, batch, i)
 
     for i in range(args.warmup):
         step(i)

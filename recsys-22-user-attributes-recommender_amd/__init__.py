@@ -5,7 +5,7 @@ registers it).  Public surface mirrors the reference (LSX-UniWue/recsys-22-user-
 models (SASRecModel, BERT4RecModel, KeBERT4RecModel, NarmModel), training modules, losses, metrics,
 and `registry.register()` for ASME's `imports:` plugin mechanism.
 """
-from . import _lib, batches, datasets, layers, losses, metrics, models, modules, ops, optim, registry, sequence, sharded, tokenization  # noqa
+from . import _lib, batches, dataparallel, datasets, layers, losses, metrics, models, modules, ops, optim, registry, sequence, sharded, tokenization  # noqa
 from .models import BERT4RecModel, KeBERT4RecModel, NarmModel, SASRecModel  # noqa
 from .modules import (MaskedTrainingModule, NextItemPredictionTrainingModule,  # noqa
                       SequenceNextItemPredictionTrainingModule)
