@@ -70,6 +70,10 @@ class _AutoFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
                     pass
 
             module.LightningModule = LightningModule
+            core = types.ModuleType("pytorch_lightning.core")  # `from pytorch_lightning import core as pl`
+            core.LightningModule = LightningModule
+            module.core = core
+            sys.modules["pytorch_lightning.core"] = core
             module.seed_everything = _seed_everything
             module.Trainer = _Dummy
             module.Callback = type("Callback", (), {})

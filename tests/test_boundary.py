@@ -86,3 +86,28 @@ def test_forward_without_gpu_fails_loudly(asme):
                                                  "negative_samples": torch.from_numpy(z["neg"])})
     with pytest.raises(asme._lib.ASMEKernelError):
         model(batch)
+
+
+def test_asme_factory_builds_our_classes(asme):
+    """tests/golden/registry_build.json (make_registry_fixture.py, generated against ASME itself): after
+    registry.register(), ASME's GenericModuleFactory built OUR module and model classes from yaml `module:`
+    sections, with the item vocabulary injected by ASME's @inject, the row-sparse table gradient on by default,
+    and the reference's state_dict key set"""
+    import json
+    import os
+    from helpers import GOLDEN
+    with open(os.path.join(GOLDEN, "registry_build.json")) as f:
+        fx = json.load(f)
+    assert set(fx["registered"]) >= {"sasrec-neg", "sasrec-cross", "bert4rec", "kebert4rec", "narm"}
+    for key, b in fx["builds"].items():
+        assert b["module_defined_in"] == "asme_amd.modules", key
+        assert b["model_defined_in"] == "asme_amd.models", key
+        assert b["item_vocab_size"] == 1003, key  # 1000 items + PAD/MASK/UNK from the injected tokenizer
+        assert b["table_grad"] == "sparse", key
+        cls = getattr(asme, b["module_class"])
+        params = [p for p in inspect.signature(cls.__init__).parameters if p != "self"]
+        assert params == b["module_init_params"], key
+    # the same model built directly has the key set ASME built
+    m = asme.SASRecModel(transformer_hidden_size=128, num_transformer_heads=2, num_transformer_layers=2,
+                         item_vocab_size=1003, max_seq_length=200, transformer_dropout=0.2)
+    assert sorted(m.state_dict().keys()) == fx["builds"]["sasrec-neg"]["state_dict_keys"]
