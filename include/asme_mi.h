@@ -256,6 +256,11 @@ int asme_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t 
                      void* stream);
 
 
+/* nn.Dropout (training): y = x * keep / (1 - p), keep iff a Philox4x32-10 uniform (seed, salt 6, element index / 4)
+ * >= p; the gradient is the same call on dy with the same seed (x may alias y).  Reference: the embedding dropout of
+ * UBERT4Rec (ubert4rec/components.py:157-160). */
+int asme_dropout(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream);
+
 /* ---- General Linear GEMMs (csrc/linear.hip), fp32 MFMA: the widths asme_ws_linear does not tile (e.g. the
  * reference's d = 32 / 64 configurations; in_f, out_f multiples of 4, rows 16-B aligned).  w is nn.Linear.weight
  * (out_f x in_f, row-major).  Reference: transformer_layers.py:175-199 (projections), 212-220

@@ -57,6 +57,7 @@ SIGNATURES = {
     "asme_linear_dx": [p, i64, i64, i64, p, i64, p, i64, i32, p],
     "asme_attention_dropout_mask_bytes": [i64, i64, i64],
     "asme_gelu_dropout_fwd": [p, i64, f32, u64, p, p],
+    "asme_dropout": [p, i64, f32, u64, p, p],
     "asme_gelu_dropout_bwd": [p, p, i64, f32, u64, p, p],
     "asme_attention_fwd": [p, p, p, i64, i64, i64, p, i64, i64, i64, i64, i32, f32, f32, u64, p, i64, p, p, p],
     "asme_attention_bwd": [p, p, p, i64, i64, i64, p, i64, p, i64, p, p, i64, i64, i64, i64, i32, f32, f32, u64, p,

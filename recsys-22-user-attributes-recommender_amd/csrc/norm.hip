@@ -213,6 +213,25 @@ __global__ __launch_bounds__(256) void gelu_dropout_fwd_kernel(const float* __re
     }
 }
 
+// y = dropout_p(x) (nn.Dropout in training mode): keep iff u >= p, kept values scaled by 1/(1-p); 4 consecutive
+// elements share one Philox4x32-10 block (salt 6).  The backward regenerates the same decisions from (seed, index).
+// Reference: UBERT4RecSequenceElementsRepresentationComponent.dropout_embedding (ubert4rec/components.py:157-160).
+__global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x, int64_t n, float p, uint64_t seed,
+                                                      float* __restrict__ y) {
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i >= n) return;
+    float u[4];
+    philox_uniform4(seed, 6u, (uint64_t)i >> 2, u);
+    const float k = 1.f / (1.f - p);
+    if (i + 3 < n && ((uintptr_t)(x + i) & 15) == 0 && ((uintptr_t)(y + i) & 15) == 0) {
+        const float4 v = *reinterpret_cast<const float4*>(x + i);
+        *reinterpret_cast<float4*>(y + i) = make_float4(u[0] >= p ? v.x * k : 0.f, u[1] >= p ? v.y * k : 0.f,
+                                                        u[2] >= p ? v.z * k : 0.f, u[3] >= p ? v.w * k : 0.f);
+    } else {
+        for (int64_t j = i; j < n && j < i + 4; ++j) y[j] = u[j - i] >= p ? x[j] * k : 0.f;
+    }
+}
+
 __global__ __launch_bounds__(256) void gelu_dropout_bwd_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ dy, int64_t n, float p,
                                                                uint64_t seed, float* __restrict__ dx) {
@@ -343,4 +362,15 @@ ASME_API int asme_gelu_dropout_bwd(const float* x, const float* dy, int64_t n, f
     hipLaunchKernelGGL(gelu_dropout_bwd_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        x, dy, n, p, seed, dx);
     ASME_LAUNCH_CHECK("asme_gelu_dropout_bwd");
+}
+
+// y = dropout_p(x); the backward is the same call on dy (identical decisions from the same seed)
+ASME_API int asme_dropout(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream) {
+    ASME_CHECK_ARG(x && y, "asme_dropout: null pointer");
+    ASME_CHECK_ARG(p >= 0.f && p < 1.f, "asme_dropout: p in [0, 1)");
+    if (n == 0) return 0;
+    const int64_t n4 = (n + 3) / 4;
+    hipLaunchKernelGGL(dropout_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, n, p,
+                       seed, y);
+    ASME_LAUNCH_CHECK("asme_dropout");
 }

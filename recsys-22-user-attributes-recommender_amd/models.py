@@ -260,6 +260,166 @@ class KeBERT4RecModel(TransformerEncoderModel):
         return True
 
 
+# ------------------------------------------------------------------------------------ UBERT4Rec
+class _UserLinearUpscaler(nn.Module):
+    """multi-hot(ids) -> Linear(vocab -> d) WITHOUT dropping the pad category (ubert4rec/components.py:13-31)"""
+
+    def __init__(self, vocab_size: int, embed_size: int):
+        super().__init__()
+        self.linear = nn.Linear(vocab_size, embed_size)
+        self.vocab_size = vocab_size
+
+    def forward(self, content_input: torch.Tensor) -> torch.Tensor:
+        table = self.linear.weight.t().contiguous()  # (vocab, d): column gather == row gather
+        return ops.gather_sum(content_input, table, self.linear.bias, skip_zero=False, multi_hot=True)
+
+
+def _build_user_embedding_type(embedding_type: str, vocab_size: int, hidden_size: int) -> nn.Module:
+    """ubert4rec/components.py:33-46"""
+    if embedding_type in ("user_embedding", "content_embedding"):
+        return Ly._ContentEmbedding(num_embeddings=vocab_size, embedding_dim=hidden_size)
+    if embedding_type == "linear_upscale":
+        return Ly.LinearUpscaler(vocab_size=vocab_size, embed_size=hidden_size)
+    if embedding_type == "user_linear_upscale":
+        return _UserLinearUpscaler(vocab_size=vocab_size, embed_size=hidden_size)
+    raise KeyError(embedding_type)
+
+
+class UBERT4RecSequenceElementsRepresentationComponent(nn.Module):
+    """ubert4rec/components.py:49-160: item + position rows (+ the additional attributes) on the embedding kernel,
+    the user-attribute token prepended, + segment rows, LayerNorm, dropout -- every gather and the LN / dropout on
+    the gfx950 kernels"""
+
+    def __init__(self, item_embedding_layer: Ly.TransformerEmbedding, embedding_size: int,
+                 additional_attributes: Optional[Dict[str, Dict[str, Any]]],
+                 user_attributes: Optional[Dict[str, Dict[str, Any]]], additional_tokenizers: Dict[str, Any],
+                 segment_embedding: bool = True, dropout: float = 0.0, replace_first_item: bool = False):
+        super().__init__()
+        if replace_first_item:
+            raise NotImplementedError("replace_first_item (unused by UBERT4RecModel) is outside the hot path")
+        self.segment_embedding = None
+        self.item_embedding_layer = item_embedding_layer
+        self.segment_embedding_active = segment_embedding
+        self.attribute_types = 0
+        self.replace_first_item = replace_first_item
+        add = {}
+        if additional_attributes is not None:
+            for name, info in additional_attributes.items():
+                vocab = len(additional_tokenizers["tokenizers." + name])
+                add[name] = _build_user_embedding_type(info["embedding_type"], vocab, embedding_size)
+            self.attribute_types += 1  # once for all additional attributes, as the reference counts
+        self.additional_attribute_embeddings = nn.ModuleDict(add)
+        users = {}
+        if user_attributes is not None:
+            for name, info in user_attributes.items():
+                vocab = len(additional_tokenizers["tokenizers." + name])
+                users[name] = _build_user_embedding_type(info["embedding_type"], vocab, embedding_size)
+                self.attribute_types += 1
+        self.user_attribute_embeddings = nn.ModuleDict(users)
+        if self.segment_embedding_active:
+            self.segment_embedding = Ly._ContentEmbedding(self.attribute_types, embedding_size)
+        self.dropout_embedding = nn.Dropout(dropout)
+        self.norm_embedding = nn.LayerNorm(embedding_size)
+
+    def forward(self, sequence) -> torch.Tensor:
+        extra = Ly._attribute_sum(self.additional_attribute_embeddings, sequence)
+        emb = self.item_embedding_layer.embed(sequence.sequence, extra=extra)  # E[id] + P[pos] + attributes
+        user = None
+        for key, module in self.user_attribute_embeddings.items():
+            meta = get_attribute(sequence, key)[:, 0:1]
+            e = module(meta)
+            user = e if user is None else user + e
+        if user is not None:
+            emb = torch.cat([user, emb], dim=1)
+        if self.segment_embedding_active:
+            B, T = emb.shape[0], emb.shape[1]
+            segs = torch.ones(B, T, dtype=torch.int64, device=emb.device)
+            if user is not None:
+                segs[:, 0] = 0
+            emb = emb + self.segment_embedding(segs)
+        return ops.dropout(ops.layer_norm(emb, self.norm_embedding), Ly._p(self.dropout_embedding, self.training))
+
+
+class UserTransformerSequenceRepresentationComponent(nn.Module):
+    """ubert4rec/components.py:162-203: the transformer over [user token, items]; the key mask gains a valid user
+    position; causal when bidirectional=False (as UBERT4RecModel builds it)"""
+
+    def __init__(self, transformer_hidden_size: int, num_transformer_heads: int, num_transformer_layers: int,
+                 transformer_dropout: float, user_attributes: Optional[Dict[str, Dict[str, Any]]], bidirectional: bool,
+                 transformer_attention_dropout: Optional[float] = None,
+                 transformer_intermediate_size: Optional[int] = None, replace_first_item: bool = False):
+        super().__init__()
+        self.user_attributes = user_attributes
+        self.bidirectional = bidirectional
+        self.replace_first_item = replace_first_item
+        if transformer_intermediate_size is None:
+            transformer_intermediate_size = 4 * transformer_hidden_size
+        self.transformer_encoder = Ly.TransformerLayer(transformer_hidden_size, num_transformer_heads,
+                                                       num_transformer_layers, transformer_intermediate_size,
+                                                       transformer_dropout,
+                                                       attention_dropout=transformer_attention_dropout)
+
+    def forward(self, embedded: torch.Tensor, padding_mask: Optional[torch.Tensor]) -> torch.Tensor:
+        if padding_mask is not None and self.user_attributes and not self.replace_first_item:
+            padding_mask = torch.cat([torch.ones(padding_mask.shape[0], 1, dtype=padding_mask.dtype,
+                                                 device=padding_mask.device), padding_mask], dim=1)
+        kv = Ly.key_valid_mask(padding_mask, embedded.shape)
+        return self.transformer_encoder(embedded, kv, causal=not self.bidirectional)
+
+
+class UBERT4RecModel(TransformerEncoderModel):
+    """core/models/ubert4rec/ubert4rec_model.py:16-92 -- the user-attribute BERT4Rec variant (the reference builds
+    its transformer with bidirectional=False).  Output (B, L + 1, |V|) when user attributes are configured."""
+
+    def __init__(self, transformer_hidden_size: int, num_transformer_heads: int, num_transformer_layers: int,
+                 item_vocab_size: int, max_seq_length: int, transformer_dropout: float,
+                 additional_attributes: Dict[str, Dict[str, Any]], additional_tokenizers: Dict[str, Any],
+                 user_attributes: Dict[str, Dict[str, Any]], positional_embedding: bool, segment_embedding: bool,
+                 embedding_pooling_type: str = None, initializer_range: float = 0.02,
+                 transformer_intermediate_size: Optional[int] = None,
+                 transformer_attention_dropout: Optional[float] = None):
+        self.additional_userdata_keys = []
+        self.additional_metadata_keys = []
+        if user_attributes is not None:
+            self.additional_metadata_keys = list(user_attributes.keys())
+            self.additional_userdata_keys = list(user_attributes.keys())
+            max_seq_length += 1
+        if additional_attributes is not None:
+            self.additional_metadata_keys = self.additional_metadata_keys + list(additional_attributes.keys())
+        emb = Ly.TransformerEmbedding(item_vocab_size, max_seq_length, transformer_hidden_size, 0.0,
+                                      embedding_pooling_type=embedding_pooling_type, norm_embedding=False,
+                                      positional_embedding=positional_embedding)
+        element_rep = UBERT4RecSequenceElementsRepresentationComponent(
+            emb, transformer_hidden_size, additional_attributes, user_attributes, additional_tokenizers,
+            segment_embedding, dropout=transformer_dropout, replace_first_item=False)
+        modifier = Ly.FFNSequenceRepresentationModifierComponent(transformer_hidden_size)
+        projection = Ly.build_projection_layer(Ly.PROJECT_TYPE_LINEAR, transformer_hidden_size, item_vocab_size,
+                                               emb.item_embedding.embedding)
+        super().__init__(transformer_hidden_size=transformer_hidden_size, num_transformer_heads=num_transformer_heads,
+                         num_transformer_layers=num_transformer_layers, transformer_dropout=transformer_dropout,
+                         embedding_layer=element_rep, sequence_representation_modifier_layer=modifier,
+                         projection_layer=projection, bidirectional=False,
+                         transformer_intermediate_size=transformer_intermediate_size,
+                         transformer_attention_dropout=transformer_attention_dropout)
+        self._sequence_representation_layer = UserTransformerSequenceRepresentationComponent(
+            transformer_hidden_size, num_transformer_heads, num_transformer_layers, transformer_dropout,
+            user_attributes, bidirectional=False, transformer_attention_dropout=transformer_attention_dropout,
+            transformer_intermediate_size=transformer_intermediate_size)
+        self.apply(functools.partial(normal_initialize_weights, initializer_range=initializer_range))
+
+    def required_metadata_keys(self):
+        return self.additional_metadata_keys
+
+    def optional_metadata_keys(self):
+        return self.additional_userdata_keys
+
+    def item_table(self):
+        return self._sequence_embedding_layer.item_embedding_layer.get_item_embedding_weight()
+
+    def table_grad_sparse_ok(self) -> bool:
+        return True
+
+
 # ------------------------------------------------------------------------------------ NARM
 class SequenceElementsEmbeddingComponent(nn.Module):
     """core/models/common/components/representations/sequence_embedding.py:12-35"""

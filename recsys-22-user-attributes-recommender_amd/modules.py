@@ -372,6 +372,43 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         return [optimizer]
 
 
+class UBERTMaskedTrainingModule(MaskedTrainingModule):
+    """core/modules/ubert_masked_training_module.py:20-208: masked-item training of UBERT4Rec, whose output has one
+    more position (the user token) in front when user attributes are configured: the targets and the eval mask
+    get a leading pad / False column.  Same loss (CrossEntropyLoss(ignore_index=pad), on the fused logits head),
+    optimizer (Adam without weight decay) and warm-up as MaskedTrainingModule."""
+
+    def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
+                 beta_2: float = 0.998, weight_decay: float = 0.001, num_warmup_steps: int = 10000,
+                 table_grad: Optional[str] = None):
+        super().__init__(model, item_tokenizer, metrics, learning_rate, beta_1, beta_2, weight_decay,
+                         num_warmup_steps, table_grad)
+        self.user_key_len = len(model.optional_metadata_keys())
+
+    def _with_user_column(self, x: torch.Tensor, fill) -> torch.Tensor:
+        if self.user_key_len == 0:
+            return x
+        return torch.cat([torch.full((x.shape[0], 1), fill, dtype=x.dtype, device=x.device), x], dim=1)
+
+    def training_step(self, batch, batch_idx):
+        batch = dict(batch)
+        target = batch[TARGET_ENTRY_NAME]
+        if target.dim() > 2:
+            raise NotImplementedError("basket (multi-target) masked training is outside the MI355X hot path")
+        batch[TARGET_ENTRY_NAME] = self._with_user_column(target, self.item_tokenizer.pad_token_id)
+        return super().training_step(batch, batch_idx)
+
+    def _get_prediction_for_masked_item(self, batch, batch_idx=None) -> torch.Tensor:
+        self._flush_table()
+        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
+        target_mask = input_seq.eq(self.item_tokenizer.mask_token_id)
+        if target_mask.dim() == 3:
+            target_mask = target_mask.max(dim=-1).values
+        target_mask = self._with_user_column(target_mask, False)
+        rows = torch.nonzero(target_mask.reshape(-1)).squeeze(1)
+        return self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
+
+
 def split_optimizers(configured):
     """Normalise configure_optimizers() output -> (optimizer, scheduler or None)."""
     if isinstance(configured, torch.optim.Optimizer):

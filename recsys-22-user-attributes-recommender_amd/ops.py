@@ -349,10 +349,10 @@ class _GatherSumFn(torch.autograd.Function):
     (multi-hot -> Linear == sum of weight columns of the non-pad ids, + bias)."""
 
     @staticmethod
-    def forward(ctx, ids, table, bias, skip_zero: bool):
+    def forward(ctx, ids, table, bias, skip_zero: bool, multi_hot: bool):
         ids = _i64(ids)
         shape = ids.shape
-        if skip_zero:  # (N, S, K) multi-hot ids
+        if multi_hot:  # (N, S, K) multi-hot ids
             n, k = ids.numel() // shape[-1], shape[-1]
             out_shape = shape[:-1]
         else:
@@ -376,7 +376,7 @@ class _GatherSumFn(torch.autograd.Function):
         g_bias = None
         if has_bias:
             g_bias = _reduce_rows(dout)
-        return None, g_table, g_bias, None
+        return None, g_table, g_bias, None, None
 
 
 def scatter_add_rows(rows: torch.Tensor, ids: torch.Tensor, dest: torch.Tensor, scale: float = 1.0):
@@ -418,8 +418,11 @@ def bucket_by_owner(unique: torch.Tensor, world: int):
     return order, send_local, counts, pos
 
 
-def gather_sum(ids, table, bias=None, skip_zero=False):
-    return _GatherSumFn.apply(ids, table, bias, skip_zero)
+def gather_sum(ids, table, bias=None, skip_zero=False, multi_hot=None):
+    """sum over the last id dimension of table rows (+ bias): multi_hot (default: skip_zero) = (..., K) ids summed
+    per position (LinearUpscaler: the pad category 0 skipped; UBERT4Rec's user upscaler counts it), else one row
+    per id (nn.Embedding)"""
+    return _GatherSumFn.apply(ids, table, bias, skip_zero, skip_zero if multi_hot is None else multi_hot)
 
 
 # ------------------------------------------------------------------------------------ linear
@@ -565,6 +568,31 @@ def ffn(x, w1, b1, w2, b2, p: float = 0.0):
             and b1 is not None and b1.is_contiguous()):
         return _FFNFn.apply(x, w1, b1, w2, b2, p)
     return linear(gelu_dropout(linear(x, w1, b1), p), w2, b2)
+
+
+class _DropoutFn(torch.autograd.Function):
+    """nn.Dropout in training mode on asme_dropout; the backward replays the decisions from the seed"""
+
+    @staticmethod
+    def forward(ctx, x, p: float):
+        xc = _f32(x)
+        seed = new_seed(p)
+        y = torch.empty_like(xc)
+        call("asme_dropout", ptr(xc), xc.numel(), p, seed, ptr(y), stream())
+        ctx.meta = (p, seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed = ctx.meta
+        g = _f32(dy)
+        dx = torch.empty_like(g)
+        call("asme_dropout", ptr(g), g.numel(), p, seed, ptr(dx), stream())
+        return dx, None
+
+
+def dropout(x, p: float):
+    return _DropoutFn.apply(x, p) if p > 0.0 else x
 
 
 # ------------------------------------------------------------------------------------ layer norm

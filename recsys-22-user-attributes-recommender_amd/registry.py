@@ -3,8 +3,8 @@
 ASME loads a plugin listed in a config's `imports:` section (core/init/factories/include/
 import_factory.py:33-79) after its default registries; the plugin calls
 `register_module(key, ModuleConfig(GenericModuleFactory, ModuleCls, {"model_cls": ...}), overwrite=True)`
-(core/modules/registry.py:19-24).  `register()` does exactly that for the five hot-path keys
-(core/modules/config.py:30-55), wrapping the classes with ASME's own @inject so `item_vocab_size`,
+(core/modules/registry.py:19-24).  `register()` does exactly that for the six hot-path keys
+(core/modules/config.py:27-55), wrapping the classes with ASME's own @inject so `item_vocab_size`,
 `item_tokenizer` and `additional_attributes_tokenizer` are injected as for the reference classes.
 """
 from __future__ import annotations
@@ -18,6 +18,7 @@ KEYS = {
                      {"loss_function": losses.SASRecFullSequenceCrossEntropyLoss}),
     "bert4rec": (modules.MaskedTrainingModule, models.BERT4RecModel, {}),
     "kebert4rec": (modules.MaskedTrainingModule, models.KeBERT4RecModel, {}),
+    "ubert4rec": (modules.UBERTMaskedTrainingModule, models.UBERT4RecModel, {}),
     "narm": (modules.NextItemPredictionTrainingModule, models.NarmModel, {}),
 }
 
@@ -37,8 +38,9 @@ def register(overwrite: bool = True):
 
     for key, (module_cls, model_cls, extra) in KEYS.items():
         model_injects = {"item_vocab_size": InjectVocabularySize("item")}
-        if "additional_attributes_tokenizer" in model_cls.__init__.__code__.co_varnames:
-            model_injects["additional_attributes_tokenizer"] = InjectTokenizers()
+        for name in ("additional_attributes_tokenizer", "additional_tokenizers"):
+            if name in model_cls.__init__.__code__.co_varnames:
+                model_injects[name] = InjectTokenizers()
         m_cls = _with_asme_injection(module_cls, item_tokenizer=InjectTokenizer("item"))
         md_cls = _with_asme_injection(model_cls, **model_injects)
         register_module(key, ModuleConfig(GenericModuleFactory, m_cls, {"model_cls": md_cls, **extra}),

@@ -69,6 +69,12 @@ class _AutoFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
                 def log(self, *a, **k):
                     pass
 
+                @property
+                def device(self):  # LightningModule.device (ubert_masked_training_module.py:72)
+                    import torch
+                    p = next(self.parameters(), None)
+                    return p.device if p is not None else torch.device("cpu")
+
             module.LightningModule = LightningModule
             core = types.ModuleType("pytorch_lightning.core")  # `from pytorch_lightning import core as pl`
             core.LightningModule = LightningModule

@@ -286,6 +286,75 @@ def gen_kebert4rec(variant: str, B=4, L=10, d=32, h=2, N=2, NI=41, NG=7, NT=9, K
     print("kebert4rec", variant + suffix, float(loss))
 
 
+def gen_ubert4rec(variant: str):
+    """ubert4rec: UBERTMaskedTrainingModule + UBERT4RecModel (the user-attribute model): a user token prepended to
+    the item sequence, attribute embeddings, optional segment embedding, causal transformer (bidirectional=False)
+    core/models/ubert4rec/ubert4rec_model.py:16-92, components.py:13-203, core/modules/ubert_masked_training_module.py"""
+    B, L, d, h, N, NI, NG, NU, K = 4, 10, 32, 2, 2, 43, 7, 6, 3
+    tok = S.make_tokenizer(NI)
+    gtok = S.make_tokenizer(NG, "Genre")
+    utok = S.make_tokenizer(NU, "User")
+    S.set_context({"item": tok, "genre": gtok, "user": utok})
+    from asme.core.models.ubert4rec.ubert4rec_model import UBERT4RecModel
+    from asme.core.modules.ubert_masked_training_module import UBERTMaskedTrainingModule
+    V = len(tok)
+    if variant == "seg":
+        additional = {"genre": {"embedding_type": "content_embedding"}}
+        users = {"user": {"embedding_type": "user_embedding"}}
+        segment = True
+    else:
+        additional = {"genre": {"embedding_type": "linear_upscale"}}
+        users = {"user": {"embedding_type": "user_linear_upscale"}}
+        segment = False
+    torch.manual_seed(10)
+    # UBERT4RecModel / UBERTMaskedTrainingModule carry the Inject* annotations without @inject: pass them
+    model = UBERT4RecModel(transformer_hidden_size=d, num_transformer_heads=h, num_transformer_layers=N,
+                           item_vocab_size=V, max_seq_length=L, transformer_dropout=0.0,
+                           additional_attributes=additional,
+                           additional_tokenizers={"tokenizers.genre": gtok, "tokenizers.user": utok},
+                           user_attributes=users, positional_embedding=True, segment_embedding=segment)
+    module = UBERTMaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None, num_warmup_steps=0)
+    sd = _sd(model)
+    g = torch.Generator().manual_seed(11)
+    lengths = [10, 7, 4, 2]
+    seq, tgt = _cloze_batch(g, B, L, V, lengths)
+    if variant == "seg":
+        genre = torch.randint(3, len(gtok), (B, L), generator=g)
+        genre[seq == PAD] = PAD
+        user = torch.randint(3, len(utok), (B, L), generator=g)   # the user id in every column; column 0 is read
+    else:
+        genre = torch.randint(3, len(gtok), (B, L, K), generator=g)
+        genre[:, :, 2][torch.rand(B, L, generator=g) < 0.5] = 0
+        genre[seq == PAD] = 0
+        user = torch.randint(3, len(utok), (B, L, K), generator=g)
+        user[:, :, 1] = 0                                          # a pad category the user upscaler does count
+    batch = {"item": seq, "item.target": tgt, "genre": genre, "user": user}
+    res = module.training_step(batch, 0)
+    loss = res["loss"]
+    loss.backward()
+    grads = _grads(model)
+    opts = module.configure_optimizers()
+    opts[0].step()
+    after = _params(model, "adam1")
+    model.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in sd.items()})
+    ev = seq.clone()
+    ev[ev == MASK] = 7
+    for b, n in enumerate(lengths):
+        ev[b, n - 1] = MASK
+    with torch.no_grad():
+        logits = module(batch, 0)
+        pred = module.predict_step(dict(batch, item=ev), 0)
+    out = dict(sd)
+    out.update(grads)
+    out.update(after)
+    out.update(dict(seq=seq.numpy(), target=tgt.numpy(), genre=genre.numpy(), user=user.numpy(),
+                    logits=logits.numpy(), loss=loss.detach().numpy(), eval_seq=ev.numpy(), eval_logits=pred.numpy(),
+                    cfg=np.array([B, L, d, h, N, V, len(gtok), len(utok)]), lr=np.float32(1e-3),
+                    betas=np.array([0.99, 0.998], np.float32)))
+    np.savez_compressed(os.path.join(HERE, f"ubert4rec_{variant}.npz"), **out)
+    print("ubert4rec", variant, float(loss), logits.shape)
+
+
 def gen_narm():
     """narm: NextItemPredictionTrainingModule + NarmModel (single-target CE)
     core/models/narm/narm_model.py:25-68, components.py:14-56, layers.py:8-120, core/losses/losses.py:65-115"""
@@ -447,6 +516,9 @@ if __name__ == "__main__":
         gen_kebert4rec("pre")
         gen_kebert4rec("post")
         gen_narm()
+    if "ubert4rec" in which or "models" in which:
+        gen_ubert4rec("seg")
+        gen_ubert4rec("upscale")
     if "d128" in which:
         # the benchmarked composition: d = 128, h = 2, d_ff = 4d = 512, L = 200 -- every
         # Linear on the weight-stationary GEMM, the fused FFN, the production weight-gradient shapes

@@ -62,6 +62,18 @@ def build_model(asme, name, z):
                                     item_vocab_size=V, max_seq_length=L, transformer_dropout=0.0,
                                     prefusion_attributes=pre, postfusion_attributes=post,
                                     additional_attributes_tokenizer=toks)
+    if name.startswith("ubert4rec"):
+        B, L, d, h, N, V, VG, VU = cfg
+        toks = {"tokenizers.genre": Tok(VG), "tokenizers.user": Tok(VU)}
+        if name.endswith("seg"):
+            add, users = {"genre": {"embedding_type": "content_embedding"}}, {"user": {"embedding_type": "user_embedding"}}
+        else:
+            add = {"genre": {"embedding_type": "linear_upscale"}}
+            users = {"user": {"embedding_type": "user_linear_upscale"}}
+        return asme.UBERT4RecModel(transformer_hidden_size=d, num_transformer_heads=h, num_transformer_layers=N,
+                                   item_vocab_size=V, max_seq_length=L, transformer_dropout=0.0,
+                                   additional_attributes=add, additional_tokenizers=toks, user_attributes=users,
+                                   positional_embedding=True, segment_embedding=name.endswith("seg"))
     if name == "narm":
         B, L, E, H, V = cfg
         return asme.NarmModel(item_vocab_size=V, item_embedding_size=E, global_encoder_size=H,
@@ -70,7 +82,7 @@ def build_model(asme, name, z):
 
 
 MODEL_FIXTURES = ["sasrec_neg", "sasrec_cross", "bert4rec_transpose_embedding", "bert4rec_linear",
-                  "kebert4rec_pre", "kebert4rec_post", "narm"]
+                  "kebert4rec_pre", "kebert4rec_post", "ubert4rec_seg", "ubert4rec_upscale", "narm"]
 # the benchmarked composition: d = 128, h = 2, d_ff = 512, L = 200 (make_golden.py d128)
 D128_FIXTURES = ["sasrec_neg_d128", "bert4rec_linear_d128", "bert4rec_transpose_embedding_d128",
                  "kebert4rec_post_d128"]

@@ -1,6 +1,6 @@
 """CPU: the drop-in boundary.  Constructor signatures equal the reference's (ASME's GenericModelFactory
 introspects them), state_dict keys equal the reference's (checkpoints / fixtures interchange), the
-registry covers the five hot-path keys, and the product path refuses to run without the GPU."""
+registry covers the six hot-path keys, and the product path refuses to run without the GPU."""
 import inspect
 
 import pytest
@@ -23,6 +23,13 @@ REFERENCE_SIGNATURES = {
                         "postfusion_attributes", "additional_attributes_tokenizer", "postfusion_merge_function",
                         "positional_embedding", "embedding_pooling_type", "initializer_range",
                         "transformer_intermediate_size", "transformer_attention_dropout"],
+    "UBERT4RecModel": ["transformer_hidden_size", "num_transformer_heads", "num_transformer_layers",
+                       "item_vocab_size", "max_seq_length", "transformer_dropout", "additional_attributes",
+                       "additional_tokenizers", "user_attributes", "positional_embedding", "segment_embedding",
+                       "embedding_pooling_type", "initializer_range", "transformer_intermediate_size",
+                       "transformer_attention_dropout"],
+    "UBERTMaskedTrainingModule": ["model", "item_tokenizer", "metrics", "learning_rate", "beta_1", "beta_2",
+                                  "weight_decay", "num_warmup_steps"],
     "NarmModel": ["item_vocab_size", "item_embedding_size", "global_encoder_size", "global_encoder_num_layers",
                   "embedding_dropout", "context_dropout", "batch_first", "embedding_pooling_type"],
     "SequenceNextItemPredictionTrainingModule": ["model", "item_tokenizer", "metrics", "learning_rate", "beta_1",
@@ -75,7 +82,7 @@ def test_bert4rec_has_no_position_embedding(asme):
 
 
 def test_registry_keys(asme):
-    assert set(asme.registry.KEYS) == {"sasrec-neg", "sasrec-cross", "bert4rec", "kebert4rec", "narm"}
+    assert set(asme.registry.KEYS) == {"sasrec-neg", "sasrec-cross", "bert4rec", "kebert4rec", "ubert4rec", "narm"}
 
 
 def test_forward_without_gpu_fails_loudly(asme):
@@ -98,7 +105,7 @@ def test_asme_factory_builds_our_classes(asme):
     from helpers import GOLDEN
     with open(os.path.join(GOLDEN, "registry_build.json")) as f:
         fx = json.load(f)
-    assert set(fx["registered"]) >= {"sasrec-neg", "sasrec-cross", "bert4rec", "kebert4rec", "narm"}
+    assert set(fx["registered"]) >= {"sasrec-neg", "sasrec-cross", "bert4rec", "kebert4rec", "ubert4rec", "narm"}
     for key, b in fx["builds"].items():
         assert b["module_defined_in"] == "asme_amd.modules", key
         assert b["model_defined_in"] == "asme_amd.models", key

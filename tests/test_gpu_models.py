@@ -24,6 +24,8 @@ def _batch(name, z, dev):
     b = {"item": t("seq"), "item.target": t("target")}
     if name.startswith("kebert4rec"):
         b["genre"], b["tags"] = t("genre"), t("tags")
+    if name.startswith("ubert4rec"):
+        b["genre"], b["user"] = t("genre"), t("user")
     return b
 
 
@@ -37,6 +39,8 @@ def _module(asme, name, model, V):
                                                      loss_function=asme.losses.SASRecFullSequenceCrossEntropyLoss)
     if name == "narm":
         return asme.NextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None)
+    if name.startswith("ubert4rec"):
+        return asme.UBERTMaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None, num_warmup_steps=0)
     warm = 10 if name.startswith("bert4rec") else 0
     return asme.MaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None, num_warmup_steps=warm)
 
@@ -163,6 +167,10 @@ def test_model_eval_outputs_match_reference(asme, dev, name):
             assert rel_err(pred.cpu().numpy(), z["eval_logits"]) < TOL
         if base_name(name).startswith("bert4rec"):
             pred = module.predict_step({"item": torch.from_numpy(z["eval_seq"]).to(dev)}, 0)
+            assert rel_err(pred.cpu().numpy(), z["eval_logits"]) < TOL
+        if name.startswith("ubert4rec"):
+            pred = module.predict_step(dict(batch, item=torch.from_numpy(z["eval_seq"]).to(dev)), 0)
+            assert pred.shape == z["eval_logits"].shape
             assert rel_err(pred.cpu().numpy(), z["eval_logits"]) < TOL
 
 
