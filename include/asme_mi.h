@@ -260,6 +260,10 @@ int asme_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t 
  * >= p; the gradient is the same call on dy with the same seed (x may alias y).  Reference: the embedding dropout of
  * UBERT4Rec (ubert4rec/components.py:157-160). */
 int asme_dropout(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream);
+/* nn.Dropout2d on (N, C, L) (training): rows of row_len values kept (scaled) or zeroed together, one Philox draw per
+ * row (salt 7, row index / 4); the gradient is the same call on dy.  Reference: NARM's embedding dropout
+ * (core/models/common/layers/sequence_embedding.py:72-73, :92 on (N, S, E) = one draw per position). */
+int asme_dropout_rows(const float* x, int64_t n, int64_t row_len, float p, uint64_t seed, float* y, void* stream);
 
 /* ---- General Linear GEMMs (csrc/linear.hip), fp32 MFMA: the widths asme_ws_linear does not tile (e.g. the
  * reference's d = 32 / 64 configurations; in_f, out_f multiples of 4, rows 16-B aligned).  w is nn.Linear.weight
@@ -322,6 +326,26 @@ int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, con
 int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N);
 int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W, int64_t N, int trans, const float* bias,
                    int epi, float* pre_out, const float* pre_in, float p, uint64_t seed, float* Y, void* stream);
+
+/* ---- NARM encoders (csrc/narm.hip).  Global encoder: one nn.GRU layer, batch_first, h_0 = 0
+ * (core/models/narm/components.py:32-56; the reference packs the padded batch, the recurrence is causal so the
+ * valid positions are identical).  Hidden size padded to hp (multiple of 16, <= 128; padded gate rows/columns and
+ * biases zero).  gx (B, L, 3hp) = x W_ih^T + b_ih (a Linear GEMM); gates (B, L, 4, hp) = r, z, n, W_hn h + b_hn.
+ * h0/dhT/dh0 nullable.  Backward: dgx (B, L, 3hp) = dL/d(input-side pre-activations) -> dX, dW_ih, db_ih;
+ * dgh (B, L, 3hp) = dL/d(W_h* h_{t-1} + b_h*) -> dW_hh = dgh^T H_{t-1}, db_hh. */
+int asme_gru_fwd(const float* gx, const float* whh, const float* bhh, const float* h0, int64_t batch,
+                 int64_t seq_len, int64_t hp, float* hout, float* gates, void* stream);
+int asme_gru_bwd(const float* dhout, const float* dhT, const float* whh, const float* h0, const float* hout,
+                 const float* gates, int64_t batch, int64_t seq_len, int64_t hp, float* dgx, float* dgh, float* dh0,
+                 void* stream);
+/* Local encoder (core/models/narm/layers.py:32-66): alpha = v . sigmoid(p1 + p2_s), c_l = sum_s mask_s alpha_s hs_s;
+ * p1 = A1 c_g (n, h), p2 = A2 h_i (n, s, h), mask (n, s) bytes.  Backward writes dp1, dp2, dhs and the per-row
+ * partials dv_part (n, h) of dL/dv. */
+int asme_narm_attend_fwd(const float* p1, const float* p2, const float* v, const float* hs, const uint8_t* mask,
+                         int64_t n, int64_t s, int64_t h, float* out, float* alpha, void* stream);
+int asme_narm_attend_bwd(const float* dc, const float* p1, const float* p2, const float* v, const float* hs,
+                         const uint8_t* mask, const float* alpha, int64_t n, int64_t s, int64_t h, float* dp1,
+                         float* dp2, float* dhs, float* dv_part, void* stream);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,11 @@ SIGNATURES = {
     "asme_attention_dropout_mask_bytes": [i64, i64, i64],
     "asme_gelu_dropout_fwd": [p, i64, f32, u64, p, p],
     "asme_dropout": [p, i64, f32, u64, p, p],
+    "asme_dropout_rows": [p, i64, i64, f32, u64, p, p],
+    "asme_gru_fwd": [p, p, p, p, i64, i64, i64, p, p, p],
+    "asme_gru_bwd": [p, p, p, p, p, p, i64, i64, i64, p, p, p, p],
+    "asme_narm_attend_fwd": [p, p, p, p, p, i64, i64, i64, p, p, p],
+    "asme_narm_attend_bwd": [p, p, p, p, p, p, p, i64, i64, i64, p, p, p, p, p],
     "asme_gelu_dropout_bwd": [p, p, i64, f32, u64, p, p],
     "asme_attention_fwd": [p, p, p, i64, i64, i64, p, i64, i64, i64, i64, i32, f32, f32, u64, p, i64, p, p, p],
     "asme_attention_bwd": [p, p, p, i64, i64, i64, p, i64, p, i64, p, p, i64, i64, i64, i64, i32, f32, f32, u64, p,

@@ -232,6 +232,18 @@ __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ 
     }
 }
 
+// Dropout2d on (N, C, L) in training mode (NARM's embedding dropout, core/models/common/layers/sequence_embedding.py:
+// 72-73 + :92): whole rows of row_len values are kept (scaled by 1 / (1 - p)) or zeroed, one draw per row.
+__global__ __launch_bounds__(256) void dropout_rows_kernel(const float* __restrict__ x, int64_t n, int64_t row_len,
+                                                           float p, uint64_t seed, float* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t row = i / row_len;
+    float u[4];
+    philox_uniform4(seed, 7u, (uint64_t)row >> 2, u);
+    y[i] = u[row & 3] >= p ? x[i] * (1.f / (1.f - p)) : 0.f;
+}
+
 __global__ __launch_bounds__(256) void gelu_dropout_bwd_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ dy, int64_t n, float p,
                                                                uint64_t seed, float* __restrict__ dx) {
@@ -373,4 +385,15 @@ ASME_API int asme_dropout(const float* x, int64_t n, float p, uint64_t seed, flo
     hipLaunchKernelGGL(dropout_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, n, p,
                        seed, y);
     ASME_LAUNCH_CHECK("asme_dropout");
+}
+
+// Row-wise dropout (Dropout2d semantics on (N, C, L): C rows of row_len); the backward is the same call on dy.
+ASME_API int asme_dropout_rows(const float* x, int64_t n, int64_t row_len, float p, uint64_t seed, float* y,
+                               void* stream) {
+    ASME_CHECK_ARG(x && y, "asme_dropout_rows: null pointer");
+    ASME_CHECK_ARG(p >= 0.f && p < 1.f && row_len >= 1 && n % row_len == 0, "asme_dropout_rows: bad argument");
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(dropout_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                       n, row_len, p, seed, y);
+    ASME_LAUNCH_CHECK("asme_dropout_rows");
 }

@@ -59,7 +59,7 @@ class SequenceElementsEmbeddingLayer(nn.Module):
         self.embedding_mode = embedding_pooling_type
         self.dropout = dropout
         self.pooling = nn.Identity()
-        # NARM's Dropout2d on (N, S, E) drops whole (n, s) positions
+        # NARM's Dropout2d on (N, S, E) drops whole (n, s) positions; applied by _dropout
         self.dropout_layer = nn.Dropout2d(p=dropout) if dropout and dropout > 0.0 else nn.Identity()
         self.embedding = nn.Embedding(num_embeddings=item_voc_size, embedding_dim=embedding_size)
         self.embedding.weight._asme_table_grad = ops.TableGrad()
@@ -67,13 +67,22 @@ class SequenceElementsEmbeddingLayer(nn.Module):
     def get_weight(self) -> torch.Tensor:
         return self.embedding.weight
 
+    def _dropout(self, emb: torch.Tensor) -> torch.Tensor:
+        """Dropout2d (training): on (N, S, E) one draw per (n, s) position, on a 2-D (NI, E) matrix one per element
+        (torch's feature dropout with no spatial dims), sequence_embedding.py:72-73, :92"""
+        p = _p(self.dropout_layer, self.training)
+        if p <= 0.0:
+            return emb
+        return ops.dropout_rows(emb, p) if emb.dim() == 3 else ops.dropout(emb, p)
+
     def forward(self, items: torch.Tensor, flatten: bool = True) -> torch.Tensor:
         spec = ops.EmbeddingSpec(seq_len=items.shape[-1] if items.dim() > 1 else max(1, items.numel()),
                                  table_grad=self.embedding.weight._asme_table_grad)
-        emb = ops.embedding(items, self.embedding.weight, spec=spec)
-        if isinstance(self.dropout_layer, nn.Dropout2d) and self.training:
-            emb = self.dropout_layer(emb)
-        return emb
+        return self._dropout(ops.embedding(items, self.embedding.weight, spec=spec))
+
+    def item_matrix(self) -> torch.Tensor:
+        """forward(arange(|V|), flatten=False) without the identity gather: the whole table through the dropout"""
+        return self._dropout(self.embedding.weight)
 
 
 class TransformerEmbedding(nn.Module):

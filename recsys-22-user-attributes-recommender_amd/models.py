@@ -435,7 +435,8 @@ class SequenceElementsEmbeddingComponent(nn.Module):
 
 
 class LocalEncoderLayer(nn.Module):
-    """v . sigmoid(A1 c_g + A2 h_i), masked weighted sum (core/models/narm/layers.py:8-66)"""
+    """v . sigmoid(A1 c_g + A2 h_i), masked weighted sum (core/models/narm/layers.py:8-66): the projections on the
+    Linear kernels, the attention and weighted sum on asme_narm_attend_fwd/_bwd"""
 
     def __init__(self, hidden_size: int, latent_size: int):
         super().__init__()
@@ -446,17 +447,15 @@ class LocalEncoderLayer(nn.Module):
         torch.nn.init.uniform_(self.v, -1.0, 1.0)
 
     def forward(self, s1, s2, mask):
-        proj = torch.sigmoid(self.A1(s1).unsqueeze(1) + self.A2(s2))      # (N, S, H)
-        alphas = torch.matmul(proj, self.v).unsqueeze(2)                   # (N, S, 1)
-        weighted = mask.unsqueeze(-1).to(s2.dtype) * (alphas * s2)
-        return weighted.sum(dim=1)
+        return ops.narm_attend(ops.linear(s1, self.A1.weight), ops.linear(s2, self.A2.weight), self.v, s2, mask)
 
 
 class NARMSequenceRepresentationComponent(nn.Module):
     """GRU global encoder + attentive local encoder (core/models/narm/components.py:14-56).
     The reference packs the padded batch (lengths.cpu(): a host sync); the GRU is causal,
-    so running it on the padded batch and reading the output at len-1 gives the same c_g and the same
-    masked local context without leaving the device."""
+    so running it on the padded batch (ops.gru: the recurrence kernel) and reading the output at len-1 gives
+    the same c_g and the same masked local context without leaving the device.  nn.GRU is kept for its
+    parameters, initialisation and state_dict keys only; its forward (MIOpen) is never called."""
 
     def __init__(self, item_embedding_size: int, global_encoder_size: int, global_encoder_num_layers: int,
                  context_dropout: float, batch_first: bool = True):
@@ -468,15 +467,18 @@ class NARMSequenceRepresentationComponent(nn.Module):
         self.context_dropout = nn.Dropout(context_dropout)
 
     def forward(self, embedded: torch.Tensor, padding_mask: torch.Tensor) -> torch.Tensor:
-        h_i, _ = self.global_encoder(embedded)
+        h_i = ops.gru(embedded, self.global_encoder)
         last = padding_mask.sum(-1) - 1
         c_g = h_i[torch.arange(h_i.shape[0], device=h_i.device), last]
         c_l = self.local_encoder(c_g, h_i, padding_mask)
-        return self.context_dropout(torch.cat([c_g, c_l], dim=1))
+        return ops.dropout(torch.cat([c_g, c_l], dim=1), Ly._p(self.context_dropout, self.training))
 
 
 class BilinearDecoderLayer(nn.Module):
-    """scores = context . (B E_items)^T over all items (core/models/narm/layers.py:69-120)"""
+    """scores = context . (B E_items)^T over all items (core/models/narm/layers.py:69-120).  The item matrix
+    goes through the embedding layer as in the reference, i.e. with its dropout in training (Dropout2d on the 2-D
+    (|V|, E) matrix = independent elements, layers.py:113-117); W_eff = B(E_items) is a Linear kernel and the
+    scores are the logits kernel (or, in training, never materialised: NarmModel.context_and_head)."""
 
     def __init__(self, embedding_layer: Ly.SequenceElementsEmbeddingLayer, encoded_representation_size: int,
                  apply_softmax: bool = False):
@@ -485,10 +487,13 @@ class BilinearDecoderLayer(nn.Module):
         self.B = nn.Linear(embedding_layer.embedding.weight.size()[1], encoded_representation_size, bias=False)
         self.activation = nn.Softmax() if apply_softmax else nn.Identity()
 
+    def item_weight(self, items: torch.Tensor = None) -> torch.Tensor:
+        """B(embedding_layer(items)) (NI, 2H); all items when items is None"""
+        emb = self.embedding_layer.item_matrix() if items is None else self.embedding_layer(items, flatten=False)
+        return ops.linear(emb, self.B.weight)
+
     def forward(self, context: torch.Tensor, items: torch.Tensor = None):
-        table = self.embedding_layer.embedding.weight
-        emb = table if items is None else F.embedding(items, table)
-        return self.activation(context @ self.B(emb).t())
+        return self.activation(ops.logits(context, self.item_weight(items)))
 
 
 class BilinearProjectionComponent(nn.Module):
@@ -514,3 +519,15 @@ class NarmModel(SequenceRecommenderModel):
 
     def item_table(self):
         return self._sequence_embedding_layer.elements_embedding.embedding.weight
+
+    def context_and_head(self, sequence):
+        """(context (N, 2H), W_eff (|V|, 2H)) with forward(sequence) == context . W_eff^T (no softmax head): the
+        single-target cross-entropy then runs on the fused logits kernels without the (N, |V|) scores"""
+        decoder = self._projection_layer.decoder
+        if not isinstance(decoder.activation, nn.Identity):
+            return None
+        return self.encode(sequence), decoder.item_weight()
+
+    def catalog_query(self, sequence):
+        cw = self.context_and_head(sequence)
+        return None if cw is None else (cw[0], cw[1], None)

@@ -242,6 +242,19 @@ def _rows_cross_entropy(model, sequence, rows, targets, pad: int) -> torch.Tenso
     return ops.cross_entropy(model.forward_rows(sequence, rows), targets, pad)
 
 
+def _single_target_cross_entropy(model, sequence, targets, pad: int) -> torch.Tensor:
+    """SingleTargetCrossEntropyLoss(context . W^T) for a bilinear head (NARM, losses.py:77-115 + narm/layers.py:
+    93-120): the fused logits + cross-entropy kernels where the width fits them, else logits on the Linear kernel
+    followed by the cross-entropy kernel."""
+    cw = model.context_and_head(sequence)
+    if cw is None:
+        return ops.cross_entropy(model(sequence), targets, pad)
+    context, weight = cw
+    if FUSED_XENT and ops.linear_xent_ok(context, weight):
+        return ops.linear_cross_entropy(context, weight, None, targets, pad)
+    return ops.cross_entropy(ops.logits(context, weight), targets, pad)
+
+
 class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
     def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
                  beta_2: float = 0.998, weight_decay: float = 0, loss_function=None, table_grad: Optional[str] = None):
@@ -267,6 +280,9 @@ class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
             rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)
             loss = _rows_cross_entropy(self.model, build_model_input(self.model, self.item_tokenizer, batch), rows,
                                        target.reshape(-1).index_select(0, rows), pad)
+        elif ce_loss and target.dim() == 1 and hasattr(self.model, "context_and_head"):
+            loss = _single_target_cross_entropy(self.model, build_model_input(self.model, self.item_tokenizer, batch),
+                                                target, pad)
         else:
             loss = self.loss_function(target, self(batch, batch_idx))
         self.log(LOG_KEY_TRAINING_LOSS, loss)

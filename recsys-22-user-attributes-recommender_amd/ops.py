@@ -595,6 +595,133 @@ def dropout(x, p: float):
     return _DropoutFn.apply(x, p) if p > 0.0 else x
 
 
+class _DropoutRowsFn(torch.autograd.Function):
+    """nn.Dropout2d in training mode on (N, C, L): whole rows of L values dropped together (asme_dropout_rows)"""
+
+    @staticmethod
+    def forward(ctx, x, p: float):
+        xc = _f32(x)
+        seed = new_seed(p)
+        y = torch.empty_like(xc)
+        call("asme_dropout_rows", ptr(xc), xc.numel(), xc.shape[-1], p, seed, ptr(y), stream())
+        ctx.meta = (p, seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed = ctx.meta
+        g = _f32(dy)
+        dx = torch.empty_like(g)
+        call("asme_dropout_rows", ptr(g), g.numel(), g.shape[-1], p, seed, ptr(dx), stream())
+        return dx, None
+
+
+def dropout_rows(x, p: float):
+    """Dropout2d semantics for a 3-D (N, C, L) input (torch 1.11 and 2.10 alike): one draw per (n, c) row"""
+    return _DropoutRowsFn.apply(x, p) if p > 0.0 else x
+
+
+# ------------------------------------------------------------------------------------ NARM encoders
+def _pad_hidden(t: torch.Tensor, H: int, hp: int, cols: bool = False) -> torch.Tensor:
+    """(3H, K) / (3H,) gate-stacked GRU parameter -> (3hp, K') with each gate block zero-padded to hp rows
+    (and, cols=True, the K = H columns to hp); differentiable, a no-op when H == hp"""
+    if hp == H:
+        return t
+    g = t.reshape(3, H, -1)
+    g = torch.nn.functional.pad(g, (0, hp - H if cols else 0, 0, hp - H))
+    return g.reshape(3 * hp, -1) if t.dim() == 2 else g.reshape(3 * hp)
+
+
+class _GRULayerFn(torch.autograd.Function):
+    """One nn.GRU layer (batch_first, h_0 = 0) on the hand kernels (core/models/narm/components.py:32-56): the input
+    half x W_ih^T + b_ih for all steps as one Linear GEMM, the recurrence on asme_gru_fwd; backward through time on
+    asme_gru_bwd, then dX, dW_ih, db_ih, dW_hh, db_hh as Linear / weight-gradient GEMMs over all steps.  Parameters
+    arrive padded to hp hidden units (zero rows / columns), x (B, L, K) with K the padded width of the layer below."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, b_ih, w_hh, b_hh):
+        B, L, K = x.shape
+        hp = w_hh.shape[1]
+        x2 = _f32(x).reshape(B * L, K)
+        w_hh = _f32(w_hh)
+        gx = _linear_fwd(x2, _f32(w_ih), _f32(b_ih))
+        hout = torch.empty(B, L, hp, device=x.device, dtype=torch.float32)
+        gates = torch.empty(B, L, 4, hp, device=x.device, dtype=torch.float32)
+        call("asme_gru_fwd", ptr(gx), ptr(w_hh), ptr(_f32(b_hh)), None, B, L, hp, ptr(hout), ptr(gates), stream())
+        ctx.save_for_backward(x2, w_ih, w_hh, hout, gates)
+        ctx.shape = (B, L, K)
+        return hout
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, w_ih, w_hh, hout, gates = ctx.saved_tensors
+        B, L, K = ctx.shape
+        hp = w_hh.shape[1]
+        dgx = torch.empty(B * L, 3 * hp, device=dh.device, dtype=torch.float32)
+        dgh = torch.empty_like(dgx)
+        call("asme_gru_bwd", ptr(_f32(dh)), None, ptr(w_hh), None, ptr(hout), ptr(gates), B, L, hp, ptr(dgx),
+             ptr(dgh), None, stream())
+        dx = _linear_dx(dgx, _f32(w_ih)).view(B, L, K) if ctx.needs_input_grad[0] else None
+        dw_ih, db_ih = _weight_grad(dgx, x2, True)
+        hprev = torch.cat([hout.new_zeros(B, 1, hp), hout[:, :-1]], dim=1).reshape(B * L, hp)
+        dw_hh, db_hh = _weight_grad(dgh, hprev, True)
+        return dx, dw_ih, db_ih, dw_hh, db_hh
+
+
+def gru(x: torch.Tensor, module: torch.nn.GRU) -> torch.Tensor:
+    """outputs h_i (B, L, H) of the last layer of a batch_first, unidirectional nn.GRU run from h_0 = 0 over the
+    padded batch (causal: identical to the packed run at every valid position)"""
+    if not module.batch_first or module.bidirectional or module.proj_size or (module.dropout and module.training
+                                                                              and module.num_layers > 1):
+        raise NotImplementedError("asme gru: batch_first, unidirectional, no projection, no inter-layer dropout")
+    H = module.hidden_size
+    hp = -(-H // 16) * 16
+    if hp > 128:
+        raise NotImplementedError(f"asme gru: hidden size {H} > 128")
+    h = x
+    for k in range(module.num_layers):
+        w_ih = getattr(module, f"weight_ih_l{k}")
+        w_hh = getattr(module, f"weight_hh_l{k}")
+        b_ih = getattr(module, f"bias_ih_l{k}") if module.bias else w_ih.new_zeros(3 * H)
+        b_hh = getattr(module, f"bias_hh_l{k}") if module.bias else w_hh.new_zeros(3 * H)
+        h = _GRULayerFn.apply(h, _pad_hidden(w_ih, H, hp, cols=k > 0), _pad_hidden(b_ih, H, hp),
+                              _pad_hidden(w_hh, H, hp, cols=True), _pad_hidden(b_hh, H, hp))
+    return h if hp == H else h[..., :H].contiguous()
+
+
+class _NarmAttendFn(torch.autograd.Function):
+    """LocalEncoderLayer's v . sigmoid(A1 c_g + A2 h_i) attention and masked weighted sum (core/models/narm/
+    layers.py:32-66) after the two projections, on asme_narm_attend_fwd / _bwd"""
+
+    @staticmethod
+    def forward(ctx, p1, p2, v, hs, mask):
+        N, S, H = hs.shape
+        p1, p2, v, hs = _f32(p1), _f32(p2), _f32(v), _f32(hs)
+        m = mask.to(torch.uint8).contiguous()
+        out = torch.empty(N, H, device=hs.device, dtype=torch.float32)
+        alpha = torch.empty(N, S, device=hs.device, dtype=torch.float32)
+        call("asme_narm_attend_fwd", ptr(p1), ptr(p2), ptr(v), ptr(hs), ptr(m), N, S, H, ptr(out), ptr(alpha),
+             stream())
+        ctx.save_for_backward(p1, p2, v, hs, m, alpha)
+        return out
+
+    @staticmethod
+    def backward(ctx, dc):
+        p1, p2, v, hs, m, alpha = ctx.saved_tensors
+        N, S, H = hs.shape
+        dp1 = torch.empty_like(p1)
+        dp2 = torch.empty_like(p2)
+        dhs = torch.empty_like(hs)
+        dv_part = torch.empty(N, H, device=hs.device, dtype=torch.float32)
+        call("asme_narm_attend_bwd", ptr(_f32(dc)), ptr(p1), ptr(p2), ptr(v), ptr(hs), ptr(m), ptr(alpha), N, S, H,
+             ptr(dp1), ptr(dp2), ptr(dhs), ptr(dv_part), stream())
+        return dp1, dp2, _reduce_rows(dv_part), dhs, None
+
+
+def narm_attend(p1, p2, v, hs, mask):
+    return _NarmAttendFn.apply(p1, p2, v, hs, mask)
+
+
 # ------------------------------------------------------------------------------------ layer norm
 class _LayerNormFn(torch.autograd.Function):
     """nn.LayerNorm over the last dim (fp32, biased variance)."""
@@ -949,11 +1076,11 @@ class _LogitsFn(torch.autograd.Function):
 
 
 def logits(hidden, weight, bias=None):
-    """full-catalogue scores hidden . weight^T (+ bias) on the bf16x6 logits kernel (library GEMM only for widths
-    it does not take)"""
+    """full-catalogue scores hidden . weight^T (+ bias) on the bf16x6 logits kernel; widths above 128 (NARM's
+    2H = 256) on the fp32-MFMA Linear kernel"""
     if linear_xent_ok(hidden, weight) and hidden.is_cuda:
         return _LogitsFn.apply(hidden, weight, bias)
-    return torch.nn.functional.linear(hidden, weight, bias)
+    return linear(hidden, weight, bias)
 
 
 class _LinearXentFn(torch.autograd.Function):
