@@ -62,9 +62,10 @@ def parse():
     ap.add_argument("--ids", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--kernel-events", choices=["on", "off"], default="on",
                     help="HIP events around the timed kernels (off: no per-kernel rooflines; for A/B of their cost)")
-    ap.add_argument("--producer", choices=["resident", "gpu"], default="resident",
-                    help="resident: two pre-built device batches; gpu: every step samples its batch from sessions "
-                         "in HBM with the GPU pos/neg sampler (asme_posneg_sample) inside the timed step")
+    ap.add_argument("--producer", choices=["resident", "gpu"], default="gpu",
+                    help="gpu (default): every step samples a fresh batch from sessions in HBM with the GPU pos/neg "
+                         "sampler (asme_posneg_sample) inside the timed step; resident: two pre-built device batches "
+                         "alternating (rows touched one or two steps earlier: less lazy catch-up per step)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -347,7 +348,8 @@ def main():
     timer = asme._lib.KernelTimer([] if args.kernel_events == "off" else [
                                    "asme_adam_rows_step", "asme_attention_fwd", "asme_attention_bwd",
                                    "asme_embedding_fwd", "asme_embedding_bwd", "asme_lazy_adam_catch_up",
-                                   "asme_lazy_adam_apply", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
+                                   "asme_lazy_adam_apply", "asme_lazy_adam_stage", "asme_lazy_adam_apply_staged",
+                                   "asme_sampled_logits_fwd", "asme_sampled_logits_bwd", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
                                    "asme_ws_linear", "asme_posneg_sample"])
     if world > 1:
@@ -408,6 +410,13 @@ def main():
         "asme_embedding_bwd": ("hbm", T * 8 + 3 * T * d * 4 + T * 16),
         "asme_lazy_adam_apply": ("hbm", U * 8 + U * d * 4 + 6 * U * d * 4 + U * 4),
         "asme_lazy_adam_catch_up": ("hbm", U * 8 + 6 * U * d * 4 + 2 * U * 4),
+        # staged form: the same rows read (random) and written to the compact staging rows (slot order); the apply
+        # reads those + the compact gradient (slot order) and writes the table rows (random) + last_step
+        "asme_lazy_adam_stage": ("hbm", U * 8 + U * 4 + 6 * U * d * 4),
+        "asme_lazy_adam_apply_staged": ("hbm", U * 8 + U * d * 4 + 6 * U * d * 4 + U * 4),
+        # sampled head: h read once, pos and neg rows gathered, two logits written (fwd); + dh written (bwd)
+        "asme_sampled_logits_fwd": ("hbm", T * d * 4 + 2 * T * 8 + 2 * T * d * 4 + 2 * T * 4),
+        "asme_sampled_logits_bwd": ("hbm", T * d * 4 + 2 * T * 8 + 2 * T * d * 4 + 2 * T * 4 + T * d * 4),
         "asme_gelu_dropout_bwd": ("hbm", 3 * T * ffn * 4),
         "asme_adam_rows_step": ("hbm", 6 * V * d * 4 + V * 4 + U * d * 4),
         # session items read once + x / pos / neg written (the in-session membership scans hit the cache)
@@ -443,7 +452,9 @@ def main():
         "metric": "training sequences/sec at B=1024 L=200 |I|=10M (SASRec-neg, fwd+bwd+Adam)",
         "value": round(value, 2), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (uniform ids, random-init weights)",
+        "vs_baseline": None, "dtype": "fp32", "data": ("synthetic sessions (uniform ids), a fresh GPU-sampled batch every step, random-init weights"
+                                                 if args.producer == "gpu" else
+                                                 "synthetic (uniform ids, two resident batches), random-init weights"),
         "config": {"workload": "sasrec-neg train step", "model": "SASRec", "global_batch": B * world,
                    "batch_per_gpu": B, "seq_len": L, "items": args.items, "dim": d, "heads": args.heads,
                    "layers": args.layers, "dropout": args.dropout, "table_grad": args.table_grad,

@@ -207,6 +207,22 @@ int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, int64_t c
 int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap, const float* grad_rows,
                          int32_t* last_step, float* param, float* exp_avg, float* exp_avg_sq, int64_t dim,
                          const float* hist, int64_t hist_rows, int64_t step, void* stream);
+/* Staged form of catch-up + apply (dim 32/64/128/256, 16-B aligned rows): asme_lazy_adam_stage writes rows[s]
+ * brought up to `upto` into staged_*[s] (slot order) WITHOUT touching the table or last_step -- the step's
+ * readers gather staged_param[inverse[t]] (near-sequential) instead of random table rows;
+ * asme_lazy_adam_apply_staged then steps `step` from staged_*[s] with grad_rows[s] into the table rows and
+ * sets last_step.  Same per-element operations as catch_up + apply, so the same bits
+ * (replaces the per-step torch.optim.Adam update of nn.Embedding.weight). */
+int asme_lazy_adam_stage_supported(int64_t dim);
+int asme_lazy_adam_stage(const int64_t* rows, const int32_t* count, int64_t cap, const int32_t* last_step,
+                         const float* param, const float* exp_avg, const float* exp_avg_sq, int64_t dim,
+                         const float* hist, int64_t hist_rows, int64_t upto, float* staged_param,
+                         float* staged_exp_avg, float* staged_exp_avg_sq, void* stream);
+int asme_lazy_adam_apply_staged(const int64_t* rows, const int32_t* count, int64_t cap, const float* grad_rows,
+                                const float* staged_param, const float* staged_exp_avg,
+                                const float* staged_exp_avg_sq, int32_t* last_step, float* param, float* exp_avg,
+                                float* exp_avg_sq, int64_t dim, const float* hist, int64_t hist_rows, int64_t step,
+                                void* stream);
 
 /* ---- input producers: sessions in HBM as flat item ids + offsets (n_sessions + 1) ---------
  * asme_session_batch: collate (data/collate.py:42-111): out (batch, seq_len) = the last min(len - drop_last,

@@ -79,6 +79,9 @@ SIGNATURES = {
     "asme_lazy_adam_record_step": [p, i64, i64, f32, f32, f32, f32, f32, p],
     "asme_lazy_adam_catch_up": [p, p, i64, p, p, p, p, i64, p, i64, i64, p],
     "asme_lazy_adam_apply": [p, p, i64, p, p, p, p, p, i64, p, i64, i64, p],
+    "asme_lazy_adam_stage_supported": [i64],
+    "asme_lazy_adam_stage": [p, p, i64, p, p, p, p, i64, p, i64, i64, p, p, p, p],
+    "asme_lazy_adam_apply_staged": [p, p, i64, p, p, p, p, p, p, p, p, i64, p, i64, i64, p],
     "asme_linear_weight_grad_workspace": [i64, i64, i64],
     "asme_linear_weight_grad": [p, i64, p, i64, i64, i64, i64, p, i64, p, p, i32, p],
     "asme_dedup_workspace_bytes": [i64],

@@ -368,6 +368,81 @@ __global__ __launch_bounds__(256) void lazy_apply_v4_kernel(const int64_t* __res
     if (lane % LPR == 0) last_step[r] = step;
 }
 
+// Staged variant (the step's unique rows read in slot order afterwards).  stage: slot s gets rows[s] brought up
+// to `upto` into the compact buffers sp/sm/sv[s] -- the table and last_step are NOT written, so a step that
+// never reaches the optimizer leaves the lazy state untouched; the row reads are random, the writes stream in
+// slot order.  Every reader of the step's rows (embedding gather, sampled head, their backwards) then reads
+// sp[inverse[t]], i.e. nearly in token order.  apply_staged: the real-gradient step from the staged values
+// (streamed) into the table rows (random writes) and last_step = step.
+template <int LPR>
+__global__ __launch_bounds__(256) void lazy_stage_v4_kernel(const int64_t* __restrict__ rows,
+                                                            const int32_t* __restrict__ count, int64_t cap,
+                                                            const int32_t* __restrict__ last_step,
+                                                            const float* __restrict__ p, const float* __restrict__ m,
+                                                            const float* __restrict__ v,
+                                                            const AdamHyper* __restrict__ hist, int32_t upto,
+                                                            float* __restrict__ sp, float* __restrict__ sm,
+                                                            float* __restrict__ sv) {
+    constexpr int D = LPR * 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LPR) + lane / LPR;
+    const int64_t n = (int64_t)*count;
+    const bool in_range = s < n && s < cap;
+    const int64_t r = in_range ? rows[s] : 0;
+    const int64_t off = r * D + (lane % LPR) * 4;
+    // the row loads do not wait for last_step
+    float4 P = make_float4(0.f, 0.f, 0.f, 0.f), M = P, Vv = P;
+    if (in_range) {
+        P = *reinterpret_cast<const float4*>(p + off);
+        M = *reinterpret_cast<const float4*>(m + off);
+        Vv = *reinterpret_cast<const float4*>(v + off);
+    }
+    const int32_t t0 = in_range ? last_step[r] : upto;
+    int32_t t_lo = t0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t_lo = min(t_lo, __shfl_xor(t_lo, o, 64));
+    t_lo = __builtin_amdgcn_readfirstlane(t_lo);
+    if (t_lo < upto) {  // wave-uniform; same replay as lazy_catch_up_v4_kernel
+        AdamHyper next = hist[t_lo + 1];
+        for (int32_t t = t_lo + 1; t <= upto; ++t) {
+            const AdamHyper hp = next;
+            next = hist[min(t + 1, upto)];
+            if (t > t0) adam_zero_grad_step4(P, M, Vv, hp);
+        }
+    }
+    if (!in_range) return;
+    const int64_t so = s * D + (lane % LPR) * 4;
+    *reinterpret_cast<float4*>(sp + so) = P;
+    *reinterpret_cast<float4*>(sm + so) = M;
+    *reinterpret_cast<float4*>(sv + so) = Vv;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void lazy_apply_staged_v4_kernel(
+    const int64_t* __restrict__ rows, const int32_t* __restrict__ count, int64_t cap,
+    const float* __restrict__ grad_rows, const float* __restrict__ sp, const float* __restrict__ sm,
+    const float* __restrict__ sv, int32_t* __restrict__ last_step, float* __restrict__ p, float* __restrict__ m,
+    float* __restrict__ v, const AdamHyper* __restrict__ hist, int32_t step) {
+    constexpr int D = LPR * 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LPR) + lane / LPR;
+    if (s >= cap || s >= (int64_t)*count) return;
+    const int c = (lane % LPR) * 4;
+    const int64_t so = s * D + c;
+    float4 P = *reinterpret_cast<const float4*>(sp + so);
+    float4 M = *reinterpret_cast<const float4*>(sm + so);
+    float4 Vv = *reinterpret_cast<const float4*>(sv + so);
+    const float4 G = *reinterpret_cast<const float4*>(grad_rows + so);
+    const int64_t r = rows[s];
+    const AdamHyper hp = hist[step];
+    adam_elem4(P, G, M, Vv, hp);
+    const int64_t off = r * D + c;
+    *reinterpret_cast<float4*>(p + off) = P;
+    *reinterpret_cast<float4*>(m + off) = M;
+    *reinterpret_cast<float4*>(v + off) = Vv;
+    if (lane % LPR == 0) last_step[r] = step;
+}
+
 #define ASME_LPR_DISPATCH(DIM, ...)                                             \
     switch (DIM) {                                                              \
         case 32: { constexpr int LPR = 8; __VA_ARGS__; } break;                 \
@@ -456,6 +531,52 @@ ASME_API int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, 
                                          count, cap, last_step, param, exp_avg, exp_avg_sq, (int)dim,
                                          reinterpret_cast<const AdamHyper*>(hist), (int32_t)upto));
     ASME_LAUNCH_CHECK("asme_lazy_adam_catch_up");
+}
+
+ASME_API int asme_lazy_adam_stage_supported(int64_t dim) {
+    return dim == 32 || dim == 64 || dim == 128 || dim == 256;
+}
+
+ASME_API int asme_lazy_adam_stage(const int64_t* rows, const int32_t* count, int64_t cap, const int32_t* last_step,
+                                  const float* param, const float* exp_avg, const float* exp_avg_sq, int64_t dim,
+                                  const float* hist, int64_t hist_rows, int64_t upto, float* staged_param,
+                                  float* staged_exp_avg, float* staged_exp_avg_sq, void* stream) {
+    ASME_CHECK_ARG(rows && count && last_step && param && exp_avg && exp_avg_sq && hist && staged_param &&
+                       staged_exp_avg && staged_exp_avg_sq, "asme_lazy_adam_stage: null pointer");
+    ASME_CHECK_ARG(upto >= 0 && upto < hist_rows && upto < (1LL << 31), "asme_lazy_adam_stage: step beyond the history");
+    ASME_CHECK_ARG(asme_lazy_adam_stage_supported(dim) && v4_ok(dim, param, exp_avg, exp_avg_sq) &&
+                       v4_ok(dim, staged_param, staged_exp_avg, staged_exp_avg_sq),
+                   "asme_lazy_adam_stage: dim must be 32/64/128/256 and every row pointer 16-B aligned");
+    if (cap == 0) return 0;
+    const int64_t rows_per_block = 4 * (256 / dim);
+    const dim3 g4((unsigned)((cap + rows_per_block - 1) / rows_per_block));
+    ASME_LPR_DISPATCH(dim, hipLaunchKernelGGL(lazy_stage_v4_kernel<LPR>, g4, dim3(256), 0, (hipStream_t)stream, rows,
+                                              count, cap, last_step, param, exp_avg, exp_avg_sq,
+                                              reinterpret_cast<const AdamHyper*>(hist), (int32_t)upto, staged_param,
+                                              staged_exp_avg, staged_exp_avg_sq));
+    ASME_LAUNCH_CHECK("asme_lazy_adam_stage");
+}
+
+ASME_API int asme_lazy_adam_apply_staged(const int64_t* rows, const int32_t* count, int64_t cap,
+                                         const float* grad_rows, const float* staged_param,
+                                         const float* staged_exp_avg, const float* staged_exp_avg_sq,
+                                         int32_t* last_step, float* param, float* exp_avg, float* exp_avg_sq,
+                                         int64_t dim, const float* hist, int64_t hist_rows, int64_t step,
+                                         void* stream) {
+    ASME_CHECK_ARG(rows && count && grad_rows && staged_param && staged_exp_avg && staged_exp_avg_sq && last_step &&
+                       param && exp_avg && exp_avg_sq && hist, "asme_lazy_adam_apply_staged: null pointer");
+    ASME_CHECK_ARG(step >= 1 && step < hist_rows, "asme_lazy_adam_apply_staged: step beyond the history");
+    ASME_CHECK_ARG(asme_lazy_adam_stage_supported(dim) && v4_ok(dim, param, exp_avg, exp_avg_sq) &&
+                       v4_ok(dim, staged_param, staged_exp_avg, staged_exp_avg_sq) && ((uintptr_t)grad_rows & 15) == 0,
+                   "asme_lazy_adam_apply_staged: dim must be 32/64/128/256 and every row pointer 16-B aligned");
+    if (cap == 0) return 0;
+    const int64_t rows_per_block = 4 * (256 / dim);
+    const dim3 g4((unsigned)((cap + rows_per_block - 1) / rows_per_block));
+    ASME_LPR_DISPATCH(dim, hipLaunchKernelGGL(lazy_apply_staged_v4_kernel<LPR>, g4, dim3(256), 0, (hipStream_t)stream,
+                                              rows, count, cap, grad_rows, staged_param, staged_exp_avg,
+                                              staged_exp_avg_sq, last_step, param, exp_avg, exp_avg_sq,
+                                              reinterpret_cast<const AdamHyper*>(hist), (int32_t)step));
+    ASME_LAUNCH_CHECK("asme_lazy_adam_apply_staged");
 }
 
 ASME_API int asme_lazy_adam_apply(const int64_t* rows, const int32_t* count, int64_t cap, const float* grad_rows,

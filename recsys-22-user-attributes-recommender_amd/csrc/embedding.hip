@@ -11,6 +11,7 @@
 // Layout: table (V, D) fp32 row-major; tokens t = b*L + s; activations (T, D) fp32.
 // One 64-lane wave owns one token row; lane l holds elements l + 64*j (coalesced 256-B segments).
 #include "rows.h"
+#include <algorithm>
 
 using namespace asme;
 
@@ -297,8 +298,16 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
     }
 }
 
+#ifndef ASME_EMB_BWD_WPE
+#define ASME_EMB_BWD_WPE 0
+#endif
+#if ASME_EMB_BWD_WPE
+#define ASME_EMB_BWD_ATTR __attribute__((amdgpu_waves_per_eu(ASME_EMB_BWD_WPE, 8)))
+#else
+#define ASME_EMB_BWD_ATTR
+#endif
 template <class R, int kPass>  // kPass: tokens per lane group per grid-stride pass
-__global__ __launch_bounds__(256) void emb_bwd4_kernel(
+__global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1,
     const float* __restrict__ extra, const float* __restrict__ w2, float p2, uint64_t seed,
@@ -573,6 +582,27 @@ inline int vpl_of(int64_t D) { return (int)((D + 63) / 64); }
 
 }  // namespace
 
+// Row layout of the embedding kernels: at D = 128 a row is 16 lanes x two float4 (4 rows per wave) rather than the
+// shared 32 x one float4, so every LayerNorm statistic reduces inside a 16-lane DPP row (no permlane step) and a
+// wave has twice the tokens in flight.
+#ifndef ASME_EMB_LPR16
+#define ASME_EMB_LPR16 1
+#endif
+#ifndef ASME_EMB_BWD_LPR16
+#define ASME_EMB_BWD_LPR16 1
+#endif
+#ifndef ASME_EMB_K
+#define ASME_EMB_K 2
+#endif
+template <class F>
+int with_emb_layout(int64_t D, F&& f, bool lpr16 = ASME_EMB_LPR16) {
+    if (lpr16 && D == 128) {
+        f(RowLayout<4, 16, 2>{});
+        return 0;
+    }
+    return with_row_layout(D, f);
+}
+
 ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
                                 int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
                                 const float* ln1_b, float ln1_eps, float p1, uint64_t seed1, const float* extra,
@@ -582,10 +612,10 @@ ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t se
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && seq_len >= 1 && n_tokens >= 0, "asme_embedding_fwd: bad shape");
     ASME_CHECK_ARG(p1 >= 0.f && p1 < 1.f && p2 >= 0.f && p2 < 1.f, "asme_embedding_fwd: dropout p must be in [0,1)");
     if (n_tokens == 0) return 0;
-    if (with_row_layout(dim, [&](auto layout) {
+    if (with_emb_layout(dim, [&](auto layout) {
             using R = decltype(layout);
             if constexpr (R::W == 4) {
-                constexpr int K = 2;  // measured at the bench shape: K = 1/2/4/8 -> 75/68/72/88 us (p = 0.2)
+                constexpr int K = ASME_EMB_K;  // tokens per lane group
                 const int64_t rows = (int64_t)kWavesPerBlock * R::RPW * K;
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K>), dim3((unsigned)((n_tokens + rows - 1) / rows)),
                                    dim3(256), 0, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim,
@@ -616,7 +646,7 @@ ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t se
     ASME_CHECK_ARG(!partials || n_partials >= 1, "asme_embedding_bwd: n_partials must be >= 1");
     if (n_tokens == 0) return 0;
     const size_t lds = partials ? (size_t)kWavesPerBlock * 4 * dim * sizeof(float) : 0;
-    if (with_row_layout(dim, [&](auto layout) {
+    if (with_emb_layout(dim, [&](auto layout) {
             using R = decltype(layout);
             const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
             // grid-stride with one partial row per block when the LN parameter grads are wanted
@@ -633,7 +663,7 @@ ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t se
                                    n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1, seed1,
                                    extra, ln2_w, p2, seed2, dout, stats, d_rows, d_extra, partials);
             }
-        }))
+        }, ASME_EMB_BWD_LPR16))
         return -1;
     ASME_LAUNCH_CHECK("asme_embedding_bwd");
 }

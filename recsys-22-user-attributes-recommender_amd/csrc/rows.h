@@ -21,10 +21,35 @@ struct RowLayout {
 template <class R>
 using RowVals = float[R::NV][R::W];
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// v(row r) + v(row r ^ 1) for 16-lane rows (v_permlane16_swap_b32) / v(half h) + v(half h ^ 1) for the two 32-lane
+// halves (v_permlane32_swap_b32): VALU lane swaps of gfx950, same operand order in every lane
+__device__ __forceinline__ float swap16_sum(float v) {
+    const int i = __builtin_bit_cast(int, v);
+    const auto r = __builtin_amdgcn_permlane16_swap(i, i, false, false);
+    return __builtin_bit_cast(float, (int)r[0]) + __builtin_bit_cast(float, (int)r[1]);
+}
+__device__ __forceinline__ float swap32_sum(float v) {
+    const int i = __builtin_bit_cast(int, v);
+    const auto r = __builtin_amdgcn_permlane32_swap(i, i, false, false);
+    return __builtin_bit_cast(float, (int)r[0]) + __builtin_bit_cast(float, (int)r[1]);
+}
+
+// Sum over the LPR-lane group, every lane gets the total.  No LDS-pipe shuffles (ds_bpermute: ~100-cycle latency
+// each, 5 dependent ones per LayerNorm statistic at LPR = 32): DPP quad permutes for lane distance 1 and 2, then
+// row_half_mirror / row_mirror (lanes of a group already agree on the partial sums, so a mirror pairs the same
+// values as an xor), then the permlane swaps across 16-lane rows and wave halves.
 template <int LPR>
 __device__ __forceinline__ float row_sum(float v) {
-#pragma unroll
-    for (int o = LPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if constexpr (LPR >= 2) v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+    if constexpr (LPR >= 4) v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+    if constexpr (LPR >= 8) v += dpp_mov<0x141>(v);   // row_half_mirror
+    if constexpr (LPR >= 16) v += dpp_mov<0x140>(v);  // row_mirror
+    if constexpr (LPR >= 32) v = swap16_sum(v);
+    if constexpr (LPR >= 64) v = swap32_sum(v);
     return v;
 }
 // sum over the rows sharing a wave (lanes with equal lane % LPR)

@@ -21,6 +21,10 @@ from ._lib import call, ptr, stream
 
 ctypes_i64, ctypes_vp = ctypes.c_int64, ctypes.c_void_p
 _N_PARTIALS = 1024  # blocks (and partial rows) used by the grid-stride backward reductions
+_EMB_PARTIALS = 2048  # the embedding backward's (2x the waves in flight: 124 -> 102 us at the bench shape)
+# lazy table Adam: stage the step's unique rows (asme_lazy_adam_stage) so every reader gathers them in slot order
+# (True), or catch them up in place in the table and gather by id (False; the A/B switch)
+STAGE_ROWS = True
 
 
 def new_seed(p: float) -> int:
@@ -98,8 +102,30 @@ class LazyTableState:
         call("asme_lazy_adam_catch_up", ptr(rows), ptr(count), cap, ptr(self.last_step), ptr(self.param),
              ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist), self.hist.shape[0], self.step, stream())
 
+    def stage_ok(self) -> bool:
+        D = self.param.shape[1]
+        return STAGE_ROWS and bool(_lib.load().asme_lazy_adam_stage_supported(D)) and all(
+            t.data_ptr() % 16 == 0 for t in (self.param, self.exp_avg, self.exp_avg_sq))
+
+    def stage(self, rows: torch.Tensor, count: torch.Tensor, cap: int) -> torch.Tensor:
+        """(3, cap, d): param / exp_avg / exp_avg_sq of rows[s] brought up to the current step, in slot order;
+        the table itself is not written (asme_lazy_adam_stage)"""
+        D = self.param.shape[1]
+        out = torch.empty(3, max(cap, 1), D, device=self.param.device, dtype=torch.float32)
+        call("asme_lazy_adam_stage", ptr(rows), ptr(count), cap, ptr(self.last_step), ptr(self.param),
+             ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist), self.hist.shape[0], self.step, ptr(out[0]),
+             ptr(out[1]), ptr(out[2]), stream())
+        return out
+
     def apply(self, plan: "SparseTablePlan", step: int):
         D = self.param.shape[1]
+        if plan.staged is not None:
+            st = plan.staged
+            call("asme_lazy_adam_apply_staged", ptr(plan.unique), ptr(plan.count), plan.capacity, ptr(plan.grad_rows),
+                 ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(self.last_step), ptr(self.param), ptr(self.exp_avg),
+                 ptr(self.exp_avg_sq), D, ptr(self.hist), self.hist.shape[0], step, stream())
+            plan.staged = None  # the staged values are one step old now (a re-apply catches up from the table)
+            return
         call("asme_lazy_adam_apply", ptr(plan.unique), ptr(plan.count), plan.capacity, ptr(plan.grad_rows),
              ptr(self.last_step), ptr(self.param), ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist),
              self.hist.shape[0], step, stream())
@@ -145,9 +171,25 @@ class SparseTablePlan:
             self._offset[key] = off
             off += k
         self.consumed = False
+        # (3, capacity, d) param / moments of unique[s] brought up to date, or None: the step's readers take
+        # `rows` + `gather_ids(ids)` instead of the table (see LazyTableState.stage)
+        self.staged: Optional[torch.Tensor] = None
         if tg is not None and tg.lazy is not None:
             # rows gathered by this step's forward must carry every earlier (zero-gradient) update
-            tg.lazy.catch_up(self.unique, self.count, self.capacity)
+            if tg.lazy.stage_ok():
+                self.staged = tg.lazy.stage(self.unique, self.count, self.capacity)
+            else:
+                tg.lazy.catch_up(self.unique, self.count, self.capacity)
+
+    def gather_source(self, table: torch.Tensor, ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(rows, row ids) a reader of `ids` gathers from: the staged rows by slot when this step staged them,
+        else the table itself by id"""
+        if self.staged is not None and self.has(ids):
+            return self.staged[0], self.inverse_of(ids)
+        return table, ids
+
+    def has(self, ids: torch.Tensor) -> bool:
+        return (ids.data_ptr(), tuple(ids.shape)) in self._inverse
 
     @classmethod
     def identity(cls, n_rows: int, id_sets: Sequence[torch.Tensor], dim: int) -> "SparseTablePlan":
@@ -169,6 +211,7 @@ class SparseTablePlan:
         self._grad_rows = None
         self._inverse, self._offset, self._contrib = {}, {}, []
         self._flat_inverse = flat
+        self.staged = None
         off = 0
         for x in id_sets:
             key = (x.data_ptr(), tuple(x.shape))
@@ -282,7 +325,11 @@ class _EmbeddingFn(torch.autograd.Function):
     def forward(ctx, ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, spec: EmbeddingSpec):
         ids = _i64(ids)
         T = ids.numel()
-        V, D = table.shape
+        D = table.shape[1]
+        # rows staged in slot order by this step's lazy Adam (SparseTablePlan.gather_source), else the table
+        plan = spec.table_grad.plan if spec.table_grad is not None else None
+        src, src_ids = plan.gather_source(table, ids) if plan is not None else (table, ids)
+        V = src.shape[0]
         out = torch.empty(T, D, device=table.device, dtype=torch.float32)
         stats = torch.empty(T, 4, device=table.device, dtype=torch.float32)
         s1, s2 = new_seed(spec.p1), new_seed(spec.p2)
@@ -290,36 +337,39 @@ class _EmbeddingFn(torch.autograd.Function):
         keep = None
         if (spec.p1 > 0 or spec.p2 > 0) and D % 4 == 0:  # dropout decisions, one byte per 4 elements
             keep = torch.empty(T, D // 4, device=table.device, dtype=torch.uint8)
-        call("asme_embedding_fwd", ptr(ids), T, spec.seq_len, ptr(table), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
+        call("asme_embedding_fwd", ptr(src_ids), T, spec.seq_len, ptr(src), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
              spec.ln1_eps, spec.p1, s1, ptr(extra_c), ptr(ln2_w), ptr(ln2_b), spec.ln2_eps, spec.p2, s2, ptr(out),
              ptr(stats), ptr(keep), None, stream())
-        ctx.save_for_backward(ids, table, pos, ln1_w, ln1_b, extra_c, ln2_w, stats, keep)
+        ctx.save_for_backward(ids, src_ids, src, pos, ln1_w, ln1_b, extra_c, ln2_w, stats, keep)
+        ctx.table_shape = tuple(table.shape)
         ctx.spec, ctx.seeds = spec, (s1, s2)
         ctx.has = (pos is not None, ln1_w is not None, extra is not None, ln2_w is not None)
         return out.view(*ids.shape, D)
 
     @staticmethod
     def backward(ctx, dout):
-        ids, table, pos, ln1_w, ln1_b, extra, ln2_w, stats, keep = ctx.saved_tensors
+        ids, src_ids, src, pos, ln1_w, ln1_b, extra, ln2_w, stats, keep = ctx.saved_tensors
         spec = ctx.spec
         s1, s2 = ctx.seeds
         T = ids.numel()
-        V, D = table.shape
+        V, D = ctx.table_shape
+        dev = src.device
         dout = _f32(dout).reshape(T, D)
-        d_rows = torch.empty(T, D, device=table.device, dtype=torch.float32)
-        d_extra = torch.empty(T, D, device=table.device, dtype=torch.float32) if ctx.has[2] else None
+        d_rows = torch.empty(T, D, device=dev, dtype=torch.float32)
+        d_extra = torch.empty(T, D, device=dev, dtype=torch.float32) if ctx.has[2] else None
         has_ln = ctx.has[1] or ctx.has[3]
-        part = torch.empty(_N_PARTIALS, 4 * D, device=table.device, dtype=torch.float32) if has_ln else None
-        call("asme_embedding_bwd", ptr(ids), T, spec.seq_len, ptr(table), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
+        part = torch.empty(_EMB_PARTIALS, 4 * D, device=dev, dtype=torch.float32) if has_ln else None
+        call("asme_embedding_bwd", ptr(src_ids), T, spec.seq_len, ptr(src), src.shape[0], D, ptr(pos), ptr(ln1_w),
+             ptr(ln1_b),
              spec.p1, s1, ptr(extra), ptr(ln2_w), spec.p2, s2, ptr(keep), ptr(dout), ptr(stats), ptr(d_rows),
-             ptr(d_extra), ptr(part), _N_PARTIALS, stream())
+             ptr(d_extra), ptr(part), _EMB_PARTIALS, stream())
         g_table = None
         if ctx.needs_input_grad[1]:
             plan = spec.table_grad.plan if spec.table_grad is not None else None
             if plan is not None:
                 plan.add_rows(ids, d_rows)
             else:
-                g_table = torch.zeros_like(table)
+                g_table = torch.zeros(V, D, device=dev, dtype=torch.float32)
                 call("asme_scatter_add_rows", ptr(d_rows), ptr(ids), T, D, ptr(g_table), V, 1.0, stream())
         g_pos = None
         if ctx.has[0] and ctx.needs_input_grad[2]:
@@ -327,7 +377,7 @@ class _EmbeddingFn(torch.autograd.Function):
             B = T // L
             g_pos = torch.zeros_like(pos)
             nch = max(1, min(32, B))
-            ws = torch.empty(nch, L, D, device=table.device, dtype=torch.float32)
+            ws = torch.empty(nch, L, D, device=dev, dtype=torch.float32)
             call("asme_position_grad", ptr(d_rows), B, L, D, ptr(ws), nch, ptr(g_pos), 0, stream())
         g = [None] * 4
         if has_ln:
@@ -928,22 +978,29 @@ class _SampledLogitsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, hidden, table, pos_ids, neg_ids, table_grad: Optional[TableGrad]):
         shape = pos_ids.shape
-        V, D = table.shape
+        D = table.shape[1]
         h2 = _f32(hidden).reshape(-1, D)
         pos_ids, neg_ids = _i64(pos_ids), _i64(neg_ids)
         T = h2.shape[0]
+        # the rows staged by this step's lazy Adam in slot order (SparseTablePlan.gather_source), else the table
+        plan = table_grad.plan if table_grad is not None else None
+        src, pos_src = plan.gather_source(table, pos_ids) if plan is not None else (table, pos_ids)
+        neg_src = plan.gather_source(table, neg_ids)[1] if plan is not None and src is not table else neg_ids
+        if src is not table and neg_src is neg_ids:
+            src, pos_src, neg_src = table, pos_ids, neg_ids  # both id sets must read the same rows
+        V = src.shape[0]
         po = torch.empty(T, device=hidden.device, dtype=torch.float32)
         no = torch.empty(T, device=hidden.device, dtype=torch.float32)
-        call("asme_sampled_logits_fwd", ptr(h2), ptr(table), ptr(pos_ids), ptr(neg_ids), T, D, V, ptr(po), ptr(no),
+        call("asme_sampled_logits_fwd", ptr(h2), ptr(src), ptr(pos_src), ptr(neg_src), T, D, V, ptr(po), ptr(no),
              stream())
-        ctx.save_for_backward(h2, table, pos_ids, neg_ids)
+        ctx.save_for_backward(h2, table, src, pos_ids, neg_ids, pos_src, neg_src)
         ctx.table_grad = table_grad
         ctx.hshape = hidden.shape
         return po.view(shape), no.view(shape)
 
     @staticmethod
     def backward(ctx, g_pos, g_neg):
-        h2, table, pos_ids, neg_ids = ctx.saved_tensors
+        h2, table, src, pos_ids, neg_ids, pos_src, neg_src = ctx.saved_tensors
         V, D = table.shape
         T = h2.shape[0]
         gp = torch.zeros(T, device=h2.device) if g_pos is None else _f32(g_pos).reshape(T)
@@ -952,9 +1009,9 @@ class _SampledLogitsFn(torch.autograd.Function):
         g_table = None
         plan = ctx.table_grad.plan if ctx.table_grad is not None else None
         if ctx.needs_input_grad[1] and plan is not None:
-            # dH pass with the real table; the table contributions go to the compact rows
-            call("asme_sampled_logits_bwd", ptr(h2), ptr(table), ptr(pos_ids), ptr(neg_ids), T, D, V, ptr(gp),
-                 ptr(gn), ptr(dh), None, stream())
+            # dH pass with the rows the forward read; the table contributions go to the compact rows
+            call("asme_sampled_logits_bwd", ptr(h2), ptr(src), ptr(pos_src), ptr(neg_src), T, D, src.shape[0],
+                 ptr(gp), ptr(gn), ptr(dh), None, stream())
             # table rows: g_pos[t] * h[t] / g_neg[t] * h[t], summed per unique row by the plan (deterministic)
             plan.add_scaled(pos_ids, gp, h2)
             plan.add_scaled(neg_ids, gn, h2)

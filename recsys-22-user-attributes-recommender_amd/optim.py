@@ -54,6 +54,8 @@ class FusedAdam(torch.optim.Optimizer):
                 tg = getattr(p, "_asme_table_grad", None)
                 if tg is not None:
                     tg.lazy = None
+                    if tg.plan is not None:  # rows staged from the old state: the loaded state is current
+                        tg.plan.staged = None
         super().load_state_dict(state_dict)
         for st in self.state.values():  # torch may restore `step` as a tensor; the kernels take an int
             if "step" in st and torch.is_tensor(st["step"]):

@@ -387,8 +387,9 @@ def test_lazy_adam_bit_exact_vs_dense(asme, dev):
         for p, mp, opt in ((p_lazy, map_l, o_lazy), (p_eager, map_e, o_eager)):
             plan = asme.ops.SparseTablePlan(p, [ids], mp)
             # the forward would gather these rows now: lazily-updated rows must equal eager rows
-            if p is p_lazy:
-                assert torch.equal(p_lazy.detach()[ids], p_eager.detach()[ids])
+            if p is p_lazy:  # (staged in slot order: the table rows themselves are caught up at apply)
+                src, sid = plan.gather_source(p_lazy.detach(), ids)
+                assert torch.equal(src[sid], p_eager.detach()[ids])
             asme._lib.call("asme_scatter_add_rows", rows.data_ptr(), plan.inverse_of(ids).data_ptr(), T, D,
                            plan.grad_rows.data_ptr(), plan.capacity, 1.0, asme._lib.stream())
             p._asme_table_grad.plan = plan

@@ -104,3 +104,33 @@ def test_int32_batch_ids_with_sparse_table(asme, dev):
         out.append(_params(model))
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
+
+
+def test_staged_rows_match_in_place_catch_up(asme, dev, monkeypatch):
+    """lazy table Adam with the step's rows staged in slot order (asme_lazy_adam_stage / _apply_staged, every
+    reader gathering the staged rows) == catching them up in place in the table, bit for bit -- across a
+    flush between forward and step (state_dict), a re-step without a new backward and a resumed step count"""
+    out = []
+    for staged in (True, False):
+        monkeypatch.setattr(asme.ops, "STAGE_ROWS", staged)
+        model, module, batch = _sasrec(asme, dev, "sparse")
+        opt = module.configure_optimizers()
+        seen = []
+        for i in range(4):
+            module.train()
+            loss = module.training_step(batch, i)["loss"]
+            table = model.item_table()
+            seen.append(table._asme_table_grad.plan.staged is not None)
+            if i == 2:
+                model.state_dict()  # flush while the step's rows are staged
+            loss.backward()
+            opt.step()
+            if i == 1:
+                opt.step()  # re-step: the kept gradient again, rows caught up from the table
+            opt.zero_grad()
+        assert seen == [False, staged, staged, staged]
+        out.append(_params(model))
+        out.append({k: v.clone() for k, v in opt.state[model.item_table()].items() if torch.is_tensor(v)})
+    for a, b in ((out[0], out[2]), (out[1], out[3])):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k

@@ -35,8 +35,11 @@ def main():
     ap.add_argument("--seq", type=int, default=200)
     ap.add_argument("--items", type=int, default=10_000_000)
     ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--partials", type=int, default=0, help="backward partial rows (ops._EMB_PARTIALS; 0: default)")
     a = ap.parse_args()
     asme = __graft_entry__.load_package()
+    if a.partials:
+        asme.ops._EMB_PARTIALS = a.partials
     dev = torch.device("cuda", 0)
     B, L, V, D = a.batch, a.seq, a.items + 3, a.dim
     T = B * L
