@@ -42,6 +42,40 @@ def mfma_peak(name):
     return round(PEAK_BF16X6_TFS, 1) if name in BF16X6_KERNELS else PEAK_FP32_MFMA_TFS
 
 
+def roofline_entries(kstats, work, traffic):
+    """one roofline per timed C-ABI call.  work[name] = (bound, amount) or ("gemm", flops, bytes): a GEMM's bound is
+    read off its arithmetic intensity against the ridge of its MFMA ceiling and the HBM peak (the transformer's
+    tall-skinny Linear GEMMs, 38-48 FLOP/B, sit below the bf16x6 ridge of 52 FLOP/B: HBM-bound)"""
+    out = []
+    for name, st in kstats.items():
+        if not st["count"] or name not in work:
+            continue
+        w = work[name]
+        secs = st["avg_ms"] / 1e3
+        extra = {}
+        if w[0] == "gemm":
+            flops, nbytes = w[1], w[2]
+            ai = flops / nbytes
+            ridge = mfma_peak(name) * 1e12 / (PEAK_HBM_GBS * 1e9)
+            bound, amount = ("mfma", flops) if ai >= ridge else ("hbm", nbytes)
+            extra = {"flop_per_byte": round(ai, 2), "ridge_flop_per_byte": round(ridge, 2),
+                     "mfma_tflops": round(flops / secs / 1e12, 2), "mfma_peak": mfma_peak(name),
+                     "mfma_frac": round(flops / secs / 1e12 / mfma_peak(name), 4),
+                     "flops_per_launch": flops, "bytes_per_launch": nbytes}
+        else:
+            bound, amount = w
+            extra = {("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): amount}
+        if bound == "mfma":
+            ach, peak, unit = amount / secs / 1e12, mfma_peak(name), "TFLOP/s"
+        else:
+            ach, peak, unit = amount / secs / 1e9, PEAK_HBM_GBS, "GB/s"
+        out.append({"kernel": name, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                    "frac": round(ach / peak, 4), "traffic": traffic.get(name), "avg_ms": round(st["avg_ms"], 4),
+                    "launches": st["count"], "total_ms": round(st["total_ms"], 3), **extra})
+    out.sort(key=lambda r: -r["total_ms"])
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,23 +275,15 @@ def bench_bert4rec(args, asme, dev, world, rank):
     T, H, dk = B * L, args.heads, d // args.heads
     pairs = B * H * L * L  # bidirectional
     wg_flops = 2.0 * T * (3 * d * d + d * d + 4 * d * d + 4 * d * d)
+    ffn = 4 * d
+    ws_bytes, wg_bytes = 2 * T * 4.0 * (8 * d + 3 * ffn), T * 4.0 * (8 * d + 2 * ffn)  # see the SASRec leg
     M = 0.9 * 0.2 * T + 0.1 * B  # expected non-ignored rows of a cloze batch
     work = {"asme_attention_fwd": ("mfma", 4.0 * pairs * dk), "asme_attention_bwd": ("mfma", 10.0 * pairs * dk),
-            "asme_ws_linear": ("mfma", 2 * wg_flops / 8), "asme_linear_weight_grad": ("mfma", wg_flops / 4),
+            "asme_ws_linear": ("gemm", 2 * wg_flops / 8, ws_bytes / 8),
+            "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4),
             "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
             "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0)}
-    rooflines = []
-    for name, st in timer.summary().items():
-        if not st["count"] or name not in work:
-            continue
-        bound, amount = work[name]
-        secs = st["avg_ms"] / 1e3
-        ach, peak, unit = ((amount / secs / 1e12, mfma_peak(name), "TFLOP/s") if bound == "mfma"
-                           else (amount / secs / 1e9, PEAK_HBM_GBS, "GB/s"))
-        rooflines.append({"kernel": name, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
-                          "frac": round(ach / peak, 4), "traffic": None, "avg_ms": round(st["avg_ms"], 4),
-                          "launches": st["count"], "total_ms": round(st["total_ms"], 3)})
-    rooflines.sort(key=lambda r: -r["total_ms"])
+    rooflines = roofline_entries(timer.summary(), work, {})
     name = "KeBERT4Rec" if kebert else "BERT4Rec"
     result = {"metric": f"training sequences/sec ({name} cloze, B={B} L={L} |V|={V}, fwd+bwd+Adam)",
               "value": round(B * world * args.steps / elapsed, 2), "unit": "sequences/s", "n_gpus": world,
@@ -397,12 +423,17 @@ def main():
     pairs = B * H * L * (L + 1) / 2.0
     # weight-gradient GEMMs: 4 per block (QKV, O, FFN in, FFN out), averaged per launch
     wg_flops = 2.0 * T * (3 * d * d + d * d + ffn * d + d * ffn)
+    # GEMM bytes per block (units of T x 4 B): forward X + Y of QKV (d + 3d), O (d + d), FFN in (d + act 4d + the
+    # activation factor 4d the backward needs in place of the pre-activation), FFN out (4d + d) = 8d + 3 ffn; the
+    # input gradients the same (dY + dX, the GELU one reading the factor); weight gradients dY + X = 8d + 2 ffn
+    ws_bytes = 2 * T * 4.0 * (8 * d + 3 * ffn)
+    wg_bytes = T * 4.0 * (8 * d + 2 * ffn)
     work = {
         "asme_attention_fwd": ("mfma", 2 * 2.0 * pairs * dk),
         "asme_attention_bwd": ("mfma", 5 * 2.0 * pairs * dk),
-        "asme_linear_weight_grad": ("mfma", wg_flops / 4),
+        "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4),
         # forward + input-gradient GEMMs: 8 per block, the same 4 shapes twice, averaged per launch
-        "asme_ws_linear": ("mfma", 2 * wg_flops / 8),
+        "asme_ws_linear": ("gemm", 2 * wg_flops / 8, ws_bytes / 8),
         "asme_gelu_dropout_fwd": ("hbm", 2 * T * ffn * 4),
         "asme_residual_ln_fwd": ("hbm", 4 * T * d * 4 + T * 8),
         "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),
@@ -431,21 +462,7 @@ def main():
             tj = json.load(f)
         if tj.get("config") == {"batch": B, "seq_len": L, "items": args.items, "dim": d, "layers": args.layers}:
             traffic = tj.get("bytes_per_launch", {})
-    rooflines = []
-    for name, st in kstats.items():
-        if not st["count"] or name not in work:
-            continue
-        bound, amount = work[name]
-        secs = st["avg_ms"] / 1e3
-        if bound == "mfma":
-            ach, peak, unit = amount / secs / 1e12, mfma_peak(name), "TFLOP/s"
-        else:
-            ach, peak, unit = amount / secs / 1e9, PEAK_HBM_GBS, "GB/s"
-        rooflines.append({"kernel": name, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
-                          "frac": round(ach / peak, 4), "traffic": traffic.get(name), "avg_ms": round(st["avg_ms"], 4),
-                          "launches": st["count"], "total_ms": round(st["total_ms"], 3),
-                          ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): amount})
-    rooflines.sort(key=lambda r: -r["total_ms"])
+    rooflines = roofline_entries(kstats, work, traffic)
     roof = rooflines[0] if rooflines else None
 
     result = {

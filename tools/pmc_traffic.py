@@ -24,6 +24,10 @@ MAP = [
     (r"emb_bwd4?_kernel", "asme_embedding_bwd", True),
     (r"lazy_catch_up(_v4)?_kernel", "asme_lazy_adam_catch_up", True),
     (r"lazy_apply(_v4)?_kernel", "asme_lazy_adam_apply", True),
+    (r"lazy_stage_v4_kernel", "asme_lazy_adam_stage", True),
+    (r"lazy_apply_staged_v4_kernel", "asme_lazy_adam_apply_staged", True),
+    (r"sampled_fwd_kernel", "asme_sampled_logits_fwd", True),
+    (r"sampled_bwd_kernel", "asme_sampled_logits_bwd", True),
     (r"gelu_dropout_fwd_kernel", "asme_gelu_dropout_fwd", True),
     (r"gelu_dropout_bwd_kernel", "asme_gelu_dropout_bwd", True),
     (r"residual_ln_fwd_kernel", "asme_residual_ln_fwd", True),

@@ -15,7 +15,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-
 echo "kernel trace done"
 if [ -n "${PMC:-1}" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "${PMC_REGEX:-asme|attn|emb|lazy|adam|residual|gelu|ln_|weight_grad|sum_slabs|ws_gemm}" \
+    timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "${PMC_REGEX:-asme|attn|emb|lazy|adam|residual|gelu|ln_|weight_grad|sum_slabs|ws_gemm|sampled}" \
         -d "$OUT/pmc_$C" -o run --output-format csv -- \
         python bench.py --steps 2 --warmup 1 --cpu-baseline 0 > "$OUT/pmc_$C.log" 2>&1 || exit $?
     echo "pmc $C done"
