@@ -84,9 +84,14 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 // so positions are stable: bucket w holds its ids in increasing unique-index order.
 constexpr int kBk = 1024, kBkThreads = 256, kMaxW = 64;
 
-__global__ __launch_bounds__(kBkThreads) void bucket_count_kernel(const int64_t* __restrict__ ids, int64_t n, int W,
+// n_dev (nullable): the number of ids is *n_dev <= n (a dedup count that never visits the host)
+__device__ __forceinline__ int64_t live_n(int64_t n, const int32_t* n_dev) { return n_dev ? min(n, (int64_t)*n_dev) : n; }
+
+__global__ __launch_bounds__(kBkThreads) void bucket_count_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                                  const int32_t* __restrict__ n_dev, int W,
                                                                   int32_t* __restrict__ bcount, int64_t nb) {
     __shared__ int32_t h[kMaxW];
+    n = live_n(n, n_dev);
     for (int w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
     __syncthreads();
     const int64_t b0 = (int64_t)blockIdx.x * kBk;
@@ -100,8 +105,10 @@ __global__ __launch_bounds__(kBkThreads) void bucket_count_kernel(const int64_t*
 
 // exclusive scan of bcount (W * nb, w-major) in place; counts[w] = ids owned by w
 __global__ __launch_bounds__(1024) void bucket_scan_kernel(int32_t* __restrict__ bcount, int64_t nb, int W, int64_t n,
+                                                           const int32_t* __restrict__ n_dev,
                                                            int64_t* __restrict__ counts) {
     __shared__ int32_t part[1024];
+    n = live_n(n, n_dev);
     const int64_t total = nb * W;
     const int64_t per = (total + blockDim.x - 1) / blockDim.x;
     const int64_t lo = min(total, (int64_t)threadIdx.x * per), hi = min(total, lo + per);
@@ -132,11 +139,13 @@ __global__ __launch_bounds__(1024) void bucket_scan_kernel(int32_t* __restrict__
     }
 }
 
-__global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_t* __restrict__ ids, int64_t n, int W,
+__global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                                    const int32_t* __restrict__ n_dev, int W,
                                                                     const int32_t* __restrict__ boff, int64_t nb,
                                                                     int64_t* __restrict__ order,
                                                                     int64_t* __restrict__ send_local) {
     constexpr int kWv = kBkThreads / 64;
+    n = live_n(n, n_dev);
     __shared__ int32_t base[kMaxW];
     __shared__ int32_t wcnt[kWv][kMaxW];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -172,7 +181,9 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_
     }
 }
 
-__global__ void invert_perm_kernel(const int64_t* __restrict__ order, int64_t n, int64_t* __restrict__ pos) {
+__global__ void invert_perm_kernel(const int64_t* __restrict__ order, int64_t n, const int32_t* __restrict__ n_dev,
+                                   int64_t* __restrict__ pos) {
+    n = live_n(n, n_dev);
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j < n) pos[order[j]] = j;
 }
@@ -237,8 +248,10 @@ ASME_API int64_t asme_bucket_by_owner_workspace(int64_t n, int world) {
 // Row-shard request routing: the n unique ids, grouped by owner (id % world) in a stable order.
 // order[j] = index into ids of the j-th id sent; send_local[j] = ids[order[j]] / world (the owner's row);
 // counts[w] = ids sent to rank w (int64, world entries); pos[order[j]] = j (nullable: the inverse permutation).
-ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, int world, void* workspace, int64_t ws_bytes,
-                                  int64_t* order, int64_t* send_local, int64_t* counts, int64_t* pos, void* stream) {
+// n_dev (nullable): only the first *n_dev <= n ids are live (the dedup count on the device: no host sync).
+ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, void* workspace,
+                                  int64_t ws_bytes, int64_t* order, int64_t* send_local, int64_t* counts, int64_t* pos,
+                                  void* stream) {
     ASME_CHECK_ARG(ids && workspace && order && send_local && counts, "asme_bucket_by_owner: null pointer");
     ASME_CHECK_ARG(world >= 1 && world <= kMaxW, "asme_bucket_by_owner: world must be in [1, 64]");
     ASME_CHECK_ARG(n >= 0 && n < ((int64_t)1 << 31), "asme_bucket_by_owner: bad n");
@@ -251,11 +264,12 @@ ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, int world, void
     }
     const int64_t nb = (n + kBk - 1) / kBk;
     int32_t* bcount = (int32_t*)workspace;
-    hipLaunchKernelGGL(bucket_count_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, world, bcount, nb);
-    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, bcount, nb, world, n, counts);
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, world, bcount, nb,
-                       order, send_local);
-    if (pos) hipLaunchKernelGGL(invert_perm_kernel, dim3(nblk(n)), dim3(256), 0, s, order, n, pos);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, n_dev, world, bcount,
+                       nb);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, bcount, nb, world, n, n_dev, counts);
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, n_dev, world, bcount,
+                       nb, order, send_local);
+    if (pos) hipLaunchKernelGGL(invert_perm_kernel, dim3(nblk(n)), dim3(256), 0, s, order, n, n_dev, pos);
     ASME_LAUNCH_CHECK("asme_bucket_by_owner");
 }
 

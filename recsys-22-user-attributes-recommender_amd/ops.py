@@ -452,9 +452,10 @@ def gather_rows(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def bucket_by_owner(unique: torch.Tensor, world: int):
+def bucket_by_owner(unique: torch.Tensor, world: int, count: Optional[torch.Tensor] = None):
     """stable grouping of unique ids by owner (id % world): (order, send_local, counts (int64, world), pos) with
-    unique[order[j]] the j-th id sent, send_local[j] its owner-local row, pos[order[j]] = j"""
+    unique[order[j]] the j-th id sent, send_local[j] its owner-local row, pos[order[j]] = j.  count (int32 (1,) on
+    the device, optional): only unique[:count] take part, the outputs past it are unspecified (no host sync)"""
     u = _i64(unique).reshape(-1)
     n = u.numel()
     dev = u.device
@@ -463,8 +464,8 @@ def bucket_by_owner(unique: torch.Tensor, world: int):
     send_local = torch.empty(n, device=dev, dtype=torch.int64)
     counts = torch.empty(world, device=dev, dtype=torch.int64)
     pos = torch.empty(n, device=dev, dtype=torch.int64)
-    call("asme_bucket_by_owner", ptr(u), n, world, ptr(ws), ws.numel(), ptr(order), ptr(send_local), ptr(counts),
-         ptr(pos), stream())
+    call("asme_bucket_by_owner", ptr(u), n, ptr(count), world, ptr(ws), ws.numel(), ptr(order), ptr(send_local),
+         ptr(counts), ptr(pos), stream())
     return order, send_local, counts, pos
 
 

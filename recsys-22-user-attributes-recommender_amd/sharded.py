@@ -98,12 +98,16 @@ class RowShardExchange:
         self.vocab = vocab
         self.local_rows = shard_rows(vocab, self.world, self.rank)
 
-    def request(self, unique: torch.Tensor) -> ExchangeState:
-        """route the requester's unique global ids to their owners"""
+    def request(self, unique: torch.Tensor, count: Optional[torch.Tensor] = None) -> ExchangeState:
+        """route the requester's unique global ids to their owners (count: int32 (1,) device tensor, only
+        unique[:count] are live -- the dedup count, read on the device; the per-owner counts below are the step's
+        one host sync)"""
         W = self.world
         if unique.is_cuda:  # stable owner bucketing in one counting-sort pass (asme_bucket_by_owner)
-            order, send_local, send_counts_t, pos = ops.bucket_by_owner(unique, W)
+            order, send_local, send_counts_t, pos = ops.bucket_by_owner(unique, W, count)
         else:
+            if count is not None:
+                unique = unique[:int(count.item())]
             owner = unique % W
             order = torch.argsort(owner, stable=True)
             send_counts_t = torch.bincount(owner, minlength=W).to(torch.int64)
@@ -115,8 +119,8 @@ class RowShardExchange:
         counts = torch.stack([send_counts_t, recv_counts_t]).cpu()  # one host sync per step
         sc, rc = counts[0].tolist(), counts[1].tolist()
         recv_local = torch.empty(sum(rc), dtype=torch.int64, device=unique.device)
-        _all_to_all(recv_local, send_local, rc, sc, group=self.group)
-        return ExchangeState(order, sc, rc, recv_local, pos)
+        _all_to_all(recv_local, send_local[:sum(sc)], rc, sc, group=self.group)
+        return ExchangeState(order[:sum(sc)], sc, rc, recv_local, pos)
 
     def reply_rows(self, st: ExchangeState, rows: torch.Tensor) -> torch.Tensor:
         """owners' rows (aligned with st.recv_local) -> the requester's rows in SEND order: row j belongs to
@@ -174,17 +178,17 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         self._maps(shard.device)
         # 1. requester: dedup every id of the step
         req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
-        U = req.n_unique()
-        unique = req.unique[:U]
-        # 2. route ids to owners; owners catch their rows up (lazy Adam) and gather them
-        st = self.exchange.request(unique)
+        # 2. route ids to owners (the dedup count stays on the device); owners bring their rows up to date (lazy
+        # Adam: staged in slot order, or caught up in the table) and gather them
+        st = self.exchange.request(req.unique, req.count)
         own = None
+        src, src_ids = shard.detach(), st.recv_local
         if train:
             own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
             own.grad_scale = 1.0 / self.exchange.world  # DDP gradient averaging, applied in the ordered row sums
+            src, src_ids = own.gather_source(shard.detach(), st.recv_local)
         with torch.no_grad():
-            rows = ops.gather_rows(st.recv_local, shard.detach()) if len(st.recv_local) \
-                else shard.new_empty(0, shard.shape[1])
+            rows = ops.gather_rows(src_ids, src) if len(st.recv_local) else shard.new_empty(0, shard.shape[1])
         # the compact table stays in send order; the ids are remapped to it (no row permutation)
         compact = self.exchange.reply_rows(st, rows)
         inv = [st.pos.index_select(0, req.inverse_of(x).reshape(-1)).view(x.shape) for x in id_sets]

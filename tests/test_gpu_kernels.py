@@ -584,6 +584,11 @@ def test_bucket_by_owner_matches_stable_argsort(asme, dev, world, n):
     assert torch.equal(counts, torch.bincount(owner, minlength=world))
     assert torch.equal(send_local, unique[ref] // world)
     assert torch.equal(pos[order], torch.arange(n, device=dev))
+    # the same ids at the head of a larger buffer with the live count on the device (the sharded step's form)
+    padded = torch.cat([unique, torch.randint(0, 10_000_003, (777,), generator=g).to(dev)])
+    o2, s2, c2, p2 = asme.ops.bucket_by_owner(padded, world, torch.tensor([n], dtype=torch.int32, device=dev))
+    assert torch.equal(o2[:n], ref) and torch.equal(c2, counts) and torch.equal(s2[:n], send_local[:n])
+    assert torch.equal(p2[:n], pos)
 
 
 @pytest.mark.parametrize("D", [128, 64, 36])

@@ -1,13 +1,13 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gpu_optim.py tests/test_gpu_kernels.py tests/test_gpu_models.py > gpurun_out/t2.log 2>&1
-rc=$?; tail -5 gpurun_out/t2.log; [ $rc -le 1 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 > gpurun_out/b2.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --producer resident > gpurun_out/b2r.log 2>&1 || exit $?
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ${TESTS:-tests/test_gpu_sharded_multirank.py tests/test_gpu_kernels.py tests/test_gpu_eval.py tests/test_gpu_optim.py} > gpurun_out/t5.log 2>&1
+rc=$?; tail -5 gpurun_out/t5.log; [ $rc -le 1 ] || exit $rc
+if [ -n "${BENCH_ARGS:-}" ]; then
+timeout -k 10 300 python bench.py $BENCH_ARGS > gpurun_out/b5.log 2>&1 || exit $?
 python - <<'P'
 import json
-for f in ("gpurun_out/b2.log","gpurun_out/b2r.log"):
-    j=json.loads(open(f).read().strip().splitlines()[-1])
-    print(f, j["value"], j["ms_per_step"], j["flush_ms"])
-    for r in j["rooflines"]: print("  ", r["kernel"], r["avg_ms"], r["frac"], r["launches"])
+j=json.loads(open("gpurun_out/b5.log").read().strip().splitlines()[-1])
+print(j["value"], j["ms_per_step"], j.get("flush_ms"))
+for r in j["rooflines"]: print("  ", r["kernel"], r["avg_ms"], r["frac"], r["launches"])
 P
+fi
