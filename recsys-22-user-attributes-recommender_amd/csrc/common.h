@@ -34,7 +34,8 @@ __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
-// reduce over the 4 lane-groups {l, l^16, l^32, l^48} (the MFMA 16x16 "row group" dimension)
+// reduce over the 4 lane-groups {l, l^16, l^32, l^48} (the MFMA 16x16 "row group" dimension).  (The gfx950
+// v_permlane16/32_swap form of these two measured 1-3 % slower inside the attention kernels: kept on ds_bpermute.)
 __device__ __forceinline__ float group4_sum(float v) {
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);

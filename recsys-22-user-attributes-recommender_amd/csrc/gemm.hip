@@ -23,6 +23,10 @@
 
 using namespace asme;
 
+#ifndef ASME_WG_STAGGER
+#define ASME_WG_STAGGER 0  // 1: waves 4-7 multiply before they stage (measured 2 % slower)
+#endif
+
 namespace {
 
 constexpr int kTile = 128;         // output tile (N and K)
@@ -38,21 +42,21 @@ __device__ __forceinline__ int tslot(int c, int s) {
     return (c ^ ((c >> 1) & 1)) * 4 + ((((c >> 2) & 3) ^ (3 * s)) & 3);
 }
 
-// rows t0 + 8 rg .. + 7, columns col0 + 2 cg, + 1 of a row-major operand (zero past T / ncols).  `full`
-// (workgroup-uniform: the whole 32-row block and 128 columns in range) takes the branch-free form.
-__device__ __forceinline__ void load_cols(const float* __restrict__ base, int64_t ld, int64_t t0, int64_t T,
-                                          int col0, int ncols, int rg, int cg, bool full, float2 (&r)[8]) {
-    const float* p = base + (t0 + 8 * rg) * ld + col0 + 2 * cg;
-    if (full) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) r[q] = *reinterpret_cast<const float2*>(p + q * ld);
-        return;
-    }
-    const bool col_ok = col0 + 2 * cg < ncols;
+typedef unsigned u32v2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kDrop = 0x80000000u;  // >= every chunk's record count: the load returns 0
+
+// rows r0 + 8 rg .. + 7 (chunk-relative) of this thread's column pair, by buffer loads against the chunk's record
+// range: rows past the chunk (and a column pair past the operand, off_col == kDrop) read as 0 with no branch, so
+// every block issues the same loads and the compiler's vmcnt waits stay exact (a branchy tail made it wait for
+// vmcnt(0): one block of loads in flight instead of two)
+__device__ __forceinline__ void load_cols(__amdgpu_buffer_rsrc_t rs, uint32_t ld_bytes, int64_t r0, int rg,
+                                          uint32_t off_col, float2 (&r)[8]) {
+    const uint32_t base = (uint32_t)(r0 + 8 * rg) * ld_bytes;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        const int64_t t = t0 + 8 * rg + q;
-        r[q] = (t < T && col_ok) ? *reinterpret_cast<const float2*>(p + q * ld) : make_float2(0.f, 0.f);
+        const uint32_t off = off_col == kDrop ? kDrop : base + (uint32_t)q * ld_bytes + off_col;
+        const u32v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        r[q] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
     }
 }
 
@@ -89,8 +93,9 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const int64_t t_end = min(T, t_begin + chunk_rows);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
     const int wr = wave >> 2, wc = wave & 3;  // 64 dY columns x 32 X columns
-    // loader role: threads 0-255 dY, 256-511 X (wave-uniform)
-    const bool load_a = threadIdx.x < 256;
+    // loader role: threads 0-255 dY, 256-511 X (wave-uniform: read from the first lane, so the operand's buffer
+    // resource lives in scalar registers)
+    const bool load_a = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4;
     const int u = threadIdx.x & 255, cg = u & 63, rg = u >> 6;
     const float* src = load_a ? A : B;
     const int64_t ld = load_a ? lda : ldb;
@@ -98,7 +103,11 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const int my_planes = load_a ? 0 : 3 * kPlane;
     const bool do_bias = bias_part != nullptr && tk == 0 && load_a;
     float2 bsum = make_float2(0.f, 0.f);  // dY columns n0 + 2cg, + 1 over this thread's rows
-    const bool cols_full = n0 + kTile <= N && k0 + kTile <= K;
+    // the chunk of this operand as a buffer resource (rows [t_begin, t_end)); this thread's column pair
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(src + t_begin * ld), 0, (int)((t_end - t_begin) * ld * 4), 0x00020000);
+    const uint32_t ld_bytes = (uint32_t)(ld * 4);
+    const uint32_t off_col = col0 + 2 * cg < ncols ? (uint32_t)((col0 + 2 * cg) * 4) : kDrop;
 
     floatx4 acc[4][2];
 #pragma unroll
@@ -106,12 +115,12 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    auto load = [&](int64_t t0, float2 (&r)[8]) {
-        if (t0 < t_end) load_cols(src, ld, t0, t_end, col0, ncols, rg, cg, cols_full && t0 + kTT <= t_end, r);
-    };
-    // the block at t0 (in r) into LDS buffer buf; r then takes the block two ahead
+    // (loads past the chunk are issued too and read zeros: unconditional, see load_cols)
+    auto load = [&](int64_t t0, float2 (&r)[8]) { load_cols(rs, ld_bytes, t0 - t_begin, rg, off_col, r); };
+    // the block at t0 (in r) into LDS buffer buf; r then takes the block two ahead.  No branch at all: a block past
+    // the chunk holds zeros (its loads read nothing) and lands in the buffer nobody multiplies any more -- any
+    // control flow here made the compiler copy the in-flight registers and wait for every load (vmcnt(0))
     auto stage = [&](int64_t t0, float2 (&r)[8], int buf) {
-        if (t0 >= t_end) return;
         store_cols(lds + buf * kBuf + my_planes, rg, cg, r);
         if (do_bias) {
 #pragma unroll
@@ -148,15 +157,32 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     load(t_begin + kTT, r1);
     stage(t_begin, r0, 0);
     __syncthreads();
-    for (int64_t t0 = t_begin; t0 < t_end; t0 += 2 * kTT) {
-        stage(t0 + kTT, r1, 1);
-        compute(0);
+    // pairs of blocks with no exit in between (buf 0 holds block i, r1 block i + 1, r0 block i + 2 at the top of a
+    // trip); an odd last block is multiplied after the loop.  Waves 4-7 may run each half's two parts in the
+    // opposite order (ASME_WG_STAGGER): stage and compute touch different buffers.
+    const int64_t nblk = (t_end - t_begin + kTT - 1) / kTT;
+    const bool late = ASME_WG_STAGGER && wave >= 4;
+    int64_t i = 0;
+    for (; i + 2 <= nblk; i += 2) {
+        const int64_t t0 = t_begin + i * kTT;
+        if (late) {
+            compute(0);
+            stage(t0 + kTT, r1, 1);
+        } else {
+            stage(t0 + kTT, r1, 1);
+            compute(0);
+        }
         __syncthreads();
-        if (t0 + kTT >= t_end) break;
-        stage(t0 + 2 * kTT, r0, 0);
-        compute(1);
+        if (late) {
+            compute(1);
+            stage(t0 + 2 * kTT, r0, 0);
+        } else {
+            stage(t0 + 2 * kTT, r0, 0);
+            compute(1);
+        }
         __syncthreads();
     }
+    if (i < nblk) compute(0);
     // partial slab: part[chunk][n][k]; lane holds rows n = ... + 4g + q, column k = ... + c16
     // chunk slab: [N x K dW partial | N db partial (when db is requested)]
     const int64_t slab = (int64_t)N * K + (bias_part != nullptr ? N : 0);
@@ -234,6 +260,10 @@ Plan make_plan(int64_t T, int64_t N, int64_t K) {
     const int64_t want = std::max<int64_t>(8, (256 / tiles) / 8 * 8);
     int64_t rows = (T + want - 1) / want;
     rows = std::max<int64_t>(kTT, ((rows + kTT - 1) / kTT) * kTT);
+    // a chunk's rows (plus the two blocks read past it) must stay within a buffer resource's 2 GiB offsets
+    const int64_t max_rows = (((int64_t)1 << 31) / (4 * std::max<int64_t>(std::max<int64_t>(N, K), 1)) - 2 * kTT) /
+                             kTT * kTT;
+    rows = std::min<int64_t>(rows, std::max<int64_t>(kTT, max_rows));
     return {(T + rows - 1) / rows, rows};  // chunks holding tokens; the grid rounds them up to a multiple of 8
 }
 
@@ -256,6 +286,8 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
                    "asme_linear_weight_grad: workspace too small");
     if (n_tokens == 0) return 0;
     const Plan p = make_plan(n_tokens, out_features, in_features);
+    ASME_CHECK_ARG((p.chunk_rows + 2 * kTT) * std::max(ld_dy, ld_x) * 4 < ((int64_t)1 << 31),
+                   "asme_linear_weight_grad: row stride too large for the chunk's buffer range");
     hipStream_t s = (hipStream_t)stream;
     float* part = workspace;
     float* bpart = db ? workspace : nullptr;  // (a flag: the bias partials sit in each chunk's slab)
@@ -268,8 +300,8 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
         if (e != hipSuccess) return hip_status(e, "asme_linear_weight_grad: LDS opt-in");
         attr = true;
     }
-    hipLaunchKernelGGL(weight_grad_kernel, grid, dim3(kWgThreads), 2 * kBuf * 16, s, dy, ld_dy, x, ld_x, n_tokens, (int)out_features,
-                       (int)in_features, p.chunk_rows, part, bpart);
+    hipLaunchKernelGGL(weight_grad_kernel, grid, dim3(kWgThreads), 2 * kBuf * 16, s, dy, ld_dy, x, ld_x, n_tokens,
+                       (int)out_features, (int)in_features, p.chunk_rows, part, bpart);
     const int64_t width_w = out_features * in_features, width_b = db ? out_features : 0;
     hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width_w + width_b + kRedCols - 1) / kRedCols)), dim3(1024), 0,
                        s, part, p.nchunks, width_w, dw, width_b, db, accumulate);
