@@ -22,6 +22,7 @@
 // Epilogues: WS_STORE       Y = C (+ bias)
 //            WS_GELU_DROP   pre = C + bias; Y = dropout(GELU(pre)); A = keep * GELU'(pre)   (FFN inner, forward)
 //            WS_GELU_BWD    Y = C * A                                                   (through the activation)
+//            WS_ACCUM       Y = C + Y                        (the second K = 256 half of a K = 512 product)
 // A (the activation factor, written by the forward in place of the pre-activation, same bytes) makes the
 // backward epilogue a single multiply: no Philox, erf or exp in the input-gradient GEMM.
 // Dropout decisions are exactly those of asme_gelu_dropout_fwd/bwd (norm.hip): one Philox block per pair of
@@ -42,7 +43,7 @@ constexpr int kWaves = 8;           // 512-thread workgroups, one per CU, two wa
 constexpr int kLdsMax = 160 * 1024;
 constexpr uint32_t kDrop = 0x80000000u;  // >= every buffer's record count: the access is dropped / reads 0
 
-enum { WS_STORE = 0, WS_GELU_DROP = 1, WS_GELU_BWD = 2 };
+enum { WS_STORE = 0, WS_GELU_DROP = 1, WS_GELU_BWD = 2, WS_ACCUM = 3 };
 
 struct WsEpi {
     const float* bias;   // [N] or null
@@ -50,11 +51,10 @@ struct WsEpi {
     const float* pre_in; // WS_GELU_BWD: activation factor in
     float p;             // dropout probability (0: none)
     uint64_t seed;
-    // split-K over K = 512 (two K = 256 launches): row strides of X and (non-trans) W, the first k column, and
-    // WS_STORE accumulating into Y (the second half)
+    // split-K over K = 512 (two K = 256 launches, the second WS_ACCUM): row strides of X and (non-trans) W and the
+    // first k column
     int64_t ldx, ldw;
     int kofs;
-    int accumulate;
 };
 
 __device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s ^ (r & 15)); }
@@ -128,7 +128,11 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         return X + (m < M ? m : M - 1) * ep.ldx + ep.kofs + 8 * g;
     };
     const __amdgpu_buffer_rsrc_t yr = rsrc(Y, M * N * 4);
-    const __amdgpu_buffer_rsrc_t pr = rsrc(EPI == WS_GELU_DROP ? (const void*)ep.pre_out : (const void*)ep.pre_in,
+    // the second operand stream of the epilogue: the activation factor (GELU forward writes / backward reads it) or,
+    // for WS_ACCUM (second K half), Y itself -- read at the tile boundary like the factor, so the epilogue's
+    // read-modify-write never drains the X ring (a load right before the store made the wave wait for vmcnt(0))
+    const __amdgpu_buffer_rsrc_t pr = EPI == WS_ACCUM ? yr
+                                    : rsrc(EPI == WS_GELU_DROP ? (const void*)ep.pre_out : (const void*)ep.pre_in,
                                            EPI == WS_STORE ? 0 : M * N * 4);
     float4 breg[CT];
 #pragma unroll
@@ -178,12 +182,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             const float4 v = *reinterpret_cast<const float4*>(stg + (idx / NB4) * SROW + 4 * (idx % NB4));
             const uint32_t off = staged_off(ct, srow0);
             if constexpr (EPI == WS_STORE) {
-                if (ep.accumulate) {
-                    const float4 o = bload(yr, off);
-                    bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off);
-                } else {
-                    bstore(v, yr, off);
-                }
+                bstore(v, yr, off);
+            } else if constexpr (EPI == WS_ACCUM) {
+                const float4 o = pre[ct];
+                bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off);
             } else if constexpr (EPI == WS_GELU_DROP) {
                 // (a lane holds one 4-element chunk here: its own half of the chunk pair's Philox block)
                 float u[4] = {1.f, 1.f, 1.f, 1.f};
@@ -204,11 +206,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         const uint32_t off = soff + ct * 64;
         float4 v = stash[ct];
         if constexpr (EPI == WS_STORE) {
-            if (ep.accumulate) {
-                const float4 o = bload(yr, off);
-                v = make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
-            }
             bstore(v, yr, off);
+        } else if constexpr (EPI == WS_ACCUM) {
+            const float4 o = pre[ct];
+            bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off);
         } else if constexpr (EPI == WS_GELU_DROP) {
             float u[4] = {1.f, 1.f, 1.f, 1.f};
             if (ep.p > 0.f) {
@@ -273,14 +274,14 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                 *reinterpret_cast<float4*>(stg + c16 * SROW + ct * 16 + 4 * g) =
                     make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
                                 acc[ct][3] + breg[ct].w);
-                if constexpr (EPI == WS_GELU_BWD) pre[ct] = bload(pr, staged_off(ct, srow0));
+                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM) pre[ct] = bload(pr, staged_off(ct, srow0));
             }
         } else {
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 stash[ct] = make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
                                         acc[ct][3] + breg[ct].w);
-                if constexpr (EPI == WS_GELU_BWD) pre[ct] = bload(pr, soff + ct * 64);
+                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM) pre[ct] = bload(pr, soff + ct * 64);
             }
         }
         rc = rn;
@@ -368,19 +369,19 @@ ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W
     ASME_CHECK_ARG(((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 15) == 0 && ((uintptr_t)W & 15) == 0,
                    "asme_ws_linear: 16-B alignment");
     ASME_CHECK_ARG(p >= 0.f && p < 1.f, "asme_ws_linear: dropout probability in [0, 1)");
-    const WsEpi ep{bias, pre_out, pre_in, p, seed, K, K, 0, 0};
+    const WsEpi ep{bias, pre_out, pre_in, p, seed, K, K, 0};
     const int ct = pick_ct((int)N, (int)K);
     hipStream_t s = (hipStream_t)stream;
     // K = 512 plain stores: two K = 256 halves with 64-feature blocks (the 512-deep split W block only fits 32
     // features, which splits and re-reads X four times); the second half accumulates into Y
     if (K == 512 && epi == 0 && pick_ct((int)N, 256) == 4) {
-        const WsEpi e1{bias, nullptr, nullptr, 0.f, 0, 512, 512, 0, 0};
-        const WsEpi e2{nullptr, nullptr, nullptr, 0.f, 0, 512, 512, 256, 1};
+        const WsEpi e1{bias, nullptr, nullptr, 0.f, 0, 512, 512, 0};
+        const WsEpi e2{nullptr, nullptr, nullptr, 0.f, 0, 512, 512, 256};
         const int rc = trans ? launch_ws<256, 4, true, WS_STORE>(X, M, W, (int)N, Y, e1, s)
                              : launch_ws<256, 4, false, WS_STORE>(X, M, W, (int)N, Y, e1, s);
         if (rc != 0) return rc;
-        return trans ? launch_ws<256, 4, true, WS_STORE>(X, M, W, (int)N, Y, e2, s)
-                     : launch_ws<256, 4, false, WS_STORE>(X, M, W, (int)N, Y, e2, s);
+        return trans ? launch_ws<256, 4, true, WS_ACCUM>(X, M, W, (int)N, Y, e2, s)
+                     : launch_ws<256, 4, false, WS_ACCUM>(X, M, W, (int)N, Y, e2, s);
     }
     if (trans) {
         if (epi == 0) return dispatch_k<true, WS_STORE>((int)K, ct, X, M, W, (int)N, Y, ep, s);
