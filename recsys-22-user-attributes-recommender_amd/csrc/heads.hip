@@ -8,7 +8,7 @@
 //   nn.CrossEntropyLoss(ignore_index=pad)      core/modules/masked_training_module.py:93-111,
 //                                              core/losses/sasrec/sas_rec_losses.py:15-32, losses.py:77-115
 //   get_true_positives / calc_ndcg             core/metrics/common.py:4-27,118-175 (rank of the target)
-#include "common.h"
+#include "rows.h"
 #include <algorithm>
 #include <cmath>
 
@@ -16,6 +16,123 @@ using namespace asme;
 
 namespace {
 constexpr int kWaves = 4;
+
+// Row-layout forms (rows.h) for 16-B aligned D % 4 == 0 tables: a token row is LPR lanes x NV float4 (16 lanes x 2 at
+// D = 128: 4 tokens per wave, K per lane group), the dot products reduce inside the lane group on DPP, every load
+// and store is a 16-B vector -- instead of one token per wave with 4-B loads and a 6-step ds_bpermute wave sum.
+template <class R, int K>
+__global__ __launch_bounds__(256) void sampled_fwd4_kernel(const float* __restrict__ H, const float* __restrict__ E,
+                                                           const int64_t* __restrict__ pos,
+                                                           const int64_t* __restrict__ neg, int64_t T, int D,
+                                                           int64_t V, float* __restrict__ pos_out,
+                                                           float* __restrict__ neg_out) {
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR;
+    const int64_t t0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * R::RPW * K + lane / R::LPR;
+    int64_t ip[K], in[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        const int64_t a = t < T ? pos[t] : 0, b = t < T ? neg[t] : 0;
+        ip[k] = (a < 0 || a >= V) ? 0 : a;
+        in[k] = (b < 0 || b >= V) ? 0 : b;
+    }
+    RowVals<R> h[K], ep[K], en[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        row_load<R>(H + (t < T ? t : 0) * D, sub, D, h[k]);
+        row_load<R>(E + ip[k] * D, sub, D, ep[k]);
+        row_load<R>(E + in[k] * D, sub, D, en[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        float sp = 0.f, sn = 0.f;
+#pragma unroll
+        for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+            for (int i = 0; i < R::W; ++i) {
+                sp += ep[k][j][i] * h[k][j][i];
+                sn += en[k][j][i] * h[k][j][i];
+            }
+        sp = row_sum<R::LPR>(sp);
+        sn = row_sum<R::LPR>(sn);
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        if (sub == 0 && t < T) {
+            pos_out[t] = sp;
+            neg_out[t] = sn;
+        }
+    }
+}
+
+template <class R, int K>
+__global__ __launch_bounds__(256) void sampled_bwd4_kernel(const float* __restrict__ H, const float* __restrict__ E,
+                                                           const int64_t* __restrict__ pos,
+                                                           const int64_t* __restrict__ neg, int64_t T, int D,
+                                                           int64_t V, const float* __restrict__ gpos,
+                                                           const float* __restrict__ gneg, float* __restrict__ dH,
+                                                           float* __restrict__ dE) {
+    const int lane = threadIdx.x & 63, sub = lane % R::LPR;
+    const int64_t t0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * R::RPW * K + lane / R::LPR;
+    int64_t ip[K], in[K];
+    float gp[K], gn[K];
+    bool okp[K], okn[K];  // out-of-range ids: dH reads row 0 (like the gather), the table gets nothing
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        const bool live = t < T;
+        const int64_t a = live ? pos[t] : -1, b = live ? neg[t] : -1;
+        okp[k] = a >= 0 && a < V;
+        okn[k] = b >= 0 && b < V;
+        ip[k] = okp[k] ? a : 0;
+        in[k] = okn[k] ? b : 0;
+        gp[k] = live ? gpos[t] : 0.f;
+        gn[k] = live ? gneg[t] : 0.f;
+    }
+    RowVals<R> ep[K], en[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        row_load<R>(E + ip[k] * D, sub, D, ep[k]);
+        row_load<R>(E + in[k] * D, sub, D, en[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        if (t >= T) break;
+        if (dH) {
+            RowVals<R> d;
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) d[j][i] = gp[k] * ep[k][j][i] + gn[k] * en[k][j][i];
+            row_store<R>(dH + t * D, sub, D, d);
+        }
+        if (dE) {
+            RowVals<R> h;
+            row_load<R>(H + t * D, sub, D, h);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j) {
+                const int c = R::col(sub, j);
+                if (c >= D) continue;
+#pragma unroll
+                for (int i = 0; i < R::W; ++i) {
+                    if (okp[k] && gp[k] != 0.f) unsafeAtomicAdd(&dE[ip[k] * D + c + i], gp[k] * h[j][i]);
+                    if (okn[k] && gn[k] != 0.f) unsafeAtomicAdd(&dE[in[k] * D + c + i], gn[k] * h[j][i]);
+                }
+            }
+        }
+    }
+}
+
+// the row layout of the sampled head (the embedding kernels' at D = 128: 16 lanes x 2 float4)
+template <class F>
+int with_head_layout(int64_t D, F&& f) {
+    if (D == 128) {
+        f(RowLayout<4, 16, 2>{});
+        return 0;
+    }
+    return with_row_layout(D, f);
+}
+constexpr int kHeadK = 2;  // tokens per lane group
 
 template <int VPL>
 __global__ __launch_bounds__(256) void sampled_fwd_kernel(const float* __restrict__ H, const float* __restrict__ E,
@@ -331,6 +448,19 @@ ASME_API int asme_sampled_logits_fwd(const float* hidden, const float* table, co
                                      float* pos_out, float* neg_out, void* stream) {
     ASME_CHECK_ARG(hidden && table && pos_ids && neg_ids && pos_out && neg_out, "asme_sampled_logits_fwd: null");
     if (n_tokens == 0) return 0;
+    if (dim % 4 == 0 && (((uintptr_t)hidden | (uintptr_t)table) & 15) == 0) {
+        if (with_head_layout(dim, [&](auto layout) {
+                using R = decltype(layout);
+                if constexpr (R::W == 4) {
+                    const int64_t per = (int64_t)kWaves * R::RPW * kHeadK;
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(sampled_fwd4_kernel<R, kHeadK>),
+                                       dim3((unsigned)((n_tokens + per - 1) / per)), dim3(256), 0, (hipStream_t)stream,
+                                       hidden, table, pos_ids, neg_ids, n_tokens, (int)dim, vocab, pos_out, neg_out);
+                }
+            }))
+            return -1;
+        ASME_LAUNCH_CHECK("asme_sampled_logits_fwd");
+    }
     const dim3 grid((unsigned)((n_tokens + kWaves - 1) / kWaves));
     ASME_VPL_DISPATCH(vpl_of(dim), hipLaunchKernelGGL(sampled_fwd_kernel<VPL>, grid, dim3(256), 0,
                                                       (hipStream_t)stream, hidden, table, pos_ids, neg_ids, n_tokens,
@@ -344,6 +474,20 @@ ASME_API int asme_sampled_logits_bwd(const float* hidden, const float* table, co
                                      void* stream) {
     ASME_CHECK_ARG(hidden && table && pos_ids && neg_ids && g_pos && g_neg, "asme_sampled_logits_bwd: null");
     if (n_tokens == 0) return 0;
+    if (dim % 4 == 0 && (((uintptr_t)hidden | (uintptr_t)table | (uintptr_t)d_hidden) & 15) == 0) {
+        if (with_head_layout(dim, [&](auto layout) {
+                using R = decltype(layout);
+                if constexpr (R::W == 4) {
+                    const int64_t per = (int64_t)kWaves * R::RPW * kHeadK;
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(sampled_bwd4_kernel<R, kHeadK>),
+                                       dim3((unsigned)((n_tokens + per - 1) / per)), dim3(256), 0, (hipStream_t)stream,
+                                       hidden, table, pos_ids, neg_ids, n_tokens, (int)dim, vocab, g_pos, g_neg,
+                                       d_hidden, d_table);
+                }
+            }))
+            return -1;
+        ASME_LAUNCH_CHECK("asme_sampled_logits_bwd");
+    }
     const dim3 grid((unsigned)((n_tokens + kWaves - 1) / kWaves));
     ASME_VPL_DISPATCH(vpl_of(dim), hipLaunchKernelGGL(sampled_bwd_kernel<VPL>, grid, dim3(256), 0,
                                                       (hipStream_t)stream, hidden, table, pos_ids, neg_ids, n_tokens,

@@ -218,9 +218,11 @@ def test_residual_ln_and_gelu_dropout(asme, dev):
     assert _rel(x.grad, xr.grad) < 1e-5
 
 
-def test_sampled_head_and_bce(asme, dev):
-    torch.manual_seed(2)
-    B, L, D, V = 5, 11, 64, 101
+@pytest.mark.parametrize("D", [64, 128, 36, 130])
+def test_sampled_head_and_bce(asme, dev, D):
+    """row-layout kernels (D % 4 == 0: 16 lanes x 2 float4 at 128, x 1 at 64 / 36) and the scalar form (130)"""
+    torch.manual_seed(2 + D)
+    B, L, V = 5, 11, 101
     H = torch.randn(B, L, D)
     E = torch.randn(V, D) * 0.3
     pos, neg = torch.randint(0, V, (B, L)), torch.randint(0, V, (B, L))
