@@ -368,6 +368,66 @@ __global__ __launch_bounds__(256) void lazy_apply_v4_kernel(const int64_t* __res
     if (lane % LPR == 0) last_step[r] = step;
 }
 
+// One row per wave (D = 128 / 256: NP float2 per lane): the replay loop runs exactly the row's own steps.  The
+// float4 kernels above put 256 / D rows in a wave and replay from the OLDEST of their last steps with the newer
+// rows masked off, which wastes the difference -- with fresh ids each step and the end-of-run flush over every
+// row, replay lengths are spread wide and that waste is most of the VALU time.  STAGE: write to the compact
+// staged rows (slot order) instead of the table, leaving last_step alone (see lazy_stage_v4_kernel).
+template <int NP, bool STAGE>
+__global__ __launch_bounds__(256) void lazy_row_kernel(const int64_t* __restrict__ rows,
+                                                       const int32_t* __restrict__ count, int64_t cap,
+                                                       int32_t* __restrict__ last_step, float* __restrict__ p,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       const AdamHyper* __restrict__ hist, int32_t upto,
+                                                       float* __restrict__ sp, float* __restrict__ sm,
+                                                       float* __restrict__ sv) {
+    constexpr int D = 128 * NP;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t n = count ? (int64_t)*count : cap;
+    if (s >= n || s >= cap) return;  // wave-uniform
+    const int64_t r = rows ? rows[s] : s;
+    float2v P[NP], M[NP], Vv[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int64_t off = r * D + 2 * lane + 128 * j;
+        const float2 a = *reinterpret_cast<const float2*>(p + off);
+        const float2 b = *reinterpret_cast<const float2*>(m + off);
+        const float2 c = *reinterpret_cast<const float2*>(v + off);
+        P[j] = float2v{a.x, a.y};
+        M[j] = float2v{b.x, b.y};
+        Vv[j] = float2v{c.x, c.y};
+    }
+    const int32_t t0 = __builtin_amdgcn_readfirstlane(last_step[r]);
+    if (!STAGE && t0 >= upto) return;
+    for (int32_t t = t0 + 1; t <= upto; ++t) {
+        const AdamHyper hp = hist[t];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            if (hp.wd != 0.f)
+                adam_elem2(P[j], float2v{0.f, 0.f}, M[j], Vv[j], hp);
+            else
+                adam_decay2(P[j], M[j], Vv[j], hp);
+        }
+    }
+    float* op = STAGE ? sp + s * D : p + r * D;
+    float* om = STAGE ? sm + s * D : m + r * D;
+    float* ov = STAGE ? sv + s * D : v + r * D;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int c = 2 * lane + 128 * j;
+        *reinterpret_cast<float2*>(op + c) = make_float2(P[j].x, P[j].y);
+        *reinterpret_cast<float2*>(om + c) = make_float2(M[j].x, M[j].y);
+        *reinterpret_cast<float2*>(ov + c) = make_float2(Vv[j].x, Vv[j].y);
+    }
+    if (!STAGE && lane == 0) last_step[r] = upto;
+}
+
+#ifndef ASME_LAZY_ROW_WAVE
+#define ASME_LAZY_ROW_WAVE 1
+#endif
+inline bool row_wave_ok(int64_t dim) { return ASME_LAZY_ROW_WAVE && (dim == 128 || dim == 256); }
+
 // Staged variant (the step's unique rows read in slot order afterwards).  stage: slot s gets rows[s] brought up
 // to `upto` into the compact buffers sp/sm/sv[s] -- the table and last_step are NOT written, so a step that
 // never reaches the optimizer leaves the lazy state untouched; the row reads are random, the writes stream in
@@ -516,6 +576,18 @@ ASME_API int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, 
     ASME_CHECK_ARG(upto < hist_rows, "asme_lazy_adam_catch_up: step beyond the history capacity");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && upto >= 0 && upto < (1LL << 31), "asme_lazy_adam_catch_up: bad shape");
     if (cap == 0 || upto == 0) return 0;
+    if (row_wave_ok(dim) && v4_ok(dim, param, exp_avg, exp_avg_sq)) {
+        const dim3 g((unsigned)((cap + 3) / 4));
+        if (dim == 128)
+            hipLaunchKernelGGL((lazy_row_kernel<1, false>), g, dim3(256), 0, (hipStream_t)stream, rows, count, cap,
+                               last_step, param, exp_avg, exp_avg_sq, reinterpret_cast<const AdamHyper*>(hist),
+                               (int32_t)upto, nullptr, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((lazy_row_kernel<2, false>), g, dim3(256), 0, (hipStream_t)stream, rows, count, cap,
+                               last_step, param, exp_avg, exp_avg_sq, reinterpret_cast<const AdamHyper*>(hist),
+                               (int32_t)upto, nullptr, nullptr, nullptr);
+        ASME_LAUNCH_CHECK("asme_lazy_adam_catch_up");
+    }
     if (v4_ok(dim, param, exp_avg, exp_avg_sq)) {
         const int64_t rows_per_block = 4 * (256 / dim);
         const dim3 g4((unsigned)((cap + rows_per_block - 1) / rows_per_block));
@@ -548,6 +620,20 @@ ASME_API int asme_lazy_adam_stage(const int64_t* rows, const int32_t* count, int
                        v4_ok(dim, staged_param, staged_exp_avg, staged_exp_avg_sq),
                    "asme_lazy_adam_stage: dim must be 32/64/128/256 and every row pointer 16-B aligned");
     if (cap == 0) return 0;
+    if (row_wave_ok(dim)) {
+        const dim3 g((unsigned)((cap + 3) / 4));
+        int32_t* ls = const_cast<int32_t*>(last_step);  // (not written in STAGE mode)
+        float *pp = const_cast<float*>(param), *mm = const_cast<float*>(exp_avg), *vv = const_cast<float*>(exp_avg_sq);
+        if (dim == 128)
+            hipLaunchKernelGGL((lazy_row_kernel<1, true>), g, dim3(256), 0, (hipStream_t)stream, rows, count, cap, ls,
+                               pp, mm, vv, reinterpret_cast<const AdamHyper*>(hist), (int32_t)upto, staged_param,
+                               staged_exp_avg, staged_exp_avg_sq);
+        else
+            hipLaunchKernelGGL((lazy_row_kernel<2, true>), g, dim3(256), 0, (hipStream_t)stream, rows, count, cap, ls,
+                               pp, mm, vv, reinterpret_cast<const AdamHyper*>(hist), (int32_t)upto, staged_param,
+                               staged_exp_avg, staged_exp_avg_sq);
+        ASME_LAUNCH_CHECK("asme_lazy_adam_stage");
+    }
     const int64_t rows_per_block = 4 * (256 / dim);
     const dim3 g4((unsigned)((cap + rows_per_block - 1) / rows_per_block));
     ASME_LPR_DISPATCH(dim, hipLaunchKernelGGL(lazy_stage_v4_kernel<LPR>, g4, dim3(256), 0, (hipStream_t)stream, rows,
