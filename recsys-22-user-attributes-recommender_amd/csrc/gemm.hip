@@ -45,17 +45,16 @@ __device__ __forceinline__ int tslot(int c, int s) {
 typedef unsigned u32v2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kDrop = 0x80000000u;  // >= every chunk's record count: the load returns 0
 
-// rows r0 + 8 rg .. + 7 (chunk-relative) of this thread's column pair, by buffer loads against the chunk's record
-// range: rows past the chunk (and a column pair past the operand, off_col == kDrop) read as 0 with no branch, so
-// every block issues the same loads and the compiler's vmcnt waits stay exact (a branchy tail made it wait for
-// vmcnt(0): one block of loads in flight instead of two)
-__device__ __forceinline__ void load_cols(__amdgpu_buffer_rsrc_t rs, uint32_t ld_bytes, int64_t r0, int rg,
-                                          uint32_t off_col, float2 (&r)[8]) {
-    const uint32_t base = (uint32_t)(r0 + 8 * rg) * ld_bytes;
+// rows 8 rg .. + 7 of a token block of this thread's column pair, by buffer loads against the chunk's record range:
+// voff[q] = the thread's constant byte offset of row 8 rg + q (kDrop for a column pair past the operand), soff =
+// the block's first row within the chunk (scalar).  Rows past the chunk read 0 with no branch, so every block issues
+// the same loads and the compiler's vmcnt waits stay exact (a branchy tail made it wait for vmcnt(0): one block of
+// loads in flight instead of two), and no per-load vector address arithmetic is left in the loop.
+__device__ __forceinline__ void load_cols(__amdgpu_buffer_rsrc_t rs, const uint32_t (&voff)[8], uint32_t soff,
+                                          float2 (&r)[8]) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        const uint32_t off = off_col == kDrop ? kDrop : base + (uint32_t)q * ld_bytes + off_col;
-        const u32v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        const u32v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[q], soff, 0);
         r[q] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
     }
 }
@@ -107,7 +106,10 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(src + t_begin * ld), 0, (int)((t_end - t_begin) * ld * 4), 0x00020000);
     const uint32_t ld_bytes = (uint32_t)(ld * 4);
-    const uint32_t off_col = col0 + 2 * cg < ncols ? (uint32_t)((col0 + 2 * cg) * 4) : kDrop;
+    const bool col_ok = col0 + 2 * cg < ncols;
+    uint32_t voff[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) voff[q] = col_ok ? (uint32_t)(8 * rg + q) * ld_bytes + (uint32_t)((col0 + 2 * cg) * 4) : kDrop;
 
     floatx4 acc[4][2];
 #pragma unroll
@@ -116,7 +118,9 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     // (loads past the chunk are issued too and read zeros: unconditional, see load_cols)
-    auto load = [&](int64_t t0, float2 (&r)[8]) { load_cols(rs, ld_bytes, t0 - t_begin, rg, off_col, r); };
+    auto load = [&](int64_t t0, float2 (&r)[8]) {
+        load_cols(rs, voff, __builtin_amdgcn_readfirstlane((uint32_t)(t0 - t_begin) * ld_bytes), r);
+    };
     // the block at t0 (in r) into LDS buffer buf; r then takes the block two ahead.  No branch at all: a block past
     // the chunk holds zeros (its loads read nothing) and lands in the buffer nobody multiplies any more -- any
     // control flow here made the compiler copy the in-flight registers and wait for every load (vmcnt(0))
