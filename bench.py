@@ -42,7 +42,17 @@ def mfma_peak(name):
     return round(PEAK_BF16X6_TFS, 1) if name in BF16X6_KERNELS else PEAK_FP32_MFMA_TFS
 
 
-def roofline_entries(kstats, work, traffic):
+def committed_profile(name, config):
+    """a committed PMC summary under profiles/ (JSON with "config"), when it was taken at this exact configuration"""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        j = json.load(f)
+    return j if j.get("config") == config else {}
+
+
+def roofline_entries(kstats, work, traffic, busy=None):
     """one roofline per timed C-ABI call.  work[name] = (bound, amount) or ("gemm", flops, bytes): a GEMM's bound is
     read off its arithmetic intensity against the ridge of its MFMA ceiling and the HBM peak (the transformer's
     tall-skinny Linear GEMMs, 38-48 FLOP/B, sit below the bf16x6 ridge of 52 FLOP/B: HBM-bound)"""
@@ -69,6 +79,11 @@ def roofline_entries(kstats, work, traffic):
             ach, peak, unit = amount / secs / 1e12, mfma_peak(name), "TFLOP/s"
         else:
             ach, peak, unit = amount / secs / 1e9, PEAK_HBM_GBS, "GB/s"
+        if busy and name in busy:  # PMC: fraction of all SIMD cycles with the matrix pipe busy (MFMA utilisation)
+            extra["mfma_busy"] = busy[name]
+        if bound == "hbm" and amount / secs / 1e9 > PEAK_HBM_GBS:
+            extra["note"] = ("above the HBM peak: part of the algorithmic bytes is served from the L2 / the 256 MB "
+                             "Infinity Cache (rows read in slot order from the step's staged rows)")
         out.append({"kernel": name, "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                     "frac": round(ach / peak, 4), "traffic": traffic.get(name), "avg_ms": round(st["avg_ms"], 4),
                     "launches": st["count"], "total_ms": round(st["total_ms"], 3), **extra})
@@ -283,7 +298,8 @@ def bench_bert4rec(args, asme, dev, world, rank):
             "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4),
             "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
             "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0)}
-    rooflines = roofline_entries(timer.summary(), work, {})
+    lb = committed_profile("logits_mfma_busy.json", {"workload": args.workload, "rows": 36966, "items": V, "dim": d})
+    rooflines = roofline_entries(timer.summary(), work, {}, lb.get("mfma_busy") if B == 1024 and L == 200 else None)
     name = "KeBERT4Rec" if kebert else "BERT4Rec"
     result = {"metric": f"training sequences/sec ({name} cloze, B={B} L={L} |V|={V}, fwd+bwd+Adam)",
               "value": round(B * world * args.steps / elapsed, 2), "unit": "sequences/s", "n_gpus": world,
@@ -462,7 +478,9 @@ def main():
             tj = json.load(f)
         if tj.get("config") == {"batch": B, "seq_len": L, "items": args.items, "dim": d, "layers": args.layers}:
             traffic = tj.get("bytes_per_launch", {})
-    rooflines = roofline_entries(kstats, work, traffic)
+    mb = committed_profile("mfma_busy.json", {"batch": B, "seq_len": L, "items": args.items, "dim": d,
+                                              "layers": args.layers})
+    rooflines = roofline_entries(kstats, work, traffic, mb.get("mfma_busy"))
     roof = rooflines[0] if rooflines else None
 
     result = {
