@@ -14,26 +14,24 @@
 // conflict-free for both the ds_read_b128 lane groups and the ds_write_b128 8-lane groups.
 //
 // Layout: A = dY (T x N, row stride lda), B = X (T x K, row stride ldb), both row-major fp32.
-// Workgroup = 8 waves (two per SIMD, one workgroup per CU) in a 2x4 grid over the 128x128 tile; each wave
-// owns 64x32 = 4x2 MFMA tiles.  The LDS holds two token blocks (double buffer, 96 KiB): while the waves
-// multiply block n, they split and store block n+1 (loaded into registers two blocks earlier) into the other
-// buffer and issue the loads of block n+3 -- one barrier per block.  Waves 0-3 load dY, 4-7 load X, each
-// thread 8 tokens x 2 columns (rows of 512 contiguous bytes per wave).
+// Workgroup = 8 waves (two per SIMD, one workgroup per CU) over a super-tile of one 128x128 tile or two paired
+// ones (WgShape): 2x4 waves of 4x2 MFMA tiles, or 4x2 / 2x4 waves of 4x4.  The LDS holds two token blocks (double
+// buffer, 96 or 144 KiB): while the waves multiply block n, they split and store block n+1 (loaded into registers
+// two blocks earlier) into the other buffer and issue the loads of block n+3 -- one barrier per block.  Each loader
+// unit is 8 tokens x 2 columns of one operand (rows of 512 contiguous bytes per wave); a thread holds one unit, or
+// two in a paired super-tile's first four waves.
 #include "common.h"
 
-using namespace asme;
+#include <cstdlib>
+#include <type_traits>
 
-#ifndef ASME_WG_STAGGER
-#define ASME_WG_STAGGER 0  // 1: waves 4-7 multiply before they stage (measured 2 % slower)
-#endif
+using namespace asme;
 
 namespace {
 
 constexpr int kTile = 128;         // output tile (N and K)
 constexpr int kTT = 32;            // token rows per LDS block
 constexpr int kWgThreads = 512;
-constexpr int kPlane = kTile * 4;  // 16-B slots of one bf16 plane of one operand (128 columns x 4 slots)
-constexpr int kBuf = 6 * kPlane;   // one token block: dY planes h, m, l then X planes h, m, l
 
 // 16-B slot of (column c, token slot s): column position c ^ ((c >> 1) & 1), slot ((c >> 2) ^ 3s) mod 4.
 // ds_read_b128 (lanes {0-3,12-15,20-27}, ...: 16 consecutive columns, s = lane / 16) and ds_write_b128
@@ -59,8 +57,10 @@ __device__ __forceinline__ void load_cols(__amdgpu_buffer_rsrc_t rs, const uint3
     }
 }
 
-// the thread's 2 columns x 8 tokens, split, into token slot rg of those columns of the three planes
-__device__ __forceinline__ void store_cols(uint4* __restrict__ planes, int rg, int cg, const float2 (&r)[8]) {
+// the thread's 2 columns x 8 tokens, split, into token slot rg of those columns of the three planes (pstride
+// slots apart)
+__device__ __forceinline__ void store_cols(uint4* __restrict__ planes, int pstride, int rg, int cg,
+                                           const float2 (&r)[8]) {
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
         const float4 a = jj == 0 ? make_float4(r[0].x, r[1].x, r[2].x, r[3].x)
@@ -70,123 +70,161 @@ __device__ __forceinline__ void store_cols(uint4* __restrict__ planes, int rg, i
         const Bf3 p = split_bf3(a, b);
         const int sl = tslot(2 * cg + jj, rg);
         planes[sl] = __builtin_bit_cast(uint4, p.h);
-        planes[kPlane + sl] = __builtin_bit_cast(uint4, p.m);
-        planes[2 * kPlane + sl] = __builtin_bit_cast(uint4, p.l);
+        planes[pstride + sl] = __builtin_bit_cast(uint4, p.m);
+        planes[2 * pstride + sl] = __builtin_bit_cast(uint4, p.l);
     }
 }
 
+// A workgroup's output super-tile: TNX x TKX tiles of 128 x 128 (dY columns x X columns).  Pairing two tiles
+// (256 x 128 or 128 x 256) shares one operand's loads and bf16 split between them: per token block the workgroup
+// loads and splits 384 columns for two tiles' products instead of 256 for one (0.75x the load / split / LDS-write
+// work per MFMA).  The buffer is then 72 KiB (144 KiB double-buffered).
+template <int TNX, int TKX>
+struct WgShape {
+    static constexpr int NA = kTile * TNX, NB = kTile * TKX;  // dY / X columns
+    static constexpr int PA = NA * 4, PB = NB * 4;            // 16-B slots of one bf16 plane
+    static constexpr int BUF = 3 * (PA + PB);                 // one token block: dY planes h, m, l then X's
+    static constexpr int UA = 2 * NA, U = 2 * (NA + NB);      // loader units (column pair x 8-token row group)
+    static constexpr int WR = NA / 64, WC = 8 / WR;           // wave grid: 64 dY columns x NB / WC X columns
+    static constexpr int MJ = NB / WC / 16;                   // MFMA tiles per wave along X (4 along dY)
+    static constexpr int LDS = 2 * BUF * 16;
+    static_assert(UA % 64 == 0 && UA <= kWgThreads && U <= 2 * kWgThreads, "loader units");
+};
+
+// one loader unit: a column pair of one operand over the 8-token row group rg of every block
+struct WgUnit {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t voff[8];
+    uint32_t ld_bytes;
+    int planes, pstride, rg, cg;
+};
+
+template <int TNX, int TKX>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void weight_grad_kernel(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, int64_t T, int N, int K,
     int64_t chunk_rows, float* __restrict__ part, float* __restrict__ bias_part) {
-    extern __shared__ uint4 lds[];  // two token blocks of kBuf slots
-    // XCD-aware order: the output tiles of one token chunk are consecutive workgroups of ONE XCD (ids
+    using S = WgShape<TNX, TKX>;
+    extern __shared__ uint4 lds[];  // two token blocks of S::BUF slots
+    // XCD-aware order: the output super-tiles of one token chunk are consecutive workgroups of ONE XCD (ids
     // xcd, xcd + 8, ...), resident together, so the dY / X rows they share come from that XCD's L2 once
-    const int ntn = (N + kTile - 1) / kTile, ntiles = ntn * ((K + kTile - 1) / kTile);
+    const int nsn = (N + S::NA - 1) / S::NA, ntiles = nsn * ((K + S::NB - 1) / S::NB);
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
     const int tile = slot % ntiles;
     const int64_t chunk = (int64_t)(slot / ntiles) * 8 + xcd;
     if (chunk * chunk_rows >= T) return;
-    const int tn = tile % ntn, tk = tile / ntn;
-    const int n0 = tn * kTile, k0 = tk * kTile;
+    const int tn = tile % nsn, tk = tile / nsn;
+    const int n0 = tn * S::NA, k0 = tk * S::NB;
     const int64_t t_begin = chunk * chunk_rows;
     const int64_t t_end = min(T, t_begin + chunk_rows);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
-    const int wr = wave >> 2, wc = wave & 3;  // 64 dY columns x 32 X columns
-    // loader role: threads 0-255 dY, 256-511 X (wave-uniform: read from the first lane, so the operand's buffer
-    // resource lives in scalar registers)
-    const bool load_a = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4;
-    const int u = threadIdx.x & 255, cg = u & 63, rg = u >> 6;
-    const float* src = load_a ? A : B;
-    const int64_t ld = load_a ? lda : ldb;
-    const int col0 = load_a ? n0 : k0, ncols = load_a ? N : K;
-    const int my_planes = load_a ? 0 : 3 * kPlane;
-    const bool do_bias = bias_part != nullptr && tk == 0 && load_a;
-    float2 bsum = make_float2(0.f, 0.f);  // dY columns n0 + 2cg, + 1 over this thread's rows
-    // the chunk of this operand as a buffer resource (rows [t_begin, t_end)); this thread's column pair
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(src + t_begin * ld), 0, (int)((t_end - t_begin) * ld * 4), 0x00020000);
-    const uint32_t ld_bytes = (uint32_t)(ld * 4);
-    const bool col_ok = col0 + 2 * cg < ncols;
-    uint32_t voff[8];
+    const int wr = wave / S::WC, wc = wave % S::WC;
+    // loader units: thread t takes unit t and, when the super-tile has more than 512, unit t + 512.  Units
+    // [0, UA) are dY, the rest X; the operand is wave-uniform (UA is a multiple of 64 and the unit index is read
+    // from the first lane), so each unit's buffer resource lives in scalar registers
+    const int wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 64;
+    auto make_unit = [&](int first, int u) {
+        const bool a = first < S::UA;
+        const int v = a ? u : u - S::UA, pairs = a ? S::NA / 2 : S::NB / 2;
+        WgUnit un;
+        un.cg = v % pairs;
+        un.rg = v / pairs;
+        const int64_t ld = a ? lda : ldb;
+        un.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>((a ? A : B) + t_begin * ld), 0,
+                                                  (int)((t_end - t_begin) * ld * 4), 0x00020000);
+        un.ld_bytes = (uint32_t)(ld * 4);
+        un.planes = a ? 0 : 3 * S::PA;
+        un.pstride = a ? S::PA : S::PB;
+        const int col = (a ? n0 : k0) + 2 * un.cg;
+        const bool col_ok = col < (a ? N : K);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) voff[q] = col_ok ? (uint32_t)(8 * rg + q) * ld_bytes + (uint32_t)((col0 + 2 * cg) * 4) : kDrop;
+        for (int q = 0; q < 8; ++q)
+            un.voff[q] = col_ok ? (uint32_t)(8 * un.rg + q) * un.ld_bytes + (uint32_t)(col * 4) : kDrop;
+        return un;
+    };
+    const WgUnit u0 = make_unit(wave_u, (int)threadIdx.x);
+    const bool do_bias = bias_part != nullptr && tk == 0 && wave_u < S::UA;  // (units past 512 are never dY)
+    float2 bsum = make_float2(0.f, 0.f);  // dY columns n0 + 2 cg, + 1 over this thread's rows
 
-    floatx4 acc[4][2];
+    floatx4 acc[4][S::MJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < S::MJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     // (loads past the chunk are issued too and read zeros: unconditional, see load_cols)
-    auto load = [&](int64_t t0, float2 (&r)[8]) {
-        load_cols(rs, voff, __builtin_amdgcn_readfirstlane((uint32_t)(t0 - t_begin) * ld_bytes), r);
-    };
-    // the block at t0 (in r) into LDS buffer buf; r then takes the block two ahead.  No branch at all: a block past
-    // the chunk holds zeros (its loads read nothing) and lands in the buffer nobody multiplies any more -- any
-    // control flow here made the compiler copy the in-flight registers and wait for every load (vmcnt(0))
-    auto stage = [&](int64_t t0, float2 (&r)[8], int buf) {
-        store_cols(lds + buf * kBuf + my_planes, rg, cg, r);
-        if (do_bias) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                bsum.x += r[q].x;
-                bsum.y += r[q].y;
-            }
-        }
-        load(t0 + 2 * kTT, r);
+    auto load = [&](const WgUnit& un, int64_t t0, float2 (&r)[8]) {
+        load_cols(un.rs, un.voff, __builtin_amdgcn_readfirstlane((uint32_t)(t0 - t_begin) * un.ld_bytes), r);
     };
     auto compute = [&](int buf) {
-        const uint4* L = lds + buf * kBuf;
-        Bf3 b[2];
+        const uint4* L = lds + buf * S::BUF;
+        Bf3 b[S::MJ];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int sl = tslot(wc * 32 + j * 16 + c16, g);
-            b[j].h = __builtin_bit_cast(bf16x8, L[3 * kPlane + sl]);
-            b[j].m = __builtin_bit_cast(bf16x8, L[4 * kPlane + sl]);
-            b[j].l = __builtin_bit_cast(bf16x8, L[5 * kPlane + sl]);
+        for (int j = 0; j < S::MJ; ++j) {
+            const int sl = tslot(wc * (S::NB / S::WC) + j * 16 + c16, g);
+            b[j].h = __builtin_bit_cast(bf16x8, L[3 * S::PA + sl]);
+            b[j].m = __builtin_bit_cast(bf16x8, L[3 * S::PA + S::PB + sl]);
+            b[j].l = __builtin_bit_cast(bf16x8, L[3 * S::PA + 2 * S::PB + sl]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int sl = tslot(wr * 64 + i * 16 + c16, g);
             Bf3 a;
             a.h = __builtin_bit_cast(bf16x8, L[sl]);
-            a.m = __builtin_bit_cast(bf16x8, L[kPlane + sl]);
-            a.l = __builtin_bit_cast(bf16x8, L[2 * kPlane + sl]);
+            a.m = __builtin_bit_cast(bf16x8, L[S::PA + sl]);
+            a.l = __builtin_bit_cast(bf16x8, L[2 * S::PA + sl]);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf3(a, b[j], acc[i][j]);
+            for (int j = 0; j < S::MJ; ++j) acc[i][j] = mfma_bf3(a, b[j], acc[i][j]);
         }
     };
-    float2 r0[8], r1[8];  // two blocks in flight (the HBM latency outlasts one block's MFMAs)
-    load(t_begin, r0);
-    load(t_begin + kTT, r1);
-    stage(t_begin, r0, 0);
-    __syncthreads();
-    // pairs of blocks with no exit in between (buf 0 holds block i, r1 block i + 1, r0 block i + 2 at the top of a
-    // trip); an odd last block is multiplied after the loop.  Waves 4-7 may run each half's two parts in the
-    // opposite order (ASME_WG_STAGGER): stage and compute touch different buffers.
     const int64_t nblk = (t_end - t_begin + kTT - 1) / kTT;
-    const bool late = ASME_WG_STAGGER && wave >= 4;
-    int64_t i = 0;
-    for (; i + 2 <= nblk; i += 2) {
-        const int64_t t0 = t_begin + i * kTT;
-        if (late) {
-            compute(0);
-            stage(t0 + kTT, r1, 1);
-        } else {
-            stage(t0 + kTT, r1, 1);
-            compute(0);
-        }
+    // The block loop, compiled once per loader role (one unit or two): the role is wave-uniform and chosen outside
+    // the loop, so the loop body has no branch -- any control flow around the loads made the compiler copy the
+    // in-flight registers and wait for every load (vmcnt(0)).
+    auto run = [&](auto two) {
+        constexpr bool kTwo = decltype(two)::value;
+        const WgUnit u1 = kTwo ? make_unit(wave_u + kWgThreads, (int)threadIdx.x + kWgThreads) : u0;
+        // the block at t0 (in r) into LDS buffer buf; r then takes the block two ahead.  A block past the chunk
+        // holds zeros (its loads read nothing) and lands in the buffer nobody multiplies any more.
+        auto stage = [&](int64_t t0, float2 (&r)[8], float2 (&q)[8], int buf) {
+            store_cols(lds + buf * S::BUF + u0.planes, u0.pstride, u0.rg, u0.cg, r);
+            if constexpr (kTwo) store_cols(lds + buf * S::BUF + u1.planes, u1.pstride, u1.rg, u1.cg, q);
+            if (do_bias) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    bsum.x += r[j].x;
+                    bsum.y += r[j].y;
+                }
+            }
+            load(u0, t0 + 2 * kTT, r);
+            if constexpr (kTwo) load(u1, t0 + 2 * kTT, q);
+        };
+        float2 r0[8], r1[8], q0r[8], q1r[8];  // two blocks in flight per unit (q: the second unit, if any)
+        load(u0, t_begin, r0);
+        if constexpr (kTwo) load(u1, t_begin, q0r);
+        load(u0, t_begin + kTT, r1);
+        if constexpr (kTwo) load(u1, t_begin + kTT, q1r);
+        stage(t_begin, r0, q0r, 0);
         __syncthreads();
-        if (late) {
+        // pairs of blocks with no exit in between (buf 0 holds block i, r1 block i + 1, r0 block i + 2 at the top
+        // of a trip); an odd last block is multiplied after the loop
+        int64_t i = 0;
+        for (; i + 2 <= nblk; i += 2) {
+            const int64_t t0 = t_begin + i * kTT;
+            stage(t0 + kTT, r1, q1r, 1);
+            compute(0);
+            __syncthreads();
+            stage(t0 + 2 * kTT, r0, q0r, 0);
             compute(1);
-            stage(t0 + 2 * kTT, r0, 0);
-        } else {
-            stage(t0 + 2 * kTT, r0, 0);
-            compute(1);
+            __syncthreads();
         }
-        __syncthreads();
+        if (i < nblk) compute(0);
+    };
+    if constexpr (S::U > kWgThreads) {
+        if (wave_u + kWgThreads < S::U) run(std::true_type{});
+        else run(std::false_type{});
+    } else {
+        run(std::false_type{});
     }
-    if (i < nblk) compute(0);
     // partial slab: part[chunk][n][k]; lane holds rows n = ... + 4g + q, column k = ... + c16
     // chunk slab: [N x K dW partial | N db partial (when db is requested)]
     const int64_t slab = (int64_t)N * K + (bias_part != nullptr ? N : 0);
@@ -194,22 +232,23 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < S::MJ; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int n = n0 + wr * 64 + i * 16 + 4 * g + q;
-                const int k = k0 + wc * 32 + j * 16 + c16;
+                const int k = k0 + wc * (S::NB / S::WC) + j * 16 + c16;
                 if (n < N && k < K) P[(int64_t)n * K + k] = acc[i][j][q];
             }
     if (bias_part != nullptr && tk == 0) {  // the 4 row groups' column sums, in row-group order
+        constexpr int kPairs = S::NA / 2;
         float2* red = reinterpret_cast<float2*>(lds);  // (the loop's last barrier retired every LDS read)
-        if (load_a) red[rg * 64 + cg] = bsum;
+        if (wave_u < S::UA) red[u0.rg * kPairs + u0.cg] = bsum;
         __syncthreads();
-        if (threadIdx.x < 64 && n0 + 2 * (int)threadIdx.x < N) {
+        if (threadIdx.x < kPairs && n0 + 2 * (int)threadIdx.x < N) {
             float2 s = red[threadIdx.x];
 #pragma unroll
             for (int q = 1; q < 4; ++q) {
-                const float2 v = red[q * 64 + threadIdx.x];
+                const float2 v = red[q * kPairs + threadIdx.x];
                 s.x += v.x;
                 s.y += v.y;
             }
@@ -258,9 +297,32 @@ struct Plan {
     int64_t nchunks, chunk_rows;
 };
 
+// super-tile shape for an N x K gradient: pair two 128-column tiles along whichever side has an even count of them
+// (the FFN's 512 x 128 and 128 x 512), else one tile per workgroup.  ASME_WG_PAIR=0 disables pairing.
+struct Pairing {
+    int tnx, tkx;
+};
+
+Pairing pick_pairing(int64_t N, int64_t K) {
+    static const bool enabled = [] {
+        const char* e = std::getenv("ASME_WG_PAIR");
+        return !(e && e[0] == '0');
+    }();
+    const int64_t ntn = (N + kTile - 1) / kTile, ntk = (K + kTile - 1) / kTile;
+    if (enabled && ntn % 2 == 0) return {2, 1};
+    if (enabled && ntk % 2 == 0) return {1, 2};
+    return {1, 1};
+}
+
+int64_t super_tiles(int64_t N, int64_t K) {
+    const Pairing pr = pick_pairing(N, K);
+    return ((N + kTile * pr.tnx - 1) / (kTile * pr.tnx)) * ((K + kTile * pr.tkx - 1) / (kTile * pr.tkx));
+}
+
 Plan make_plan(int64_t T, int64_t N, int64_t K) {
-    const int64_t tiles = ((N + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-    // one workgroup per CU (96 KiB of LDS each): chunks a multiple of 8 (one per XCD lane), tiles x chunks <= 256
+    const int64_t tiles = super_tiles(N, K);
+    // one workgroup per CU (96 or 144 KiB of LDS each): chunks a multiple of 8 (one per XCD lane), tiles x chunks
+    // <= 256
     const int64_t want = std::max<int64_t>(8, (256 / tiles) / 8 * 8);
     int64_t rows = (T + want - 1) / want;
     rows = std::max<int64_t>(kTT, ((rows + kTT - 1) / kTT) * kTT);
@@ -269,6 +331,22 @@ Plan make_plan(int64_t T, int64_t N, int64_t K) {
                              kTT * kTT;
     rows = std::min<int64_t>(rows, std::max<int64_t>(kTT, max_rows));
     return {(T + rows - 1) / rows, rows};  // chunks holding tokens; the grid rounds them up to a multiple of 8
+}
+
+template <int TNX, int TKX>
+hipError_t launch_weight_grad(dim3 grid, hipStream_t s, const float* dy, int64_t ld_dy, const float* x,
+                              int64_t ld_x, int64_t T, int N, int K, int64_t chunk_rows, float* part, float* bpart) {
+    static bool attr = false;  // 96 / 144 KiB of dynamic LDS: opt in once per shape
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)weight_grad_kernel<TNX, TKX>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, WgShape<TNX, TKX>::LDS);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    constexpr int kLds = WgShape<TNX, TKX>::LDS;
+    weight_grad_kernel<TNX, TKX><<<grid, dim3(kWgThreads), kLds, s>>>(dy, ld_dy, x, ld_x, T, N, K, chunk_rows, part,
+                                                                      bpart);
+    return hipSuccess;
 }
 
 }  // namespace
@@ -295,17 +373,15 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
     hipStream_t s = (hipStream_t)stream;
     float* part = workspace;
     float* bpart = db ? workspace : nullptr;  // (a flag: the bias partials sit in each chunk's slab)
-    const int64_t ntiles = ((out_features + kTile - 1) / kTile) * ((in_features + kTile - 1) / kTile);
-    const dim3 grid((unsigned)(ntiles * ((p.nchunks + 7) / 8) * 8));
-    static bool attr = false;  // 96 KiB of dynamic LDS: opt in once
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)weight_grad_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kBuf * 16);
-        if (e != hipSuccess) return hip_status(e, "asme_linear_weight_grad: LDS opt-in");
-        attr = true;
-    }
-    hipLaunchKernelGGL(weight_grad_kernel, grid, dim3(kWgThreads), 2 * kBuf * 16, s, dy, ld_dy, x, ld_x, n_tokens,
-                       (int)out_features, (int)in_features, p.chunk_rows, part, bpart);
+    const dim3 grid((unsigned)(super_tiles(out_features, in_features) * ((p.nchunks + 7) / 8) * 8));
+    const Pairing pr = pick_pairing(out_features, in_features);
+    const int N = (int)out_features, K = (int)in_features;
+    const hipError_t e =
+        pr.tnx == 2 ? launch_weight_grad<2, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart)
+        : pr.tkx == 2
+            ? launch_weight_grad<1, 2>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart)
+            : launch_weight_grad<1, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart);
+    if (e != hipSuccess) return hip_status(e, "asme_linear_weight_grad: LDS opt-in");
     const int64_t width_w = out_features * in_features, width_b = db ? out_features : 0;
     hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width_w + width_b + kRedCols - 1) / kRedCols)), dim3(1024), 0,
                        s, part, p.nchunks, width_w, dw, width_b, db, accumulate);

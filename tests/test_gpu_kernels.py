@@ -469,9 +469,11 @@ def test_sharded_module_single_rank_matches_unsharded(asme, dev):
 
 
 @pytest.mark.parametrize("T,N,K", [(1, 4, 4), (33, 128, 128), (1000, 384, 128), (4099, 128, 512), (70000, 512, 128),
-                                   (517, 36, 200)])
+                                   (517, 36, 200), (2000, 256, 256), (2001, 132, 384), (95, 200, 36), (300, 128, 260)])
 def test_linear_weight_grad(asme, dev, T, N, K):
-    """dW = dY^T X and db = sum dY (split-token MFMA kernel) vs an fp64 reference."""
+    """dW = dY^T X and db = sum dY (split-token MFMA kernel) vs an fp64 reference.  The shapes cover single tiles,
+    tiles paired along N (N / 128 even: 512 x 128, 256 x 256, ragged 132 and 200) and along K (128 x 512), and
+    odd tile counts (384 x 128, 128 x 260)."""
     torch.manual_seed(T + N + K)
     x = torch.randn(T, K, device=dev)
     w = torch.randn(N, K, device=dev, requires_grad=True)
