@@ -320,10 +320,11 @@ int asme_catalog_count_above(const float* H, int64_t ld_h, int64_t nq, int64_t d
 
 /* ---- Deterministic table gradient (csrc/sharding.hip; SURVEY §8b embedding_scatter_add_bwd
  * mode=deterministic; reference: autograd embedding_dense_backward).  Occurrences grouped per unique row
- * by a stable radix sort, then ordered sums: bit-reproducible, no atomics, no zero fill. */
+ * by a counting sort (each slot's list then put in occurrence order: the arrays of a stable sort), then
+ * ordered sums: bit-reproducible, no float atomics, no zero fill. */
 int64_t asme_occurrence_csr_workspace(int64_t n);
-/* inverse (n int64 slots < cap) -> order (n int32 occurrences grouped by slot, increasing within a slot),
- * sorted_slot (n int32, slot of order[i]), seg_off (cap + 1 int32) */
+/* inverse (n int64 slots < cap <= n) -> order (n int32 occurrences grouped by slot, increasing within a slot;
+ * slot-less occurrences last), sorted_slot (n int32, slot of order[i], cap for none), seg_off (cap + 1 int32) */
 int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap, void* workspace, int64_t workspace_bytes,
                         int32_t* order, int32_t* sorted_slot, int32_t* seg_off, void* stream);
 int64_t asme_table_grad_workspace(int64_t n, int64_t dim);

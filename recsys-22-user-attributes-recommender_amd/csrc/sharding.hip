@@ -10,7 +10,6 @@
 // representative flags assigns compact slots in first-occurrence order.  The map is then rewritten
 // to hold the slot (row_slot for the Adam kernel) and must be reset with asme_dedup_reset.
 #include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include "common.h"
 
@@ -277,32 +276,97 @@ ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* 
 // Deterministic table gradient (SURVEY §8b `embedding_scatter_add_bwd(..., mode=deterministic)`, A19).
 // Reference: autograd's embedding_dense_backward sums every occurrence's gradient row into the table
 // row.  Here the step's occurrences (the dedup inverse, slot per occurrence) are grouped by slot with a
-// stable radix sort (slot, occurrence) -> per-slot lists in increasing occurrence order; each unique
-// row's gradient is then the ordered sum over its list (no atomics: bit-reproducible run to run, and
-// the compact gradient buffer needs no zero fill).
+// counting sort -> per-slot lists in increasing occurrence order; each unique row's gradient is then the
+// ordered sum over its list (no float atomics: bit-reproducible run to run, and the compact gradient buffer
+// needs no zero fill).
 namespace {
 
-// occurrences without a slot (inverse -1: id outside the table) get the sentinel key cap: sorted last
-__global__ void csr_prep_kernel(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
-                                int32_t* __restrict__ keys, int32_t* __restrict__ vals) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// Counting sort of the occurrences by slot.  Key of occurrence i: its slot, or cap for an occurrence without one
+// (inverse -1: an id outside the table), which sorts last.  (1) per-key counts (integer atomics), (2) exclusive
+// scan -> seg_off, (3) scatter: each occurrence takes a position of its key's range by an atomic count-down (any
+// order), (4) each range is then put in increasing occurrence order -- the same arrays a stable sort gives, so the
+// sums are bit-reproducible.  Ranges of up to kShortSeg by their own thread (insertion sort), longer ones (popular
+// items) by a workgroup that ranks every element against the range (listed by (4), done by (5)).
+constexpr int kShortSeg = 16;
+
+__device__ __forceinline__ int32_t occ_key(const int64_t* __restrict__ inverse, int64_t i, int64_t cap) {
     const int64_t k = inverse[i];
-    keys[i] = (int32_t)(k >= 0 && k < cap ? k : cap);
-    vals[i] = (int32_t)i;
+    return (int32_t)(k >= 0 && k < cap ? k : cap);
 }
 
-// seg_off[k] = first sorted position of slot k, seg_off[last + 1] = end of the last slot's list
-__global__ void csr_bounds_kernel(const int32_t* __restrict__ keys, int64_t n, int64_t cap,
-                                  int32_t* __restrict__ seg_off) {
+__global__ void csr_count_kernel(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
+                                 int32_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(cnt + occ_key(inverse, i, cap), 1);
+}
+
+__global__ void csr_scatter_kernel(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
+                                   const int32_t* __restrict__ seg_off, int32_t* __restrict__ cnt,
+                                   int32_t* __restrict__ order, int32_t* __restrict__ sorted_slot) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int32_t k = keys[i];
-    if (i == 0 || keys[i - 1] != k) {
-        if (k < cap) seg_off[k] = (int32_t)i;
-        if (i > 0 && keys[i - 1] < cap) seg_off[keys[i - 1] + 1] = (int32_t)i;
+    const int32_t k = occ_key(inverse, i, cap);
+    const int32_t pos = seg_off[k] + atomicSub(cnt + k, 1) - 1;
+    order[pos] = (int32_t)i;
+    sorted_slot[pos] = k;
+}
+
+// one thread per key: ranges of 2..kShortSeg sorted in registers (an odd-even transposition network over a padded
+// array: static indices only), longer ones appended to longs[1..] (longs[0] = their count)
+__global__ void csr_order_kernel(const int32_t* __restrict__ seg_off, int64_t n, int64_t cap,
+                                 int32_t* __restrict__ order, int32_t* __restrict__ longs) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > cap) return;
+    const int32_t b = seg_off[k];
+    const int len = (k < cap ? seg_off[k + 1] : (int32_t)n) - b;
+    if (len < 2) return;
+    if (len == 2) {
+        const int32_t x = order[b], y = order[b + 1];
+        if (x > y) {
+            order[b] = y;
+            order[b + 1] = x;
+        }
+        return;
     }
-    if (i == n - 1 && k < cap) seg_off[k + 1] = (int32_t)n;
+    if (len > kShortSeg) {
+        longs[1 + atomicAdd(longs, 1)] = (int32_t)k;
+        return;
+    }
+    int32_t v[kShortSeg];
+#pragma unroll
+    for (int j = 0; j < kShortSeg; ++j) v[j] = j < len ? order[b + j] : INT32_MAX;
+#pragma unroll
+    for (int r = 0; r < kShortSeg; ++r)
+#pragma unroll
+        for (int j = r & 1; j + 1 < kShortSeg; j += 2) {
+            const int32_t lo = min(v[j], v[j + 1]), hi = max(v[j], v[j + 1]);
+            v[j] = lo;
+            v[j + 1] = hi;
+        }
+#pragma unroll
+    for (int j = 0; j < kShortSeg; ++j)
+        if (j < len) order[b + j] = v[j];
+}
+
+// long ranges: one workgroup each; an element's place is the number of smaller occurrence indices in its range
+__global__ __launch_bounds__(256) void csr_long_kernel(const int32_t* __restrict__ seg_off, int64_t n, int64_t cap,
+                                                       const int32_t* __restrict__ longs, int32_t* __restrict__ order,
+                                                       int32_t* __restrict__ tmp) {
+    const int nl = longs[0];
+    for (int t = blockIdx.x; t < nl; t += gridDim.x) {
+        const int64_t k = longs[1 + t];
+        const int32_t b = seg_off[k];
+        const int len = (k < cap ? seg_off[k + 1] : (int32_t)n) - b;
+        for (int e = threadIdx.x; e < len; e += blockDim.x) {
+            const int32_t x = order[b + e];
+            int r = 0;
+            for (int j = 0; j < len; ++j) r += order[b + j] < x ? 1 : 0;
+            tmp[b + r] = x;
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < len; e += blockDim.x) order[b + e] = tmp[b + e];
+        __syncthreads();
+    }
 }
 
 constexpr int kMaxContrib = 4;
@@ -432,49 +496,44 @@ __global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restric
     }
 }
 
-int end_bit_for(int64_t cap) {
-    int b = 1;
-    while (((int64_t)1 << b) < cap + 1 && b < 31) ++b;
-    return b;
-}
 
 }  // namespace
 
-// rocprim picks a block-sort + merge-sort path below 2^20 items (10 merge passes at 6e5 occurrences); the
-// limit 0 forces Onesweep LSD radix (one histogram pass + one pass per 8-bit digit of the slot range)
-using OccurrenceSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                         rocprim::default_config, 0>;
-
 ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
     size_t temp = 0;
-    (void)rocprim::radix_sort_pairs<OccurrenceSortConfig>(nullptr, temp, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                                          (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0,
-                                                          31);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (int32_t*)nullptr, (int32_t*)nullptr, (int)(n + 1));
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    return (int64_t)(2 * up((size_t)n * sizeof(int32_t)) + up(temp));
+    // per-key counts (n + 1), long-range list (n + 2), rank scratch (n), scan temp
+    return (int64_t)(up((size_t)(n + 1) * 4) + up((size_t)(n + 2) * 4) + up((size_t)n * 4) + up(temp));
 }
 
-// inverse (n int64 slots < cap) -> order (n int32 occurrence indices grouped by slot, increasing within a
-// slot), sorted_slot (n int32: the slot of order[i]) and seg_off (cap + 1 int32; entries beyond the number
-// of slots + 1 are left untouched)
+// inverse (n int64 slots < cap <= n) -> order (n int32 occurrence indices grouped by slot, increasing within a
+// slot; occurrences without a slot last), sorted_slot (n int32: the slot of order[i], cap for none) and seg_off
+// (cap + 1 int32: first sorted position of each slot, slots past the last one at the end of the slotted ones)
 ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap, void* workspace,
                                  int64_t workspace_bytes, int32_t* order, int32_t* sorted_slot, int32_t* seg_off,
                                  void* stream) {
     ASME_CHECK_ARG(inverse && workspace && order && sorted_slot && seg_off, "asme_occurrence_csr: null pointer");
-    ASME_CHECK_ARG(n >= 1 && n < (int64_t)1 << 31 && cap < (int64_t)1 << 31, "asme_occurrence_csr: bad size");
+    ASME_CHECK_ARG(n >= 1 && n < (int64_t)1 << 31 && cap >= 0 && cap <= n, "asme_occurrence_csr: bad size");
     ASME_CHECK_ARG(workspace_bytes >= asme_occurrence_csr_workspace(n), "asme_occurrence_csr: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     char* ws = (char*)workspace;
-    int32_t* keys = (int32_t*)ws;
-    int32_t* vals = (int32_t*)(ws + up((size_t)n * 4));
-    void* temp = ws + 2 * up((size_t)n * 4);
-    size_t temp_bytes = (size_t)workspace_bytes - 2 * up((size_t)n * 4);
-    hipLaunchKernelGGL(csr_prep_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, keys, vals);
-    if (rocprim::radix_sort_pairs<OccurrenceSortConfig>(temp, temp_bytes, keys, sorted_slot, vals, order, (size_t)n,
-                                                         0, end_bit_for(cap), s) != hipSuccess)
-        return hip_status(hipErrorUnknown, "asme_occurrence_csr: sort");
-    hipLaunchKernelGGL(csr_bounds_kernel, dim3(nblk(n)), dim3(256), 0, s, sorted_slot, n, cap, seg_off);
+    int32_t* cnt = (int32_t*)ws;
+    int32_t* longs = (int32_t*)(ws + up((size_t)(n + 1) * 4));
+    int32_t* tmp = (int32_t*)((char*)longs + up((size_t)(n + 2) * 4));
+    void* temp = (char*)tmp + up((size_t)n * 4);
+    size_t temp_bytes = (size_t)workspace_bytes - ((char*)temp - ws);
+    // counts of keys 0..cap and the long-range counter, zeroed together (longs follows cnt)
+    if (hipMemsetAsync(cnt, 0, (char*)longs - ws + 4, s) != hipSuccess)
+        return hip_status(hipGetLastError(), "asme_occurrence_csr: zero");
+    hipLaunchKernelGGL(csr_count_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, cnt);
+    if (hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, cnt, seg_off, (int)(cap + 1), s) != hipSuccess)
+        return hip_status(hipErrorUnknown, "asme_occurrence_csr: scan");
+    hipLaunchKernelGGL(csr_scatter_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, seg_off, cnt, order,
+                       sorted_slot);
+    hipLaunchKernelGGL(csr_order_kernel, dim3(nblk(cap + 1)), dim3(256), 0, s, seg_off, n, cap, order, longs);
+    hipLaunchKernelGGL(csr_long_kernel, dim3(64), dim3(256), 0, s, seg_off, n, cap, longs, order, tmp);
     ASME_LAUNCH_CHECK("asme_occurrence_csr");
 }
 

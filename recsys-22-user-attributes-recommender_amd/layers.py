@@ -44,7 +44,7 @@ def _p(module: nn.Module, training: bool) -> float:
 def key_valid_mask(padding_mask: Optional[torch.Tensor], shape) -> Optional[torch.Tensor]:
     if padding_mask is None:
         return None
-    return padding_mask.reshape(shape[0], shape[1]).to(torch.uint8).contiguous()
+    return ops.as_u8(padding_mask.reshape(shape[0], shape[1]))
 
 
 # ------------------------------------------------------------------------------------ embeddings

@@ -33,6 +33,13 @@ def new_seed(p: float) -> int:
     return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
 
 
+def as_u8(mask: torch.Tensor) -> torch.Tensor:
+    """a 0/1 mask as contiguous uint8 bytes: a bool mask is reinterpreted in place (same bytes, no copy kernel)"""
+    if mask.dtype == torch.bool:
+        return mask.contiguous().view(torch.uint8)
+    return mask.to(torch.uint8).contiguous()
+
+
 def _f32(t: torch.Tensor) -> torch.Tensor:
     if t.dtype != torch.float32:
         raise TypeError(f"expected float32 tensor, got {t.dtype}")
@@ -150,7 +157,9 @@ class SparseTablePlan:
         self.slot_map = slot_map
         self.unique = torch.empty(n, device=dev, dtype=torch.int64)
         inverse = torch.empty(n, device=dev, dtype=torch.int64)
-        self.count = torch.zeros(1, device=dev, dtype=torch.int32)
+        # (asme_dedup_ids always writes the count)
+        self.count = torch.empty(1, device=dev, dtype=torch.int32) if n > 0 else torch.zeros(1, device=dev,
+                                                                                          dtype=torch.int32)
         if n > 0:
             ws_bytes = int(_lib.load().asme_dedup_workspace_bytes(n))
             ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
@@ -245,7 +254,7 @@ class SparseTablePlan:
 
     def _reduce_contributions(self) -> torch.Tensor:
         """deterministic table gradient: occurrences grouped by row (stable radix sort), sums in a fixed
-        order (asme_occurrence_csr + asme_table_grad_reduce); no atomics, no zero fill"""
+        order (asme_occurrence_csr + asme_table_grad_reduce); no float atomics, no zero fill"""
         dev = self.unique.device
         n, d = self.capacity, self.dim
         if n == 0:
@@ -375,7 +384,8 @@ class _EmbeddingFn(torch.autograd.Function):
         if ctx.has[0] and ctx.needs_input_grad[2]:
             L = spec.seq_len
             B = T // L
-            g_pos = torch.zeros_like(pos)
+            # rows [0, L) are written (accumulate = 0); only rows past the sequence length need zeros
+            g_pos = torch.empty_like(pos) if pos.shape[0] == L else torch.zeros_like(pos)
             nch = max(1, min(32, B))
             ws = torch.empty(nch, L, D, device=dev, dtype=torch.float32)
             call("asme_position_grad", ptr(d_rows), B, L, D, ptr(ws), nch, ptr(g_pos), 0, stream())
@@ -748,7 +758,7 @@ class _NarmAttendFn(torch.autograd.Function):
     def forward(ctx, p1, p2, v, hs, mask):
         N, S, H = hs.shape
         p1, p2, v, hs = _f32(p1), _f32(p2), _f32(v), _f32(hs)
-        m = mask.to(torch.uint8).contiguous()
+        m = as_u8(mask)
         out = torch.empty(N, H, device=hs.device, dtype=torch.float32)
         alpha = torch.empty(N, S, device=hs.device, dtype=torch.float32)
         call("asme_narm_attend_fwd", ptr(p1), ptr(p2), ptr(v), ptr(hs), ptr(m), N, S, H, ptr(out), ptr(alpha),
@@ -1035,7 +1045,7 @@ class _SASRecBCEFn(torch.autograd.Function):
     def forward(ctx, pos, neg, mask):
         pos_shape, neg_shape = pos.shape, neg.shape
         pos, neg = _f32(pos).reshape(-1), _f32(neg).reshape(-1)
-        m = mask.reshape(-1).to(torch.uint8).contiguous()
+        m = as_u8(mask.reshape(-1))
         T = pos.numel()
         nparts = max(1, min(1024, (T + 255) // 256))
         ws = torch.empty(nparts, 2, device=pos.device, dtype=torch.float32)

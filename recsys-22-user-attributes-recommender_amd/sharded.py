@@ -202,7 +202,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         st, own, compact, (inv_seq, inv_pos, inv_neg) = self._fetch([input_seq, pos, neg], train=True)
         compact.requires_grad_(True)
         U = compact.shape[0]
-        # its gradient: the heads' contributions summed per compact row in a fixed order (no atomics, no zero fill)
+        # its gradient: the heads' contributions summed per compact row in a fixed order (no float atomics, no zero fill)
         cplan = ops.SparseTablePlan.identity(U, [inv_seq, inv_pos, inv_neg], compact.shape[1])
         compact._asme_table_grad = ops.TableGrad()
         compact._asme_table_grad.plan = cplan

@@ -367,6 +367,42 @@ def test_deterministic_table_grad(asme, dev, D):
     assert (a.double() - want).abs().max().item() < 1e-4 * max(1.0, want.abs().max().item())
 
 
+@pytest.mark.parametrize("n,cap", [(1, 1), (7, 7), (5000, 5000), (70000, 70000), (3000, 2000)])
+def test_occurrence_csr_equals_stable_sort(asme, dev, n, cap):
+    """asme_occurrence_csr (counting sort + per-range ordering) == a stable sort of the occurrences by slot:
+    order, sorted_slot (cap for slot-less occurrences, sorted last) and seg_off, exactly.  Slots with one, two,
+    a few and thousands of occurrences (ranges longer than the register-sorted ones) and slot-less ones."""
+    L = asme._lib
+    g = torch.Generator().manual_seed(n + cap)
+    u = max(1, cap // 3)
+    inv = torch.randint(0, u, (n,), generator=g)
+    if n > 100:
+        inv[torch.rand(n, generator=g) < 0.3] = 0          # one hot slot
+        inv[torch.rand(n, generator=g) < 0.05] = -1        # slot-less
+        inv[torch.rand(n, generator=g) < 0.02] = min(5, u - 1)
+    seen = torch.zeros(u, dtype=torch.bool)
+    seen[inv[inv >= 0]] = True
+    remap = torch.cumsum(seen.to(torch.int64), 0) - 1      # dense slots 0..U-1 (every slot occurs)
+    inv = torch.where(inv >= 0, remap[inv.clamp(min=0)], inv)
+    U = int(seen.sum())
+    key = torch.where(inv >= 0, inv, torch.full_like(inv, cap))
+    want_order = torch.sort(key, stable=True).indices.to(torch.int32)
+    want_slot = key[want_order.long()].to(torch.int32)
+    counts = torch.bincount(key, minlength=cap + 1)
+    want_off = (torch.cumsum(counts, 0) - counts).to(torch.int32)
+    inv_d = inv.to(dev)
+    nb = int(L.load().asme_occurrence_csr_workspace(n))
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    slot = torch.empty(n, dtype=torch.int32, device=dev)
+    off = torch.empty(cap + 1, dtype=torch.int32, device=dev)
+    L.call("asme_occurrence_csr", L.ptr(inv_d), n, cap, L.ptr(ws), nb, L.ptr(order), L.ptr(slot), L.ptr(off),
+           L.stream())
+    assert torch.equal(order.cpu(), want_order)
+    assert torch.equal(slot.cpu(), want_slot)
+    assert torch.equal(off.cpu()[:U + 1], want_off[:U + 1])
+
+
 def test_lazy_adam_bit_exact_vs_dense(asme, dev):
     """Exact catch-up: lazily replayed zero-gradient steps == the dense row update every step, bitwise."""
     torch.manual_seed(6)

@@ -8,7 +8,7 @@ import sys
 d = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else ""
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(f"{d}/*counter_collection.csv"):
+for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
         if pat not in k:

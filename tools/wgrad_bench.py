@@ -27,6 +27,7 @@ def bench(fn, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--shapes", default="qkv,out,w1,w2")
     a = ap.parse_args()
     asme = __graft_entry__.load_package()
     dev = torch.device("cuda:0")
@@ -35,6 +36,8 @@ def main():
     tot = 0.0
     torch.manual_seed(0)
     for name, (k, n) in shapes.items():
+        if name not in a.shapes.split(","):
+            continue
         x = torch.randn(T, k, device=dev)
         dy = torch.randn(T, n, device=dev)
         nb = int(asme._lib.load().asme_linear_weight_grad_workspace(T, n, k))
