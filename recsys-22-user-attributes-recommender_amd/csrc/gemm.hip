@@ -58,40 +58,20 @@ __device__ __forceinline__ void load_cols(__amdgpu_buffer_rsrc_t rs, const uint3
 }
 
 // the thread's 2 columns x 8 tokens, split, into token slot rg of those columns of the three planes (pstride
-// slots apart).  The split runs on each token's loaded column pair as it lies in its register pair (packed
-// v_cvt_pk_bf16_f32 / v_pk_add_f32), and byte permutes then gather each column's 8 tokens: the loaded registers are
-// consumed in place (splitting by column made the compiler re-pair them with moves at the loop latch, which waits
-// for the loads in flight).  Same values as split_bf3.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_bf16(f32x2 v) {
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
-}
-__device__ __forceinline__ f32x2 unpk_bf16(uint32_t p) {
-    return f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
-}
+// slots apart)
 __device__ __forceinline__ void store_cols(uint4* __restrict__ planes, int pstride, int rg, int cg,
                                            const float2 (&r)[8]) {
-    uint32_t H[8], M[8], Lw[8];  // per token: (column 0 | column 1 << 16) of each plane
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const f32x2 x = {r[q].x, r[q].y};
-        H[q] = pk_bf16(x);
-        const f32x2 rr = x - unpk_bf16(H[q]);
-        M[q] = pk_bf16(rr);
-        Lw[q] = pk_bf16(rr - unpk_bf16(M[q]));
-    }
-    auto col = [](const uint32_t (&P)[8], uint32_t sel) {
-        return make_uint4(__builtin_amdgcn_perm(P[1], P[0], sel), __builtin_amdgcn_perm(P[3], P[2], sel),
-                          __builtin_amdgcn_perm(P[5], P[4], sel), __builtin_amdgcn_perm(P[7], P[6], sel));
-    };
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
-        const uint32_t sel = jj == 0 ? 0x05040100u : 0x07060302u;  // low / high halves of two tokens
+        const float4 a = jj == 0 ? make_float4(r[0].x, r[1].x, r[2].x, r[3].x)
+                                 : make_float4(r[0].y, r[1].y, r[2].y, r[3].y);
+        const float4 b = jj == 0 ? make_float4(r[4].x, r[5].x, r[6].x, r[7].x)
+                                 : make_float4(r[4].y, r[5].y, r[6].y, r[7].y);
+        const Bf3 p = split_bf3(a, b);
         const int sl = tslot(2 * cg + jj, rg);
-        planes[sl] = col(H, sel);
-        planes[pstride + sl] = col(M, sel);
-        planes[2 * pstride + sl] = col(Lw, sel);
+        planes[sl] = __builtin_bit_cast(uint4, p.h);
+        planes[pstride + sl] = __builtin_bit_cast(uint4, p.m);
+        planes[2 * pstride + sl] = __builtin_bit_cast(uint4, p.l);
     }
 }
 
@@ -277,188 +257,6 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     }
 }
 
-// ---- Warp-specialised form (default): 4 producer waves load, split and store the token blocks into the LDS
-// image; 8 consumer waves only read fragments and multiply.  One workgroup barrier per block hands a buffer over
-// (producers write block i + 1 while the consumers multiply block i), so the loads, the VALU split and the LDS
-// stores of the producers issue in the MFMA gaps of the consumers on the same SIMD instead of alternating with the
-// MFMAs in every wave (the single-role kernel above: measured MFMA busy 0.40, its LDS skeleton alone ~0.8 us per
-// block).  Same super-tiles, LDS image, slot layout, slabs and results as weight_grad_kernel.
-constexpr int kWsProd = 4, kWsCons = 8, kWsThreads = (kWsProd + kWsCons) * 64;
-
-template <int TNX, int TKX>
-__global__ __launch_bounds__(kWsThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void weight_grad_ws_kernel(
-    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, int64_t T, int N, int K,
-    int64_t chunk_rows, float* __restrict__ part, float* __restrict__ bias_part) {
-    using S = WgShape<TNX, TKX>;
-    constexpr int UPL = S::U / (kWsProd * 64);  // loader units per producer lane (2 or 3)
-    constexpr int KA = S::UA / (kWsProd * 64);  // units k < KA are dY, the rest X (compile-time per k)
-    constexpr int kPairs = S::NA / 2;
-    static_assert(S::U % (kWsProd * 64) == 0 && S::UA % (kWsProd * 64) == 0, "units per producer lane");
-    extern __shared__ uint4 lds[];  // two token blocks of S::BUF slots, then the bias row-group sums
-    const int nsn = (N + S::NA - 1) / S::NA, ntiles = nsn * ((K + S::NB - 1) / S::NB);
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int tile = slot % ntiles;
-    const int64_t chunk = (int64_t)(slot / ntiles) * 8 + xcd;
-    if (chunk * chunk_rows >= T) return;
-    const int tn = tile % nsn, tk = tile / nsn;
-    const int n0 = tn * S::NA, k0 = tk * S::NB;
-    const int64_t t_begin = chunk * chunk_rows;
-    const int64_t t_end = min(T, t_begin + chunk_rows);
-    const int64_t nblk = (t_end - t_begin + kTT - 1) / kTT;
-    const int64_t niter = (nblk + 1) & ~(int64_t)1;  // even: the producers' loop is unrolled by two
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool with_bias = bias_part != nullptr && tk == 0;
-    float2* red = reinterpret_cast<float2*>(lds + 2 * S::BUF);  // [4 row groups][kPairs]
-
-    if (wave >= kWsCons) {
-        // ---------------- producers: lane p holds units p + 256 k, k < UPL
-        const int p = (int)threadIdx.x - kWsCons * 64;
-        __amdgpu_buffer_rsrc_t rs[UPL];
-        uint32_t voff[UPL], ldb_[UPL];
-        int rg[UPL], cg[UPL];
-#pragma unroll
-        for (int k = 0; k < UPL; ++k) {
-            const bool a = k < KA;
-            const int v = p + kWsProd * 64 * (a ? k : k - KA), pairs = a ? S::NA / 2 : S::NB / 2;
-            cg[k] = v % pairs;
-            rg[k] = v / pairs;
-            const int64_t ld = a ? lda : ldb;
-            rs[k] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>((a ? A : B) + t_begin * ld), 0,
-                                                      (int)((t_end - t_begin) * ld * 4), 0x00020000);
-            ldb_[k] = (uint32_t)(ld * 4);
-            const int col = (a ? n0 : k0) + 2 * cg[k];
-            voff[k] = col < (a ? N : K) ? (uint32_t)(8 * rg[k]) * ldb_[k] + (uint32_t)(col * 4) : kDrop;
-        }
-        float2 bsum[KA > 0 ? KA : 1];
-#pragma unroll
-        for (int k = 0; k < (KA > 0 ? KA : 1); ++k) bsum[k] = make_float2(0.f, 0.f);
-        // rows 8 rg + q of block blk of unit k: one voffset, the row step in the scalar offset
-        auto load = [&](int k, int64_t blk, float2 (&r)[8]) {
-            const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(blk * kTT) * ldb_[k]);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const u32v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs[k], voff[k],
-                                                                     base + (uint32_t)q * ldb_[k], 0);
-                r[q] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
-            }
-        };
-        float2 r0[UPL][8], r1[UPL][8];
-#pragma unroll
-        for (int k = 0; k < UPL; ++k) load(k, 0, r0[k]);
-        __builtin_amdgcn_sched_barrier(0);  // block 0's loads older than block 1's: the loop's waits assume it
-#pragma unroll
-        for (int k = 0; k < UPL; ++k) load(k, 1, r1[k]);
-        // (sched_barrier: the compiler otherwise hoists the next block's split above this block's loads and waits for
-        // every load in flight at the top of the loop)
-        auto produce = [&](int64_t i, float2 (&r)[UPL][8]) {
-            __builtin_amdgcn_sched_barrier(0);
-            uint4* buf = lds + (i & 1) * S::BUF;
-#pragma unroll
-            for (int k = 0; k < UPL; ++k) {
-                const bool a = k < KA;
-#if defined(ASME_WS_KO_SPLIT)
-                {
-                    uint4* pl = buf + (a ? 0 : 3 * S::PA);
-                    const int ps = a ? S::PA : S::PB;
-                    const uint4 u0 = make_uint4(__float_as_uint(r[k][0].x), __float_as_uint(r[k][1].x),
-                                                __float_as_uint(r[k][2].x), __float_as_uint(r[k][3].y));
-                    const uint4 u1 = make_uint4(__float_as_uint(r[k][4].x), __float_as_uint(r[k][5].x),
-                                                __float_as_uint(r[k][6].x), __float_as_uint(r[k][7].y));
-                    pl[tslot(2 * cg[k], rg[k])] = u0; pl[ps + tslot(2 * cg[k], rg[k])] = u1;
-                    pl[2 * ps + tslot(2 * cg[k], rg[k])] = u0; pl[tslot(2 * cg[k] + 1, rg[k])] = u1;
-                    pl[ps + tslot(2 * cg[k] + 1, rg[k])] = u0; pl[2 * ps + tslot(2 * cg[k] + 1, rg[k])] = u1;
-                }
-#else
-                store_cols(buf + (a ? 0 : 3 * S::PA), a ? S::PA : S::PB, rg[k], cg[k], r[k]);
-#endif
-                if (a) {
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        bsum[k < KA ? k : 0].x += r[k][q].x;
-                        bsum[k < KA ? k : 0].y += r[k][q].y;
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < UPL; ++k) load(k, i + 2, r[k]);
-            __syncthreads();
-        };
-        for (int64_t i = 0; i < niter; i += 2) {
-            produce(i, r0);
-            produce(i + 1, r1);
-        }
-        if (with_bias) {
-#pragma unroll
-            for (int k = 0; k < KA; ++k) red[rg[k] * kPairs + cg[k]] = bsum[k];
-        }
-    } else {
-        // ---------------- consumers: 8 waves over the super-tile, 64 dY columns x NB / WC X columns each
-        const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
-        const int wr = wave / S::WC, wc = wave % S::WC;
-        floatx4 acc[4][S::MJ];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < S::MJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int64_t i = 0; i < niter; ++i) {
-            __syncthreads();  // block i is in buffer i & 1
-            if (i < nblk) {
-                const uint4* L = lds + (i & 1) * S::BUF;
-                Bf3 b[S::MJ];
-#pragma unroll
-                for (int j = 0; j < S::MJ; ++j) {
-                    const int sl = tslot(wc * (S::NB / S::WC) + j * 16 + c16, g);
-                    b[j].h = __builtin_bit_cast(bf16x8, L[3 * S::PA + sl]);
-                    b[j].m = __builtin_bit_cast(bf16x8, L[3 * S::PA + S::PB + sl]);
-                    b[j].l = __builtin_bit_cast(bf16x8, L[3 * S::PA + 2 * S::PB + sl]);
-                }
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii) {
-                    const int sl = tslot(wr * 64 + ii * 16 + c16, g);
-                    Bf3 a;
-                    a.h = __builtin_bit_cast(bf16x8, L[sl]);
-                    a.m = __builtin_bit_cast(bf16x8, L[S::PA + sl]);
-                    a.l = __builtin_bit_cast(bf16x8, L[2 * S::PA + sl]);
-#pragma unroll
-                    for (int j = 0; j < S::MJ; ++j) {
-#if defined(ASME_WS_KO_MFMA)
-                        acc[ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b[j].l, acc[ii][j], 0, 0, 0);
-#else
-                        acc[ii][j] = mfma_bf3(a, b[j], acc[ii][j]);
-#endif
-                    }
-                }
-            }
-        }
-        const int64_t slab = (int64_t)N * K + (bias_part != nullptr ? N : 0);
-        float* P = part + chunk * slab;
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-            for (int j = 0; j < S::MJ; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int n = n0 + wr * 64 + ii * 16 + 4 * g + q;
-                    const int k = k0 + wc * (S::NB / S::WC) + j * 16 + c16;
-                    if (n < N && k < K) P[(int64_t)n * K + k] = acc[ii][j][q];
-                }
-    }
-    if (with_bias) {  // the 4 row groups' column sums, in row-group order
-        __syncthreads();
-        if (threadIdx.x < kPairs && n0 + 2 * (int)threadIdx.x < N) {
-            const int64_t slab = (int64_t)N * K + N;
-            float2 s = red[threadIdx.x];
-#pragma unroll
-            for (int q = 1; q < 4; ++q) {
-                const float2 v = red[q * kPairs + threadIdx.x];
-                s.x += v.x;
-                s.y += v.y;
-            }
-            *reinterpret_cast<float2*>(part + chunk * slab + (int64_t)N * K + n0 + 2 * threadIdx.x) = s;
-        }
-    }
-}
-
 // column sums with a fixed order (see reduce_rows_kernel in embedding.hip)
 constexpr int kRedCols = 64, kRedGroups = 16;
 // Column c of the slabs (row stride width_w + width_b) goes to out_w[c] (c < width_w) or out_b[c - width_w]:
@@ -551,30 +349,6 @@ hipError_t launch_weight_grad(dim3 grid, hipStream_t s, const float* dy, int64_t
     return hipSuccess;
 }
 
-template <int TNX, int TKX>
-hipError_t launch_weight_grad_ws(dim3 grid, hipStream_t s, const float* dy, int64_t ld_dy, const float* x,
-                                 int64_t ld_x, int64_t T, int N, int K, int64_t chunk_rows, float* part, float* bpart) {
-    constexpr int kLds = WgShape<TNX, TKX>::LDS + 4 * 128 * TNX / 2 * 8;  // + the bias row-group sums
-    static bool attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)weight_grad_ws_kernel<TNX, TKX>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    weight_grad_ws_kernel<TNX, TKX><<<grid, dim3(kWsThreads), kLds, s>>>(dy, ld_dy, x, ld_x, T, N, K, chunk_rows,
-                                                                         part, bpart);
-    return hipSuccess;
-}
-
-bool wg_specialised() {  // ASME_WG_WS=0: the single-role kernel (A/B switch)
-    static const bool on = [] {
-        const char* e = std::getenv("ASME_WG_WS");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 }  // namespace
 
 ASME_API int64_t asme_linear_weight_grad_workspace(int64_t n_tokens, int64_t out_features, int64_t in_features) {
@@ -602,16 +376,11 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
     const dim3 grid((unsigned)(super_tiles(out_features, in_features) * ((p.nchunks + 7) / 8) * 8));
     const Pairing pr = pick_pairing(out_features, in_features);
     const int N = (int)out_features, K = (int)in_features;
-    const bool ws = wg_specialised();
     const hipError_t e =
-        pr.tnx == 2
-            ? (ws ? launch_weight_grad_ws<2, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart)
-                  : launch_weight_grad<2, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart))
+        pr.tnx == 2 ? launch_weight_grad<2, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart)
         : pr.tkx == 2
-            ? (ws ? launch_weight_grad_ws<1, 2>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart)
-                  : launch_weight_grad<1, 2>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart))
-            : (ws ? launch_weight_grad_ws<1, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart)
-                  : launch_weight_grad<1, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart));
+            ? launch_weight_grad<1, 2>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart)
+            : launch_weight_grad<1, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart);
     if (e != hipSuccess) return hip_status(e, "asme_linear_weight_grad: LDS opt-in");
     const int64_t width_w = out_features * in_features, width_b = db ? out_features : 0;
     hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width_w + width_b + kRedCols - 1) / kRedCols)), dim3(1024), 0,
