@@ -214,6 +214,16 @@ class MultiHeadedAttention(nn.Module):
         b = torch.cat([l.bias for l in self.linear_layers], 0)
         return w, b
 
+    def qkv(self, x):
+        """the fused Q/K/V projection (transformer_layers.py:191-194) as one GEMM: the three weights (and biases) are
+        kept as consecutive row blocks of one buffer, re-homed there on first use, so no per-forward concatenation"""
+        ws = [l.weight for l in self.linear_layers]
+        bs = [l.bias for l in self.linear_layers]
+        if ops.adjacent_rows(ws) is None or ops.adjacent_rows(bs) is None:
+            ops.fuse_rows_(ws)
+            ops.fuse_rows_(bs)
+        return ops.linear_row_parts(x, ws, bs)
+
 
 class PositionwiseFeedForward(nn.Module):
     def __init__(self, d_model: int, d_ff: int, dropout: float = 0.1):
@@ -256,8 +266,7 @@ class TransformerLayer(nn.Module):
         x, ln = ops.layer_norm_pass(x, blocks[0].input_sublayer.norm)
         for i, blk in enumerate(blocks):
             att, ff = blk.attention, blk.feed_forward
-            w_qkv, b_qkv = att.qkv_weights()
-            qkv = ops.linear(ln, w_qkv, b_qkv)
+            qkv = att.qkv(ln)
             o = ops.attention(qkv, key_valid, att.heads, causal, _p(att.dropout, tr))
             a = ops.linear(o, att.output_linear.weight, att.output_linear.bias)
             h1, ln2 = ops.residual_ln(x, a, blk.output_sublayer.norm, _p(blk.input_sublayer.dropout, tr), 0.0)

@@ -589,6 +589,72 @@ def linear(x, w, b=None):
     return _LinearFn.apply(x, w, b)
 
 
+def adjacent_rows(parts: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
+    """the tensors' rows as ONE tensor when they are consecutive row blocks of one buffer (a view, no copy), else None"""
+    t0 = parts[0]
+    if not all(t.is_contiguous() and t.dtype == t0.dtype and t.device == t0.device and t.shape[1:] == t0.shape[1:]
+               for t in parts):
+        return None
+    if any(t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() for t in parts):
+        return None
+    row = t0[0].numel() if t0.dim() > 1 else 1
+    off = t0.storage_offset()
+    for t in parts:
+        if t.storage_offset() != off:
+            return None
+        off += t.shape[0] * row
+    rows = sum(t.shape[0] for t in parts)
+    return t0.detach().as_strided((rows,) + tuple(t0.shape[1:]), t0.stride())
+
+
+def fuse_rows_(params: Sequence[torch.nn.Parameter]) -> None:
+    """re-home parameters onto consecutive row blocks of one new buffer (values unchanged), so adjacent_rows finds
+    them; optimizer state is keyed by the parameter objects and is unaffected"""
+    with torch.no_grad():
+        buf = torch.cat([p.detach() for p in params], 0)
+        r = 0
+        for p in params:
+            p.data = buf[r:r + p.shape[0]]
+            r += p.shape[0]
+
+
+class _RowPartsLinearFn(torch.autograd.Function):
+    """_LinearFn for a weight / bias given as k row blocks that lie consecutively in one buffer (W, B views of it):
+    the GEMMs read the buffer in place (no per-forward concatenation) and each block's gradient is a row block of
+    the one fused weight / bias gradient."""
+
+    @staticmethod
+    def forward(ctx, x, W, B, *parts):
+        N, K = W.shape
+        x2 = _f32(x).reshape(-1, K)
+        ctx.save_for_backward(x2, W)
+        ctx.xshape = x.shape
+        ctx.rows = [t.shape[0] for t in parts[:len(parts) // 2]]
+        return _linear_fwd(x2, W, B).view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, W = ctx.saved_tensors
+        N, K = W.shape
+        dy2 = _f32(dy).reshape(-1, N)
+        dx = _linear_dx(dy2, W).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw, db = _weight_grad(dy2, x2, True)
+        gw, gb, r = [], [], 0
+        for n in ctx.rows:
+            gw.append(dw[r:r + n])
+            gb.append(db[r:r + n])
+            r += n
+        return (dx, None, None, *gw, *gb)
+
+
+def linear_row_parts(x, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor]):
+    """linear(x, cat(weights), cat(biases)) without the concatenation when the blocks are adjacent in memory"""
+    W, B = adjacent_rows(weights), adjacent_rows(biases)
+    if W is None or B is None:
+        return linear(x, torch.cat(list(weights), 0), torch.cat(list(biases), 0))
+    return _RowPartsLinearFn.apply(x, W, B, *weights, *biases)
+
+
 class _FFNFn(torch.autograd.Function):
     """PositionwiseFeedForward W2(dropout(GELU_erf(W1 x + b1))) + b2 (transformer_layers.py:212-220) with the
     activation fused into the GEMMs: forward GEMM1 writes dropout(GELU(pre)) and the activation factor
