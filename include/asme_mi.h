@@ -336,6 +336,16 @@ int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, con
                            const int64_t* c_off, const int64_t* c_n, const float* const* c_rows,
                            const float* const* c_scale, float out_scale, void* workspace, int64_t workspace_bytes,
                            float* grad_rows, void* stream);
+/* The same sums with each finished row applied at once as the lazy table Adam's real-gradient step (from the
+ * staged rows sp/sm/sv[s] into param/exp_avg/exp_avg_sq[rows[s]], last_step[rows[s]] = step) instead of being
+ * stored: bit-identical to asme_table_grad_reduce + asme_lazy_adam_apply_staged, no gradient-row round trip. */
+int asme_table_grad_reduce_apply(const int32_t* order, const int32_t* sorted_slot, const int32_t* seg_off,
+                                 const int32_t* count, int64_t n, int64_t cap, int64_t dim, int n_contrib,
+                                 const int64_t* c_off, const int64_t* c_n, const float* const* c_rows,
+                                 const float* const* c_scale, float out_scale, void* workspace,
+                                 int64_t workspace_bytes, const int64_t* rows, const float* sp, const float* sm,
+                                 const float* sv, int32_t* last_step, float* param, float* exp_avg,
+                                 float* exp_avg_sq, const float* hist, int64_t hist_cap, int64_t step, void* stream);
 
 
 /* ---- Weight-stationary Linear GEMM (csrc/wsgemm.hip; transformer_layers.py:175-199, 212-220 nn.Linear and

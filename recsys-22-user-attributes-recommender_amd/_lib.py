@@ -42,6 +42,8 @@ SIGNATURES = {
     "asme_occurrence_csr": [p, i64, i64, p, i64, p, p, p, p],
     "asme_table_grad_workspace": [i64, i64],
     "asme_table_grad_reduce": [p, p, p, p, i64, i64, i64, i32, p, p, p, p, f32, p, i64, p, p],
+    "asme_table_grad_reduce_apply": [p, p, p, p, i64, i64, i64, i32, p, p, p, p, f32, p, i64, p, p, p, p, p, p, p,
+                                     p, p, i64, i64, p],
     "asme_catalog_rank": [p, i64, i64, i64, p, i64, i64, p, p, p, p, p],
     "asme_linear_xent_fwd_workspace": [i64, i64, i64],
     "asme_linear_xent_fwd": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, p, i64, p, p],

@@ -11,6 +11,7 @@
 // to hold the slot (row_slot for the Adam kernel) and must be reset with asme_dedup_reset.
 #include <hipcub/hipcub.hpp>
 
+#include "adam_math.h"
 #include "common.h"
 
 using namespace asme;
@@ -391,18 +392,50 @@ __device__ __forceinline__ float4 scale4(const float4& a, float s) {
     return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
 }
 
+// Fused optimizer step (asme_table_grad_reduce_apply): a finished gradient row of slot s is not stored but
+// applied at once -- the lazy table Adam's real-gradient step from the staged row values (slot order) into the
+// table row rows[s] -- exactly asme_lazy_adam_apply_staged's arithmetic on the same gradient values.
+struct TableApply {
+    const int64_t* rows;
+    const float* sp;
+    const float* sm;
+    const float* sv;
+    int32_t* last_step;
+    float* p;
+    float* m;
+    float* v;
+    const AdamHyper* hist;
+    int32_t step;
+};
+
+__device__ __forceinline__ void apply_grad4(const TableApply& A, int64_t s, int dim, int c0, const float4& G) {
+    const AdamHyper hp = A.hist[A.step];
+    const int64_t so = s * dim + c0;
+    float4 P = *reinterpret_cast<const float4*>(A.sp + so);
+    float4 M = *reinterpret_cast<const float4*>(A.sm + so);
+    float4 V = *reinterpret_cast<const float4*>(A.sv + so);
+    adam_elem4(P, G, M, V, hp);
+    const int64_t r = A.rows[s];
+    const int64_t off = r * dim + c0;
+    *reinterpret_cast<float4*>(A.p + off) = P;
+    *reinterpret_cast<float4*>(A.m + off) = M;
+    *reinterpret_cast<float4*>(A.v + off) = V;
+    if (c0 == 0) A.last_step[r] = A.step;
+}
+
 // Pass 1: one 32-lane group per chunk of kChunk consecutive sorted occurrences (float4 per lane).  A slot
 // whose occurrence list lies inside the chunk gets its final row; the list cut by the chunk's start is
 // left in head[chunk], the list cut by its end in tail[chunk] (a chunk inside one list: head).  Each lane
 // first resolves one occurrence (slot, source row, scale: coalesced loads) into LDS; the group then walks
 // the chunk with eight row gathers in flight.
 constexpr int kChunkGroups = 8;  // 32-lane groups per 256-thread block
+template <bool APPLY>
 __global__ __launch_bounds__(256) void grad_chunk_kernel(const int32_t* __restrict__ order,
                                                          const int32_t* __restrict__ slot,
                                                          const int32_t* __restrict__ seg_off, int64_t n,
                                                          int64_t cap, int dim, Contribs C, float out_scale,
                                                          float* __restrict__ grad_rows, float* __restrict__ head,
-                                                         float* __restrict__ tail) {
+                                                         float* __restrict__ tail, TableApply A) {
     __shared__ int32_t s_slot[kChunkGroups][kChunk];
     __shared__ const float* s_src[kChunkGroups][kChunk];
     __shared__ float s_sc[kChunkGroups][kChunk];
@@ -446,9 +479,12 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(const int32_t* __restri
         bool started = seg_off[cur] == i0;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         auto flush = [&](bool ended) {
-            if (started && ended)
-                *reinterpret_cast<float4*>(grad_rows + (int64_t)cur * dim + c0) = scale4(acc, out_scale);
-            else
+            if (started && ended) {
+                if constexpr (APPLY)
+                    apply_grad4(A, cur, dim, c0, scale4(acc, out_scale));
+                else
+                    *reinterpret_cast<float4*>(grad_rows + (int64_t)cur * dim + c0) = scale4(acc, out_scale);
+            } else
                 *reinterpret_cast<float4*>((started ? tail : head) + c * dim + c0) = acc;
         };
         for (int j0 = 0; j0 < cnt; j0 += 8) {
@@ -479,23 +515,33 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(const int32_t* __restri
 }
 
 // Pass 2: slots whose list spans chunks: tail of the first chunk + heads of the following ones, in order.
-__global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restrict__ seg_off,
-                                                        const int32_t* __restrict__ count, int64_t cap, int dim,
-                                                        float out_scale, const float* __restrict__ head,
+// One 32-lane group per chunk boundary k (sorted position k * kChunk): the slot there spans chunks iff its list
+// started in chunk k - 1; that boundary is the slot's first, so each spanning slot is summed exactly once (a grid
+// over the boundaries, not over every slot: the spanning ones are few).
+template <bool APPLY>
+__global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restrict__ slot,
+                                                        const int32_t* __restrict__ seg_off,
+                                                        const int32_t* __restrict__ count, int64_t n, int64_t cap,
+                                                        int dim, float out_scale, const float* __restrict__ head,
                                                         const float* __restrict__ tail,
-                                                        float* __restrict__ grad_rows) {
+                                                        float* __restrict__ grad_rows, TableApply A) {
     const int lane = threadIdx.x & 31;
-    const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
+    const int64_t k = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5) + 1;
+    if (k * kChunk >= n) return;
+    const int32_t s = slot[k * kChunk];
     if (s >= cap || s >= *count) return;
-    const int64_t cf = seg_off[s] / kChunk, cl = (seg_off[s + 1] - 1) / kChunk;
-    if (cf == cl) return;
+    const int64_t cf = seg_off[s] / kChunk;
+    if (cf != k - 1) return;
+    const int64_t cl = (seg_off[s + 1] - 1) / kChunk;
     for (int c0 = 4 * lane; c0 < dim; c0 += 128) {
         float4 acc = *reinterpret_cast<const float4*>(tail + cf * dim + c0);
-        for (int64_t k = cf + 1; k <= cl; ++k) add4(acc, *reinterpret_cast<const float4*>(head + k * dim + c0));
-        *reinterpret_cast<float4*>(grad_rows + s * dim + c0) = scale4(acc, out_scale);
+        for (int64_t q = cf + 1; q <= cl; ++q) add4(acc, *reinterpret_cast<const float4*>(head + q * dim + c0));
+        if constexpr (APPLY)
+            apply_grad4(A, s, dim, c0, scale4(acc, out_scale));
+        else
+            *reinterpret_cast<float4*>(grad_rows + (int64_t)s * dim + c0) = scale4(acc, out_scale);
     }
 }
-
 
 }  // namespace
 
@@ -541,16 +587,13 @@ ASME_API int64_t asme_table_grad_workspace(int64_t n, int64_t dim) {
     return 2 * ((n + kChunk - 1) / kChunk) * dim * (int64_t)sizeof(float);
 }
 
-// grad_rows[s] = out_scale * sum over slot s's occurrences of their contribution rows, in a fixed order
-// (chunks of 32 sorted occurrences, then chunk partials in order: bit-reproducible).  Contribution k covers
-// flat occurrences [c_off[k], c_off[k] + c_n[k]): row t = c_rows[k][t] (* c_scale[k][t]).  Host arrays of at
-// most 4 contributions, sorted by c_off and disjoint; dim % 4 == 0.  Rows of slots >= *count are untouched.
-ASME_API int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, const int32_t* seg_off,
-                                    const int32_t* count, int64_t n, int64_t cap, int64_t dim, int n_contrib,
-                                    const int64_t* c_off, const int64_t* c_n, const float* const* c_rows,
-                                    const float* const* c_scale, float out_scale, void* workspace,
-                                    int64_t workspace_bytes, float* grad_rows, void* stream) {
-    ASME_CHECK_ARG(order && sorted_slot && seg_off && count && grad_rows && c_off && c_n && c_rows,
+namespace {
+
+int table_grad_launch(const int32_t* order, const int32_t* sorted_slot, const int32_t* seg_off, const int32_t* count,
+                      int64_t n, int64_t cap, int64_t dim, int n_contrib, const int64_t* c_off, const int64_t* c_n,
+                      const float* const* c_rows, const float* const* c_scale, float out_scale, void* workspace,
+                      int64_t workspace_bytes, float* grad_rows, const TableApply* apply, void* stream) {
+    ASME_CHECK_ARG(order && sorted_slot && seg_off && count && (grad_rows || apply) && c_off && c_n && c_rows,
                    "asme_table_grad_reduce: null");
     ASME_CHECK_ARG(n_contrib >= 1 && n_contrib <= kMaxContrib, "asme_table_grad_reduce: 1..4 contributions");
     ASME_CHECK_ARG(dim > 0 && dim % 4 == 0 && ((uintptr_t)grad_rows & 15) == 0,
@@ -572,9 +615,60 @@ ASME_API int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_
     const int64_t nchunks = (n + kChunk - 1) / kChunk;
     float* head = (float*)workspace;
     float* tail = head + nchunks * dim;
-    hipLaunchKernelGGL(grad_chunk_kernel, dim3((unsigned)((nchunks + kChunkGroups - 1) / kChunkGroups)), dim3(256), 0, s, order,
-                       sorted_slot, seg_off, n, cap, (int)dim, C, out_scale, grad_rows, head, tail);
-    hipLaunchKernelGGL(grad_span_kernel, dim3((unsigned)((cap * 32 + 255) / 256)), dim3(256), 0, s, seg_off, count,
-                       cap, (int)dim, out_scale, head, tail, grad_rows);
+    const TableApply A = apply ? *apply : TableApply{};
+    const dim3 gc((unsigned)((nchunks + kChunkGroups - 1) / kChunkGroups));
+    const dim3 gs((unsigned)(((nchunks > 1 ? nchunks - 1 : 1) * 32 + 255) / 256));
+    if (apply) {
+        hipLaunchKernelGGL(grad_chunk_kernel<true>, gc, dim3(256), 0, s, order, sorted_slot, seg_off, n, cap, (int)dim,
+                           C, out_scale, grad_rows, head, tail, A);
+        if (nchunks > 1)
+            hipLaunchKernelGGL(grad_span_kernel<true>, gs, dim3(256), 0, s, sorted_slot, seg_off, count, n, cap,
+                               (int)dim, out_scale, head, tail, grad_rows, A);
+    } else {
+        hipLaunchKernelGGL(grad_chunk_kernel<false>, gc, dim3(256), 0, s, order, sorted_slot, seg_off, n, cap,
+                           (int)dim, C, out_scale, grad_rows, head, tail, A);
+        if (nchunks > 1)
+            hipLaunchKernelGGL(grad_span_kernel<false>, gs, dim3(256), 0, s, sorted_slot, seg_off, count, n, cap,
+                               (int)dim, out_scale, head, tail, grad_rows, A);
+    }
     ASME_LAUNCH_CHECK("asme_table_grad_reduce");
+}
+
+}  // namespace
+
+// grad_rows[s] = out_scale * sum over slot s's occurrences of their contribution rows, in a fixed order
+// (chunks of 32 sorted occurrences, then chunk partials in order: bit-reproducible).  Contribution k covers
+// flat occurrences [c_off[k], c_off[k] + c_n[k]): row t = c_rows[k][t] (* c_scale[k][t]).  Host arrays of at
+// most 4 contributions, sorted by c_off and disjoint; dim % 4 == 0.  Rows of slots >= *count are untouched.
+ASME_API int asme_table_grad_reduce(const int32_t* order, const int32_t* sorted_slot, const int32_t* seg_off,
+                                    const int32_t* count, int64_t n, int64_t cap, int64_t dim, int n_contrib,
+                                    const int64_t* c_off, const int64_t* c_n, const float* const* c_rows,
+                                    const float* const* c_scale, float out_scale, void* workspace,
+                                    int64_t workspace_bytes, float* grad_rows, void* stream) {
+    return table_grad_launch(order, sorted_slot, seg_off, count, n, cap, dim, n_contrib, c_off, c_n, c_rows, c_scale,
+                             out_scale, workspace, workspace_bytes, grad_rows, nullptr, stream);
+}
+
+// The same sums, each finished row applied at once as the lazy table Adam's real-gradient step instead of being
+// stored: from the staged values sp/sm/sv[s] into param/exp_avg/exp_avg_sq[rows[s]], last_step[rows[s]] = step --
+// bit-identical to asme_table_grad_reduce followed by asme_lazy_adam_apply_staged, without the gradient rows'
+// round trip through HBM.  dim % 4 == 0; every pointer 16-B aligned.
+ASME_API int asme_table_grad_reduce_apply(const int32_t* order, const int32_t* sorted_slot, const int32_t* seg_off,
+                                          const int32_t* count, int64_t n, int64_t cap, int64_t dim, int n_contrib,
+                                          const int64_t* c_off, const int64_t* c_n, const float* const* c_rows,
+                                          const float* const* c_scale, float out_scale, void* workspace,
+                                          int64_t workspace_bytes, const int64_t* rows, const float* sp,
+                                          const float* sm, const float* sv, int32_t* last_step, float* param,
+                                          float* exp_avg, float* exp_avg_sq, const float* hist, int64_t hist_cap,
+                                          int64_t step, void* stream) {
+    ASME_CHECK_ARG(rows && sp && sm && sv && last_step && param && exp_avg && exp_avg_sq && hist,
+                   "asme_table_grad_reduce_apply: null pointer");
+    ASME_CHECK_ARG(step >= 1 && step < hist_cap, "asme_table_grad_reduce_apply: step outside the history");
+    ASME_CHECK_ARG(((((uintptr_t)sp) | ((uintptr_t)sm) | ((uintptr_t)sv) | ((uintptr_t)param) | ((uintptr_t)exp_avg) |
+                     ((uintptr_t)exp_avg_sq)) & 15) == 0,
+                   "asme_table_grad_reduce_apply: 16-B aligned rows");
+    const TableApply A{rows, sp, sm, sv, last_step, param, exp_avg, exp_avg_sq,
+                       reinterpret_cast<const AdamHyper*>(hist), (int32_t)step};
+    return table_grad_launch(order, sorted_slot, seg_off, count, n, cap, dim, n_contrib, c_off, c_n, c_rows, c_scale,
+                             out_scale, workspace, workspace_bytes, nullptr, &A, stream);
 }

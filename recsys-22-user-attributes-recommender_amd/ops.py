@@ -10,6 +10,7 @@ kernels derive the mask from (seed, element index) with Philox, so the backward 
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -25,6 +26,8 @@ _EMB_PARTIALS = 2048  # the embedding backward's (2x the waves in flight: 124 ->
 # lazy table Adam: stage the step's unique rows (asme_lazy_adam_stage) so every reader gathers them in slot order
 # (True), or catch them up in place in the table and gather by id (False; the A/B switch)
 STAGE_ROWS = True
+# reduce the table gradient and apply the staged Adam step in one pass when nothing else needs the gradient rows
+FUSED_APPLY = os.environ.get("ASME_FUSED_APPLY", "1") != "0"
 
 
 def new_seed(p: float) -> int:
@@ -127,6 +130,9 @@ class LazyTableState:
     def apply(self, plan: "SparseTablePlan", step: int):
         D = self.param.shape[1]
         if plan.staged is not None:
+            if FUSED_APPLY and plan.reduce_apply(self, step):
+                plan.staged = None
+                return
             st = plan.staged
             call("asme_lazy_adam_apply_staged", ptr(plan.unique), ptr(plan.count), plan.capacity, ptr(plan.grad_rows),
                  ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(self.last_step), ptr(self.param), ptr(self.exp_avg),
@@ -252,13 +258,9 @@ class SparseTablePlan:
             raise RuntimeError("table gradient already materialised for this step")
         self._contrib.append((self._offset[key], ids.numel(), rows, scale))
 
-    def _reduce_contributions(self) -> torch.Tensor:
-        """deterministic table gradient: occurrences grouped by row (stable radix sort), sums in a fixed
-        order (asme_occurrence_csr + asme_table_grad_reduce); no float atomics, no zero fill"""
+    def _occurrence_csr(self):
+        n = self.capacity
         dev = self.unique.device
-        n, d = self.capacity, self.dim
-        if n == 0:
-            return torch.zeros(0, d, device=dev, dtype=torch.float32)
         lib = _lib.load()
         ws_bytes = int(lib.asme_occurrence_csr_workspace(n))
         ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
@@ -267,17 +269,46 @@ class SparseTablePlan:
         seg_off = torch.empty(n + 1, device=dev, dtype=torch.int32)
         call("asme_occurrence_csr", ptr(self._flat_inverse), n, n, ptr(ws), ws_bytes, ptr(order), ptr(slot),
              ptr(seg_off), stream())
-        part_bytes = int(lib.asme_table_grad_workspace(n, d))
+        part_bytes = int(lib.asme_table_grad_workspace(n, self.dim))
         parts = torch.empty(max(part_bytes, 4) // 4, device=dev, dtype=torch.float32)
+        return order, slot, seg_off, parts, part_bytes
+
+    @staticmethod
+    def _contrib_arrays(part):
+        k = len(part)
+        return (k, (ctypes_i64 * k)(*[c[0] for c in part]), (ctypes_i64 * k)(*[c[1] for c in part]),
+                (ctypes_vp * k)(*[c[2].data_ptr() for c in part]),
+                (ctypes_vp * k)(*[(c[3].data_ptr() if c[3] is not None else None) for c in part]))
+
+    def reduce_apply(self, lazy: "LazyTableState", step: int) -> bool:
+        """the table gradient reduced and applied as the lazy Adam's real-gradient step in one pass from the staged
+        rows (asme_table_grad_reduce_apply); False (nothing done) where the gradient rows are needed as such"""
+        if self.staged is None or self._grad_rows is not None or not 1 <= len(self._contrib) <= 4 \
+                or self.capacity == 0:
+            return False
+        order, slot, seg_off, parts, part_bytes = self._occurrence_csr()
+        k, offs, ns, rows, scales = self._contrib_arrays(sorted(self._contrib, key=lambda c: c[0]))
+        st = self.staged
+        n, d = self.capacity, self.dim
+        call("asme_table_grad_reduce_apply", ptr(order), ptr(slot), ptr(seg_off), ptr(self.count), n, n, d, k, offs,
+             ns, rows, scales, self.grad_scale, ptr(parts), part_bytes, ptr(self.unique), ptr(st[0]), ptr(st[1]),
+             ptr(st[2]), ptr(lazy.last_step), ptr(lazy.param), ptr(lazy.exp_avg), ptr(lazy.exp_avg_sq),
+             ptr(lazy.hist), lazy.hist.shape[0], step, stream())
+        # (the contributions stay registered: a re-step without a new backward reduces them again via grad_rows)
+        return True
+
+    def _reduce_contributions(self) -> torch.Tensor:
+        """deterministic table gradient: occurrences grouped by row (counting sort), sums in a fixed order
+        (asme_occurrence_csr + asme_table_grad_reduce); no float atomics, no zero fill"""
+        dev = self.unique.device
+        n, d = self.capacity, self.dim
+        if n == 0:
+            return torch.zeros(0, d, device=dev, dtype=torch.float32)
+        order, slot, seg_off, parts, part_bytes = self._occurrence_csr()
         out = torch.empty(n, d, device=dev, dtype=torch.float32)
         contrib = sorted(self._contrib, key=lambda c: c[0])
         for i in range(0, len(contrib), 4):
-            part = contrib[i:i + 4]
-            k = len(part)
-            offs = (ctypes_i64 * k)(*[c[0] for c in part])
-            ns = (ctypes_i64 * k)(*[c[1] for c in part])
-            rows = (ctypes_vp * k)(*[c[2].data_ptr() for c in part])
-            scales = (ctypes_vp * k)(*[(c[3].data_ptr() if c[3] is not None else None) for c in part])
+            k, offs, ns, rows, scales = self._contrib_arrays(contrib[i:i + 4])
             dest = out if i == 0 else torch.empty_like(out)  # more than 4 contributions: add the rest
             call("asme_table_grad_reduce", ptr(order), ptr(slot), ptr(seg_off), ptr(self.count), n, n, d, k, offs,
                  ns, rows, scales, self.grad_scale, ptr(parts), part_bytes, ptr(dest), stream())

@@ -109,10 +109,12 @@ def test_int32_batch_ids_with_sparse_table(asme, dev):
 def test_staged_rows_match_in_place_catch_up(asme, dev, monkeypatch):
     """lazy table Adam with the step's rows staged in slot order (asme_lazy_adam_stage / _apply_staged, every
     reader gathering the staged rows) == catching them up in place in the table, bit for bit -- across a
-    flush between forward and step (state_dict), a re-step without a new backward and a resumed step count"""
+    flush between forward and step (state_dict), a re-step without a new backward and a resumed step count; the
+    staged step both fused with the gradient reduction (asme_table_grad_reduce_apply) and separate"""
     out = []
-    for staged in (True, False):
+    for staged, fused in ((True, True), (True, False), (False, True)):
         monkeypatch.setattr(asme.ops, "STAGE_ROWS", staged)
+        monkeypatch.setattr(asme.ops, "FUSED_APPLY", fused)
         model, module, batch = _sasrec(asme, dev, "sparse")
         opt = module.configure_optimizers()
         seen = []
@@ -131,6 +133,6 @@ def test_staged_rows_match_in_place_catch_up(asme, dev, monkeypatch):
         assert seen == [False, staged, staged, staged]
         out.append(_params(model))
         out.append({k: v.clone() for k, v in opt.state[model.item_table()].items() if torch.is_tensor(v)})
-    for a, b in ((out[0], out[2]), (out[1], out[3])):
+    for a, b in ((out[0], out[4]), (out[1], out[5]), (out[2], out[4]), (out[3], out[5])):
         for k in a:
             assert torch.equal(a[k], b[k]), k
