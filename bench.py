@@ -121,7 +121,7 @@ def parse():
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-sharded path even at N=1 (1-rank RCCL group): its overhead without the fabric")
     ap.add_argument("--cpu-batch", type=int, default=0, help="sequences per CPU-baseline step (0: --batch)")
-    ap.add_argument("--cpu-warmup", type=int, default=1)
+    ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--cpu-batch-1t", type=int, default=16, help="sequences of the single-thread CPU step")
     ap.add_argument("--sampler-sessions", type=int, default=16, help="sessions for the CPU sampler rate")
