@@ -364,6 +364,108 @@ __global__ __launch_bounds__(256) void lazy_row_kernel(const int64_t* __restrict
     if (!STAGE && lane == 0) last_step[r] = upto;
 }
 
+// Software-pipelined lazy replay: the full-table catch-up (flush(): every row brought to `upto`; rows == null) and
+// the staging of the step's unique rows (STAGE: rows[s] -> the compact buffers at slot s).  In lazy_row_kernel a
+// wave reads its slot's row id, waits, reads last_step, waits, reads the row, waits, replays and stores: at most one
+// row's 1.5 KB in flight per wave and none while it replays, so the flush ran at ~3 TB/s with the VALU half idle.
+// Here a wave owns RPW consecutive slots: one load brings all their row ids and one their last steps (lane i: slot
+// base + i), and the p/m/v of slot i + PF - 1 are requested before slot i is replayed (a PF-deep register ring), so
+// the row reads stream while the replay runs.  Same per-element operations (adam_elem2 / adam_decay2): same bits.
+#ifndef ASME_FLUSH_PIPE
+#define ASME_FLUSH_PIPE 1
+#endif
+#ifndef ASME_STAGE_PIPE
+#define ASME_STAGE_PIPE 1
+#endif
+#ifndef ASME_FLUSH_RPW
+#define ASME_FLUSH_RPW 16
+#endif
+#ifndef ASME_FLUSH_PF
+#define ASME_FLUSH_PF 4
+#endif
+constexpr int kPipeRows = ASME_FLUSH_RPW;  // slots per wave
+constexpr int kPipeDepth = ASME_FLUSH_PF;  // rows in the register ring (PF - 1 in flight during a replay)
+template <int NP, int RPW, int PF, bool STAGE>
+__global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restrict__ rows,
+                                                        const int32_t* __restrict__ count, int64_t cap,
+                                                        int32_t* __restrict__ last_step, float* __restrict__ p,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        const AdamHyper* __restrict__ hist, int32_t upto,
+                                                        float* __restrict__ sp, float* __restrict__ sm,
+                                                        float* __restrict__ sv) {
+    static_assert(RPW <= 64 && PF >= 2 && PF <= RPW, "ring depth");
+    constexpr int D = 128 * NP;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+    int64_t n = count ? (int64_t)*count : cap;
+    n = n < cap ? n : cap;
+    if (base >= n) return;  // wave-uniform
+    const int nr = (int)(n - base < RPW ? n - base : RPW);
+    const int64_t my_r = lane < nr ? (rows ? rows[base + lane] : base + lane) : 0;
+    const int32_t my_t = lane < nr ? last_step[my_r] : upto;
+    auto row_of = [&](int i) -> int64_t {  // slots past the end re-read the last row (never stored)
+        const int k = i < nr ? i : nr - 1;
+        if (!rows) return base + k;
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_r, k);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)my_r >> 32), k);
+        return (int64_t)(((uint64_t)hi << 32) | lo);
+    };
+    float2v P[PF][NP], M[PF][NP], Vv[PF][NP];
+    auto load = [&](int i, int slot) {
+        const int64_t r = row_of(i);
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            const int64_t off = r * D + 2 * lane + 128 * j;
+            const float2 a = *reinterpret_cast<const float2*>(p + off);
+            const float2 b = *reinterpret_cast<const float2*>(m + off);
+            const float2 c = *reinterpret_cast<const float2*>(v + off);
+            P[slot][j] = float2v{a.x, a.y};
+            M[slot][j] = float2v{b.x, b.y};
+            Vv[slot][j] = float2v{c.x, c.y};
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < PF - 1; ++i) load(i, i);
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        if (i + PF - 1 < RPW) load(i + PF - 1, (i + PF - 1) % PF);
+        const int sl = i % PF;
+        const int32_t t0 = __builtin_amdgcn_readlane(my_t, i);
+        if (i < nr && (STAGE || t0 < upto)) {
+            for (int32_t t = t0 + 1; t <= upto; ++t) {
+                const AdamHyper hp = hist[t];
+#pragma unroll
+                for (int j = 0; j < NP; ++j) {
+                    if (hp.wd != 0.f)
+                        adam_elem2(P[sl][j], float2v{0.f, 0.f}, M[sl][j], Vv[sl][j], hp);
+                    else
+                        adam_decay2(P[sl][j], M[sl][j], Vv[sl][j], hp);
+                }
+            }
+            const int64_t orow = STAGE ? base + i : row_of(i);
+            float* op = STAGE ? sp : p;
+            float* om = STAGE ? sm : m;
+            float* ov = STAGE ? sv : v;
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {
+                const int64_t off = orow * D + 2 * lane + 128 * j;
+                *reinterpret_cast<float2*>(op + off) = make_float2(P[sl][j].x, P[sl][j].y);
+                *reinterpret_cast<float2*>(om + off) = make_float2(M[sl][j].x, M[sl][j].y);
+                *reinterpret_cast<float2*>(ov + off) = make_float2(Vv[sl][j].x, Vv[sl][j].y);
+            }
+        }
+    }
+    if (!STAGE && lane < nr && my_t < upto) last_step[my_r] = upto;
+}
+template <int NP, bool STAGE>
+void launch_pipe(const int64_t* rows, const int32_t* count, int64_t cap, int32_t* last_step, float* p, float* m,
+                 float* v, const float* hist, int64_t upto, float* sp, float* sm, float* sv, hipStream_t s) {
+    const int64_t per_block = 4 * kPipeRows;
+    hipLaunchKernelGGL((lazy_pipe_kernel<NP, kPipeRows, kPipeDepth, STAGE>),
+                       dim3((unsigned)((cap + per_block - 1) / per_block)), dim3(256), 0, s, rows, count, cap,
+                       last_step, p, m, v, reinterpret_cast<const AdamHyper*>(hist), (int32_t)upto, sp, sm, sv);
+}
+
 #ifndef ASME_LAZY_ROW_WAVE
 #define ASME_LAZY_ROW_WAVE 1
 #endif
@@ -517,6 +619,15 @@ ASME_API int asme_lazy_adam_catch_up(const int64_t* rows, const int32_t* count, 
     ASME_CHECK_ARG(upto < hist_rows, "asme_lazy_adam_catch_up: step beyond the history capacity");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && upto >= 0 && upto < (1LL << 31), "asme_lazy_adam_catch_up: bad shape");
     if (cap == 0 || upto == 0) return 0;
+    if (ASME_FLUSH_PIPE && !rows && !count && row_wave_ok(dim) && v4_ok(dim, param, exp_avg, exp_avg_sq)) {
+        if (dim == 128)
+            launch_pipe<1, false>(rows, count, cap, last_step, param, exp_avg, exp_avg_sq, hist, upto, nullptr, nullptr,
+                                  nullptr, (hipStream_t)stream);
+        else
+            launch_pipe<2, false>(rows, count, cap, last_step, param, exp_avg, exp_avg_sq, hist, upto, nullptr, nullptr,
+                                  nullptr, (hipStream_t)stream);
+        ASME_LAUNCH_CHECK("asme_lazy_adam_catch_up");
+    }
     if (row_wave_ok(dim) && v4_ok(dim, param, exp_avg, exp_avg_sq)) {
         const dim3 g((unsigned)((cap + 3) / 4));
         if (dim == 128)
@@ -561,6 +672,17 @@ ASME_API int asme_lazy_adam_stage(const int64_t* rows, const int32_t* count, int
                        v4_ok(dim, staged_param, staged_exp_avg, staged_exp_avg_sq),
                    "asme_lazy_adam_stage: dim must be 32/64/128/256 and every row pointer 16-B aligned");
     if (cap == 0) return 0;
+    if (ASME_STAGE_PIPE && row_wave_ok(dim)) {
+        int32_t* ls = const_cast<int32_t*>(last_step);  // (not written in STAGE mode)
+        float *pp = const_cast<float*>(param), *mm = const_cast<float*>(exp_avg), *vv = const_cast<float*>(exp_avg_sq);
+        if (dim == 128)
+            launch_pipe<1, true>(rows, count, cap, ls, pp, mm, vv, hist, upto, staged_param, staged_exp_avg,
+                                 staged_exp_avg_sq, (hipStream_t)stream);
+        else
+            launch_pipe<2, true>(rows, count, cap, ls, pp, mm, vv, hist, upto, staged_param, staged_exp_avg,
+                                 staged_exp_avg_sq, (hipStream_t)stream);
+        ASME_LAUNCH_CHECK("asme_lazy_adam_stage");
+    }
     if (row_wave_ok(dim)) {
         const dim3 g((unsigned)((cap + 3) / 4));
         int32_t* ls = const_cast<int32_t*>(last_step);  // (not written in STAGE mode)

@@ -403,10 +403,13 @@ def test_occurrence_csr_equals_stable_sort(asme, dev, n, cap):
     assert torch.equal(off.cpu()[:U + 1], want_off[:U + 1])
 
 
-def test_lazy_adam_bit_exact_vs_dense(asme, dev):
-    """Exact catch-up: lazily replayed zero-gradient steps == the dense row update every step, bitwise."""
+@pytest.mark.parametrize("V,D", [(2000, 64), (2003, 128), (1601, 256)])
+def test_lazy_adam_bit_exact_vs_dense(asme, dev, V, D):
+    """Exact catch-up: lazily replayed zero-gradient steps == the dense row update every step, bitwise.  D = 128 / 256
+    stage and flush through the pipelined replay (lazy_pipe_kernel: 16 slots per wave, a ragged last wave here)."""
     torch.manual_seed(6)
-    V, D, T, steps = 2000, 64, 300, 7
+    T, steps = 300, 7
+    assert V // 5 >= T  # the narrow steps draw T distinct ids below V // 5
     base = torch.randn(V, D, device=dev)
     p_lazy = torch.nn.Parameter(base.clone())
     p_lazy._asme_table_grad = asme.ops.TableGrad()
@@ -436,6 +439,11 @@ def test_lazy_adam_bit_exact_vs_dense(asme, dev):
     assert torch.equal(p_lazy.detach(), p_eager.detach())
     st_l, st_e = o_lazy.state[p_lazy], o_eager.state[p_eager]
     assert torch.equal(st_l["exp_avg"], st_e["exp_avg"]) and torch.equal(st_l["exp_avg_sq"], st_e["exp_avg_sq"])
+    lazy = p_lazy._asme_table_grad.lazy
+    assert bool((lazy.last_step == steps).all())
+    snapshot = p_lazy.detach().clone()
+    o_lazy.flush()  # every row current: a second flush changes nothing
+    assert torch.equal(p_lazy.detach(), snapshot)
 
 
 def test_sasrec_sparse_lazy_matches_dense_training(asme, dev):
