@@ -124,6 +124,8 @@ def parse():
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--cpu-batch-1t", type=int, default=16, help="sequences of the single-thread CPU step")
+    ap.add_argument("--cpu-batch-masked", type=int, default=64,
+                    help="sequences per CPU-baseline step of the BERT4Rec / KeBERT4Rec workloads")
     ap.add_argument("--sampler-sessions", type=int, default=16, help="sessions for the CPU sampler rate")
     return ap.parse_args()
 
@@ -218,6 +220,48 @@ def cpu_baseline(args, V):
                       f"(this job's CPU share; the machine has {os.cpu_count()}), torch CPU fp32, {cpu_model_name()}"}
 
 
+def cpu_baseline_masked(args, model, V, kebert, n_genre):
+    """CPU restatement (oracle/asme_oracle.py bert4rec_logits / kebert4rec_logits, reference op order) of the C3 / C5
+    step timed on the host cores: the model's own initial parameters (reference state_dict keys) copied to the CPU,
+    the reference's full (B, L, |V|) logits + CrossEntropyLoss(ignore_index) (masked_training_module.py:93-111),
+    backward, torch.optim.Adam; dropout off.  A bounded sample: --cpu-batch-masked sequences of a 20 % cloze
+    batch (the full-catalogue logits, linear in B, dominate), --cpu-warmup + --cpu-steps steps."""
+    from oracle import asme_oracle as O
+    threads = cpu_share()
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().float().cpu().clone().requires_grad_(True) for k, v in model.state_dict().items()
+          if v.dtype.is_floating_point}
+    opt = torch.optim.Adam(list(sd.values()), lr=1e-3, betas=(0.9, 0.999), foreach=False)
+    B, L = args.cpu_batch_masked, args.seq_len
+    g = torch.Generator().manual_seed(4321)
+    seq = torch.randint(3, V, (B, L), generator=g)
+    masked = torch.rand(B, L, generator=g) < 0.2
+    target = torch.where(masked, seq, torch.zeros_like(seq))
+    inp = torch.where(masked, torch.ones_like(seq), seq)
+    genre = torch.where(inp > 0, seq % (n_genre - 1) + 1, 0)
+    times = []
+    for i in range(args.cpu_warmup + args.cpu_steps):
+        t0 = time.perf_counter()
+        opt.zero_grad(set_to_none=True)
+        if kebert:
+            logits = O.kebert4rec_logits(sd, inp, args.heads, {"genre": (genre, "content_embedding", n_genre)}, {})
+        else:
+            logits = O.bert4rec_logits(sd, inp, args.heads, tied=True)
+        loss = O.cross_entropy(logits.reshape(-1, logits.shape[-1]), target.reshape(-1))
+        loss.backward()
+        opt.step()
+        times.append(time.perf_counter() - t0)
+        print(f"[cpu_baseline] {args.workload} B={B} step {i + 1}/{args.cpu_warmup + args.cpu_steps}: "
+              f"{times[-1]:.2f} s", file=sys.stderr, flush=True)
+    per_step = sum(times[args.cpu_warmup:]) / args.cpu_steps
+    name = "KeBERT4Rec" if kebert else "BERT4Rec"
+    return {"value": round(B / per_step, 3), "unit": "sequences/s", "cores": threads, "kind": "port", "batch": B,
+            "s_per_step": round(per_step, 3), "machine_cpus": os.cpu_count(),
+            "sample": f"{name} cloze fwd+bwd+Adam, B={B} L={L} |V|={V} (full (B, L, |V|) logits + CE, as the "
+                      f"reference), {args.cpu_steps} timed steps after {args.cpu_warmup} warm-up, "
+                      f"{per_step:.2f} s/step on {threads} threads, torch CPU fp32, dropout off, {cpu_model_name()}"}
+
+
 def bench_bert4rec(args, asme, dev, world, rank):
     """BASELINE config C3: BERT4Rec (tied head), cloze masking p = 0.2 / last-item-only 0.1, B per GPU, full
     catalogue CE over |V| = items + 3.  Every step builds its batch on the GPU (collate + asme_cloze_mask) from
@@ -299,7 +343,11 @@ def bench_bert4rec(args, asme, dev, world, rank):
             "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
             "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0)}
     lb = committed_profile("logits_mfma_busy.json", {"workload": args.workload, "rows": 36966, "items": V, "dim": d})
-    rooflines = roofline_entries(timer.summary(), work, {}, lb.get("mfma_busy") if B == 1024 and L == 200 else None)
+    # HBM traffic per launch from the committed rocprofv3 PMC pass over this workload (tools/pmc_traffic.py)
+    tp = committed_profile(f"pmc_traffic_{args.workload}.json", {"batch": B, "seq_len": L, "items": args.items,
+                                                                   "dim": d, "layers": args.layers})
+    rooflines = roofline_entries(timer.summary(), work, tp.get("bytes_per_launch", {}),
+                                 lb.get("mfma_busy") if B == 1024 and L == 200 else None)
     name = "KeBERT4Rec" if kebert else "BERT4Rec"
     result = {"metric": f"training sequences/sec ({name} cloze, B={B} L={L} |V|={V}, fwd+bwd+Adam)",
               "value": round(B * world * args.steps / elapsed, 2), "unit": "sequences/s", "n_gpus": world,
@@ -312,6 +360,8 @@ def bench_bert4rec(args, asme, dev, world, rank):
                          "dim": d, "heads": H, "layers": args.layers, "dropout": args.dropout,
                          "fused_xent": asme.modules.FUSED_XENT, "parallelism": f"dp{world}"},
               "roofline": rooflines[0] if rooflines else None, "rooflines": rooflines, "cpu_baseline": None}
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_masked(args, model, V, kebert, n_genre)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist.is_initialized():

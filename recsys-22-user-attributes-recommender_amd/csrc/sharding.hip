@@ -18,12 +18,43 @@ using namespace asme;
 
 namespace {
 
-__global__ void claim_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V, int32_t* __restrict__ map) {
+// Block-level aggregation of the per-key global atomics (claim, CSR count and scatter).  A key on a large share of
+// the batch (PAD of short sessions, the cloze MASK token, a small attribute vocabulary) made every occurrence an
+// atomic on ONE address -- 0.34 ms per kernel for the 37k MASK occurrences of a KeBERT4Rec batch, against ~10 us
+// for uniform ids.  Each 256-thread block first combines its occurrences per key in an LDS hash table (512 slots,
+// linear probing, at most 256 keys: every insert terminates) and then issues one global atomic per distinct key.
+constexpr int kHashSlots = 512;
+struct BlockHash {
+    int32_t key[kHashSlots];
+    int32_t val[kHashSlots];
+    int32_t aux[kHashSlots];
+};
+__device__ __forceinline__ void hash_init(BlockHash& t, int32_t v0) {
+    for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x) {
+        t.key[j] = -1;
+        t.val[j] = v0;
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ int hash_insert(BlockHash& t, int32_t key) {  // key >= 0
+    uint32_t h = ((uint32_t)key * 2654435761u) >> 23;  // 9 bits
+    for (;;) {
+        const int32_t prev = atomicCAS(&t.key[h], -1, key);
+        if (prev == -1 || prev == key) return (int)h;
+        h = (h + 1) & (kHashSlots - 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void claim_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V,
+                                                    int32_t* __restrict__ map) {
+    __shared__ BlockHash t;
+    hash_init(t, INT32_MAX);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t id = ids[i];
-    if (id < 0 || id >= V) return;
-    atomicMin(reinterpret_cast<unsigned int*>(map + id), (unsigned int)i);
+    const int64_t id = i < n ? ids[i] : -1;
+    if (id >= 0 && id < V) atomicMin(&t.val[hash_insert(t, (int32_t)id)], (int32_t)i);
+    __syncthreads();
+    for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x)
+        if (t.key[j] >= 0) atomicMin(reinterpret_cast<unsigned int*>(map + t.key[j]), (unsigned int)t.val[j]);
 }
 
 __global__ void flag_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V, const int32_t* __restrict__ map,
@@ -205,6 +236,7 @@ ASME_API int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_
                             void* stream) {
     ASME_CHECK_ARG(ids && map && workspace && unique && count, "asme_dedup_ids: null pointer");
     ASME_CHECK_ARG(n >= 1 && n < (int64_t)1 << 31, "asme_dedup_ids: n must be in [1, 2^31)");
+    ASME_CHECK_ARG(vocab >= 1 && vocab < (int64_t)1 << 31, "asme_dedup_ids: vocab must be in [1, 2^31)");
     ASME_CHECK_ARG(workspace_bytes >= asme_dedup_workspace_bytes(n), "asme_dedup_ids: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -286,28 +318,53 @@ namespace {
 // (inverse -1: an id outside the table), which sorts last.  (1) per-key counts (integer atomics), (2) exclusive
 // scan -> seg_off, (3) scatter: each occurrence takes a position of its key's range by an atomic count-down (any
 // order), (4) each range is then put in increasing occurrence order -- the same arrays a stable sort gives, so the
-// sums are bit-reproducible.  Ranges of up to kShortSeg by their own thread (insertion sort), longer ones (popular
-// items) by a workgroup that ranks every element against the range (listed by (4), done by (5)).
+// sums are bit-reproducible.  Ranges of up to kShortSeg by their own thread (a sorting network), up to kLongSeg
+// (popular items) by a workgroup that ranks every element against the range (listed by (4), done by (5)), longer
+// ones -- a key on a large share of the batch: PAD of short sessions, the cloze MASK token, a small attribute
+// vocabulary; the quadratic ranking took 0.15 s for the 37k MASK occurrences of a KeBERT4Rec batch -- by a segmented
+// radix sort over at most n / kLongSeg segments (their list and bounds written by (4)).
 constexpr int kShortSeg = 16;
+constexpr int kLongSeg = 2048;
+inline int64_t max_huge(int64_t n) { return n / (kLongSeg + 1) + 1; }
 
 __device__ __forceinline__ int32_t occ_key(const int64_t* __restrict__ inverse, int64_t i, int64_t cap) {
     const int64_t k = inverse[i];
     return (int32_t)(k >= 0 && k < cap ? k : cap);
 }
 
-__global__ void csr_count_kernel(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
-                                 int32_t* __restrict__ cnt) {
+__global__ __launch_bounds__(256) void csr_count_kernel(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
+                                                        int32_t* __restrict__ cnt) {
+    __shared__ BlockHash t;
+    hash_init(t, 0);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(cnt + occ_key(inverse, i, cap), 1);
+    if (i < n) atomicAdd(&t.val[hash_insert(t, occ_key(inverse, i, cap))], 1);
+    __syncthreads();
+    for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x)
+        if (t.key[j] >= 0) atomicAdd(cnt + t.key[j], t.val[j]);
 }
 
-__global__ void csr_scatter_kernel(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
-                                   const int32_t* __restrict__ seg_off, int32_t* __restrict__ cnt,
-                                   int32_t* __restrict__ order, int32_t* __restrict__ sorted_slot) {
+// each block reserves one run of positions per key of its own (count-down from the key's count), its occurrences
+// take the places of that run in any order (put in occurrence order per range afterwards)
+__global__ __launch_bounds__(256) void csr_scatter_kernel(const int64_t* __restrict__ inverse, int64_t n,
+                                                          int64_t cap, const int32_t* __restrict__ seg_off,
+                                                          int32_t* __restrict__ cnt, int32_t* __restrict__ order,
+                                                          int32_t* __restrict__ sorted_slot) {
+    __shared__ BlockHash t;
+    hash_init(t, 0);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t k = 0;
+    int h = 0, r = 0;
+    if (i < n) {
+        k = occ_key(inverse, i, cap);
+        h = hash_insert(t, k);
+        r = atomicAdd(&t.val[h], 1);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x)
+        if (t.key[j] >= 0) t.aux[j] = atomicSub(cnt + t.key[j], t.val[j]) - t.val[j];
+    __syncthreads();
     if (i >= n) return;
-    const int32_t k = occ_key(inverse, i, cap);
-    const int32_t pos = seg_off[k] + atomicSub(cnt + k, 1) - 1;
+    const int32_t pos = seg_off[k] + t.aux[h] + r;
     order[pos] = (int32_t)i;
     sorted_slot[pos] = k;
 }
@@ -315,7 +372,8 @@ __global__ void csr_scatter_kernel(const int64_t* __restrict__ inverse, int64_t 
 // one thread per key: ranges of 2..kShortSeg sorted in registers (an odd-even transposition network over a padded
 // array: static indices only), longer ones appended to longs[1..] (longs[0] = their count)
 __global__ void csr_order_kernel(const int32_t* __restrict__ seg_off, int64_t n, int64_t cap,
-                                 int32_t* __restrict__ order, int32_t* __restrict__ longs) {
+                                 int32_t* __restrict__ order, int32_t* __restrict__ longs, int32_t* __restrict__ huge,
+                                 int32_t* __restrict__ hbeg, int32_t* __restrict__ hend) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > cap) return;
     const int32_t b = seg_off[k];
@@ -327,6 +385,12 @@ __global__ void csr_order_kernel(const int32_t* __restrict__ seg_off, int64_t n,
             order[b] = y;
             order[b + 1] = x;
         }
+        return;
+    }
+    if (len > kLongSeg) {  // (hbeg / hend of unused segments stay 0: empty)
+        const int t = atomicAdd(huge, 1);
+        hbeg[t] = b;
+        hend[t] = b + len;
         return;
     }
     if (len > kShortSeg) {
@@ -368,6 +432,17 @@ __global__ __launch_bounds__(256) void csr_long_kernel(const int32_t* __restrict
         for (int e = threadIdx.x; e < len; e += blockDim.x) order[b + e] = tmp[b + e];
         __syncthreads();
     }
+}
+
+// the radix-sorted huge ranges back into place
+__global__ __launch_bounds__(256) void csr_huge_copy_kernel(const int32_t* __restrict__ huge,
+                                                            const int32_t* __restrict__ hbeg,
+                                                            const int32_t* __restrict__ hend,
+                                                            const int32_t* __restrict__ sorted,
+                                                            int32_t* __restrict__ order) {
+    if ((int)blockIdx.x >= *huge) return;
+    const int32_t b = hbeg[blockIdx.x], e = hend[blockIdx.x];
+    for (int32_t i = b + (int32_t)threadIdx.x; i < e; i += 256) order[i] = sorted[i];
 }
 
 constexpr int kMaxContrib = 4;
@@ -545,12 +620,23 @@ __global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restric
 
 }  // namespace
 
+namespace {
+size_t csr_up(size_t x) { return (x + 255) & ~(size_t)255; }
+size_t csr_temp_bytes(int64_t n) {
+    size_t scan = 0, seg = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (int32_t*)nullptr, (int32_t*)nullptr, (int)(n + 1));
+    (void)hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, seg, (const int32_t*)nullptr, (int32_t*)nullptr, (int)n,
+                                                     (int)max_huge(n), (const int32_t*)nullptr,
+                                                     (const int32_t*)nullptr, 0, 32);
+    return scan > seg ? scan : seg;
+}
+}  // namespace
+
 ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
-    size_t temp = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (int32_t*)nullptr, (int32_t*)nullptr, (int)(n + 1));
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    // per-key counts (n + 1), long-range list (n + 2), rank scratch (n), scan temp
-    return (int64_t)(up((size_t)(n + 1) * 4) + up((size_t)(n + 2) * 4) + up((size_t)n * 4) + up(temp));
+    // per-key counts (n + 1), huge-range count + bounds (1 + 2 max_huge), long-range list (n + 2), rank / sort
+    // scratch (n), scan / segmented-sort temp
+    return (int64_t)(csr_up((size_t)(n + 1) * 4) + csr_up((size_t)(1 + 2 * max_huge(n)) * 4) +
+                     csr_up((size_t)(n + 2) * 4) + csr_up((size_t)n * 4) + csr_up(csr_temp_bytes(n)));
 }
 
 // inverse (n int64 slots < cap <= n) -> order (n int32 occurrence indices grouped by slot, increasing within a
@@ -563,14 +649,17 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     ASME_CHECK_ARG(n >= 1 && n < (int64_t)1 << 31 && cap >= 0 && cap <= n, "asme_occurrence_csr: bad size");
     ASME_CHECK_ARG(workspace_bytes >= asme_occurrence_csr_workspace(n), "asme_occurrence_csr: workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const int64_t nh = max_huge(n);
     char* ws = (char*)workspace;
     int32_t* cnt = (int32_t*)ws;
-    int32_t* longs = (int32_t*)(ws + up((size_t)(n + 1) * 4));
-    int32_t* tmp = (int32_t*)((char*)longs + up((size_t)(n + 2) * 4));
-    void* temp = (char*)tmp + up((size_t)n * 4);
+    int32_t* huge = (int32_t*)(ws + csr_up((size_t)(n + 1) * 4));
+    int32_t* hbeg = huge + 1;
+    int32_t* hend = hbeg + nh;
+    int32_t* longs = (int32_t*)((char*)huge + csr_up((size_t)(1 + 2 * nh) * 4));
+    int32_t* tmp = (int32_t*)((char*)longs + csr_up((size_t)(n + 2) * 4));
+    void* temp = (char*)tmp + csr_up((size_t)n * 4);
     size_t temp_bytes = (size_t)workspace_bytes - ((char*)temp - ws);
-    // counts of keys 0..cap and the long-range counter, zeroed together (longs follows cnt)
+    // counts of keys 0..cap, the huge-range count and bounds, the long-range counter: zeroed together (contiguous)
     if (hipMemsetAsync(cnt, 0, (char*)longs - ws + 4, s) != hipSuccess)
         return hip_status(hipGetLastError(), "asme_occurrence_csr: zero");
     hipLaunchKernelGGL(csr_count_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, cnt);
@@ -578,8 +667,17 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
         return hip_status(hipErrorUnknown, "asme_occurrence_csr: scan");
     hipLaunchKernelGGL(csr_scatter_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, seg_off, cnt, order,
                        sorted_slot);
-    hipLaunchKernelGGL(csr_order_kernel, dim3(nblk(cap + 1)), dim3(256), 0, s, seg_off, n, cap, order, longs);
+    hipLaunchKernelGGL(csr_order_kernel, dim3(nblk(cap + 1)), dim3(256), 0, s, seg_off, n, cap, order, longs, huge,
+                       hbeg, hend);
     hipLaunchKernelGGL(csr_long_kernel, dim3(64), dim3(256), 0, s, seg_off, n, cap, longs, order, tmp);
+    if (n > kLongSeg) {  // a huge range is possible: sort them (occurrence indices < n: only the bits n needs)
+        int bits = 1;
+        while (bits < 31 && ((int64_t)1 << bits) < n) ++bits;
+        if (hipcub::DeviceSegmentedRadixSort::SortKeys(temp, temp_bytes, order, tmp, (int)n, (int)nh, hbeg, hend, 0,
+                                                       bits, s) != hipSuccess)
+            return hip_status(hipErrorUnknown, "asme_occurrence_csr: huge-range sort");
+        hipLaunchKernelGGL(csr_huge_copy_kernel, dim3((unsigned)nh), dim3(256), 0, s, huge, hbeg, hend, tmp, order);
+    }
     ASME_LAUNCH_CHECK("asme_occurrence_csr");
 }
 

@@ -367,11 +367,13 @@ def test_deterministic_table_grad(asme, dev, D):
     assert (a.double() - want).abs().max().item() < 1e-4 * max(1.0, want.abs().max().item())
 
 
-@pytest.mark.parametrize("n,cap", [(1, 1), (7, 7), (5000, 5000), (70000, 70000), (3000, 2000)])
+@pytest.mark.parametrize("n,cap", [(1, 1), (7, 7), (5000, 5000), (70000, 70000), (3000, 2000), (5000, 1),
+                                   (204800, 60000)])
 def test_occurrence_csr_equals_stable_sort(asme, dev, n, cap):
     """asme_occurrence_csr (counting sort + per-range ordering) == a stable sort of the occurrences by slot:
     order, sorted_slot (cap for slot-less occurrences, sorted last) and seg_off, exactly.  Slots with one, two,
-    a few and thousands of occurrences (ranges longer than the register-sorted ones) and slot-less ones."""
+    a few, hundreds (workgroup-ranked ranges) and tens of thousands of occurrences (> 2048: the segmented radix sort
+    -- the PAD / MASK / small-vocabulary case) and slot-less ones."""
     L = asme._lib
     g = torch.Generator().manual_seed(n + cap)
     u = max(1, cap // 3)

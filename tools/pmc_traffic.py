@@ -4,7 +4,7 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes
 reads -> x2; WRITE_SIZE is exact for 16-B stores; both are reported in KiB.  An API call that launches
 several kernels is the sum of its kernels; the per-call value is the median over calls (the end-of-run
 flush launch of the lazy-Adam catch-up is an outlier, not a step).
-Usage: python tools/pmc_traffic.py <dir with pmc_FETCH_SIZE/ pmc_WRITE_SIZE/> <out.json> B L ITEMS DIM LAYERS
+Usage: python tools/pmc_traffic.py <dir with pmc_FETCH_SIZE/ pmc_WRITE_SIZE/> <out.json> B L ITEMS DIM LAYERS [WORKLOAD]
 """
 import collections
 import csv
@@ -33,7 +33,15 @@ MAP = [
     (r"residual_ln_fwd_kernel", "asme_residual_ln_fwd", True),
     (r"residual_ln_bwd_kernel", "asme_residual_ln_bwd", True),
     (r"ws_gemm_kernel", "asme_ws_linear", True),
+    # the fused logits + CE head (csrc/logits.hip): the engine's mode names the call; the operand splits that open
+    # a call are attributed to the call of the engine launch that follows them (see per_call)
+    (r"logits_engine_kernel<0", "asme_linear_xent_fwd", True),
+    (r"lce_finish_kernel", "asme_linear_xent_fwd", False),
+    (r"logits_engine_kernel<1", "asme_linear_xent_bwd", True),
+    (r"logits_engine_kernel<2", "asme_linear_xent_bwd", False),
+    (r"sum_parts_kernel", "asme_linear_xent_bwd", False),
 ]
+PENDING = r"split_planes_kernel"  # belongs to the next logits call
 # calls whose launches have different shapes (the bench's work figure is their mean): mean, not median
 MEAN = {"asme_ws_linear", "asme_linear_weight_grad"}
 
@@ -50,13 +58,19 @@ def load(path, counter):
 def per_call(rows, scale):
     calls = collections.defaultdict(list)
     cur = {}
+    pending = 0.0
     for _, name, b in rows:
+        if re.search(PENDING, name):
+            pending += b * scale
+            continue
         for rx, api, counts in MAP:
             if re.search(rx, name):
                 if counts or api not in cur:
                     calls[api].append(0.0)
                     cur[api] = True
-                calls[api][-1] += b * scale
+                calls[api][-1] += b * scale + (pending if counts else 0.0)
+                if counts:
+                    pending = 0.0
                 break
     return calls
 
@@ -73,8 +87,10 @@ def main():
             continue
         tot = [f[api][i] + w[api][i] for i in range(n)]
         res[api] = round(statistics.mean(tot) if api in MEAN else statistics.median(tot))
+    wl = sys.argv[8] if len(sys.argv) > 8 else "sasrec-neg"
     json.dump({"config": {"batch": B, "seq_len": L, "items": items, "dim": dim, "layers": layers},
-               "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py --steps 2",
+               "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py --workload {wl} "
+                         "--steps 2",
                "bytes_per_launch": res}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
