@@ -62,6 +62,11 @@ int asme_embedding_bwd_partials_count(void);
  * (hardware fp32 atomics; ids outside [0, vocab) are skipped). */
 int asme_scatter_add_rows(const float* rows, const int64_t* ids, int64_t n_rows, int64_t dim, float* grad,
                           int64_t vocab, float scale, void* stream);
+/* dest[ids[s]] = rows[s] for s < min(*count, cap) (device count; distinct ids): the dense nn.Embedding gradient
+ * written from the deduplicated, occurrence-ordered row sums (replaces embedding_dense_backward's scatter-add,
+ * core/models/common/layers/transformer_layers.py:55-80 item_embedding, without float atomics). */
+int asme_scatter_rows(const float* rows, const int64_t* ids, const int32_t* count, int64_t cap, int64_t dim,
+                      float* dest, int64_t vocab, void* stream);
 /* position-embedding gradient: grad_pos[p] (+)= sum_b rows[b*seq_len + p]; workspace n_chunks*seq_len*dim */
 int asme_position_grad(const float* rows, int64_t batch, int64_t seq_len, int64_t dim, float* workspace,
                        int64_t n_chunks, float* grad_pos, int accumulate, void* stream);

@@ -26,6 +26,7 @@ SIGNATURES = {
     "asme_embedding_bwd": [p, i64, i64, p, i64, i64, p, p, p, f32, u64, p, p, f32, u64, p, p, p, p, p, p, i64, p],
     "asme_embedding_bwd_partials_count": [],
     "asme_scatter_add_rows": [p, p, i64, i64, p, i64, f32, p],
+    "asme_scatter_rows": [p, p, p, i64, i64, p, i64, p],
     "asme_position_grad": [p, i64, i64, i64, p, i64, p, i32, p],
     "asme_reduce_rows": [p, i64, i64, p, i32, p],
     "asme_gather_sum_fwd": [p, i64, i64, i32, p, i64, i64, p, p, i32, p],

@@ -446,6 +446,24 @@ __global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float* __re
     }
 }
 
+// dest[ids[s]] = rows[s] for the s < *count first rows (distinct ids: the dedup's unique rows): one row per wave
+template <int VPL>
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restrict__ rows,
+                                                           const int64_t* __restrict__ ids,
+                                                           const int32_t* __restrict__ count, int64_t cap, int D,
+                                                           float* __restrict__ dest, int64_t V) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (s >= cap || s >= (int64_t)*count) return;
+    const int64_t id = ids[s];
+    if (id < 0 || id >= V) return;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int e = lane + 64 * j;
+        if (e < D) dest[id * D + e] = rows[s * D + e];
+    }
+}
+
 // sum over the batch of per-token rows -> per-position grad; grid (L, nchunk), partial per chunk
 __global__ __launch_bounds__(256) void pos_partial_kernel(const float* __restrict__ rows, int64_t B, int64_t L, int D,
                                                           int64_t chunk, float* __restrict__ part) {
@@ -678,6 +696,18 @@ ASME_API int asme_scatter_add_rows(const float* rows, const int64_t* ids, int64_
                                                       (hipStream_t)stream, rows, ids, n_rows, (int)dim, grad, vocab,
                                                       scale));
     ASME_LAUNCH_CHECK("asme_scatter_add_rows");
+}
+
+ASME_API int asme_scatter_rows(const float* rows, const int64_t* ids, const int32_t* count, int64_t cap, int64_t dim,
+                              float* dest, int64_t vocab, void* stream) {
+    ASME_CHECK_ARG(rows && ids && count && dest, "asme_scatter_rows: null pointer");
+    ASME_CHECK_ARG(dim >= 1 && dim <= 512 && cap >= 0, "asme_scatter_rows: bad shape");
+    if (cap == 0) return 0;
+    const dim3 grid((unsigned)((cap + kWavesPerBlock - 1) / kWavesPerBlock));
+    ASME_VPL_DISPATCH(vpl_of(dim), hipLaunchKernelGGL(scatter_rows_kernel<VPL>, grid, dim3(256), 0,
+                                                      (hipStream_t)stream, rows, ids, count, cap, (int)dim, dest,
+                                                      vocab));
+    ASME_LAUNCH_CHECK("asme_scatter_rows");
 }
 
 ASME_API int asme_position_grad(const float* rows, int64_t batch, int64_t seq_len, int64_t dim, float* workspace,

@@ -409,8 +409,7 @@ class _EmbeddingFn(torch.autograd.Function):
             if plan is not None:
                 plan.add_rows(ids, d_rows)
             else:
-                g_table = torch.zeros(V, D, device=dev, dtype=torch.float32)
-                call("asme_scatter_add_rows", ptr(d_rows), ptr(ids), T, D, ptr(g_table), V, 1.0, stream())
+                g_table = dense_table_grad(ids, d_rows, V, D)
         g_pos = None
         if ctx.has[0] and ctx.needs_input_grad[2]:
             L = spec.seq_len
@@ -468,6 +467,28 @@ class _GatherSumFn(torch.autograd.Function):
         if has_bias:
             g_bias = _reduce_rows(dout)
         return None, g_table, g_bias, None, None
+
+
+_DENSE_SLOT_MAPS = {}
+
+
+def dense_table_grad(ids: torch.Tensor, rows: torch.Tensor, V: int, D: int) -> torch.Tensor:
+    """nn.Embedding's dense (V, D) gradient (embedding_dense_backward) without float atomics: the occurrences are
+    deduplicated and summed per row in occurrence order (the sparse plan's ordered reduction), then written to their
+    rows (asme_scatter_rows).  Deterministic, and a hot id (the cloze MASK token: ~18 % of a BERT4Rec batch) no
+    longer serialises tens of thousands of atomics on one row (0.78 ms per C3 step)."""
+    dev = rows.device
+    key = (dev, V)
+    slot_map = _DENSE_SLOT_MAPS.get(key)
+    if slot_map is None:  # -1 at rest; every plan resets the entries it used
+        slot_map = _DENSE_SLOT_MAPS[key] = torch.full((V,), -1, dtype=torch.int32, device=dev)
+    plan = SparseTablePlan(None, [ids], slot_map, vocab=V, dim=D)
+    plan.add_rows(ids, rows)
+    g = torch.zeros(V, D, device=dev, dtype=torch.float32)
+    call("asme_scatter_rows", ptr(plan.grad_rows), ptr(plan.unique), ptr(plan.count), plan.capacity, D, ptr(g), V,
+         stream())
+    plan.release()
+    return g
 
 
 def scatter_add_rows(rows: torch.Tensor, ids: torch.Tensor, dest: torch.Tensor, scale: float = 1.0):

@@ -679,3 +679,21 @@ def test_gelu_pair_precision(asme, dev):
     assert float(rel_g[mask].max()) < 3e-5, float(rel_g[mask].max())
     assert float(rel_g[core].max()) < 3e-6, float(rel_g[core].max())
     assert float((d.double().cpu() - ref_d).abs().max()) < 2e-6  # GELU' crosses 0 near x = -0.75: absolute
+
+
+def test_dense_table_grad_deterministic_with_hot_id(asme, dev):
+    """The dense nn.Embedding gradient (ops.dense_table_grad: dedup + occurrence-ordered row sums + asme_scatter_rows)
+    equals the float64 index_add within fp32 summation error and is bitwise reproducible, with a hot id on 40 % of
+    the occurrences (the cloze MASK token) and ids that never occur (zero rows)."""
+    torch.manual_seed(11)
+    V, D, n = 3001, 128, 40000
+    ids = torch.randint(3, V, (n,), device=dev)
+    ids[torch.rand(n, device=dev) < 0.4] = 1
+    rows = torch.randn(n, D, device=dev)
+    want = torch.zeros(V, D, dtype=torch.float64).index_add_(0, ids.cpu(), rows.cpu().double())
+    g1 = asme.ops.dense_table_grad(ids, rows, V, D)
+    g2 = asme.ops.dense_table_grad(ids, rows, V, D)
+    assert torch.equal(g1, g2)
+    err = (g1.cpu().double() - want).abs().max().item()
+    assert err <= 1e-5 * want.abs().max().item() + 1e-6, err
+    assert not g1[2].any()  # an id that never occurs
