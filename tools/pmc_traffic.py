@@ -25,6 +25,8 @@ MAP = [
     (r"lazy_catch_up(_v4)?_kernel", "asme_lazy_adam_catch_up", True),
     (r"lazy_apply(_v4)?_kernel", "asme_lazy_adam_apply", True),
     (r"lazy_stage_v4_kernel", "asme_lazy_adam_stage", True),
+    (r"lazy_row_kernel<\d+, true>", "asme_lazy_adam_stage", True),
+    (r"lazy_pipe_kernel<\d+, \d+, \d+, true>", "asme_lazy_adam_stage", True),
     (r"lazy_apply_staged_v4_kernel", "asme_lazy_adam_apply_staged", True),
     (r"sampled_fwd_kernel", "asme_sampled_logits_fwd", True),
     (r"sampled_bwd_kernel", "asme_sampled_logits_bwd", True),
