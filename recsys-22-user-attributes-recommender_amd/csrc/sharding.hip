@@ -318,13 +318,16 @@ namespace {
 // (inverse -1: an id outside the table), which sorts last.  (1) per-key counts (integer atomics), (2) exclusive
 // scan -> seg_off, (3) scatter: each occurrence takes a position of its key's range by an atomic count-down (any
 // order), (4) each range is then put in increasing occurrence order -- the same arrays a stable sort gives, so the
-// sums are bit-reproducible.  Ranges of up to kShortSeg by their own thread (a sorting network), up to kLongSeg
+// sums are bit-reproducible.  Ranges of up to kShortSeg by their own thread (a sorting network), up to kLongSeg = 256
 // (popular items) by a workgroup that ranks every element against the range (listed by (4), done by (5)), longer
 // ones -- a key on a large share of the batch: PAD of short sessions, the cloze MASK token, a small attribute
 // vocabulary; the quadratic ranking took 0.15 s for the 37k MASK occurrences of a KeBERT4Rec batch -- by a segmented
 // radix sort over at most n / kLongSeg segments (their list and bounds written by (4)).
 constexpr int kShortSeg = 16;
-constexpr int kLongSeg = 2048;
+#ifndef ASME_LONG_SEG
+#define ASME_LONG_SEG 256
+#endif
+constexpr int kLongSeg = ASME_LONG_SEG;  // (a 2,048-long range took ~100 us in one workgroup)
 inline int64_t max_huge(int64_t n) { return n / (kLongSeg + 1) + 1; }
 
 __device__ __forceinline__ int32_t occ_key(const int64_t* __restrict__ inverse, int64_t i, int64_t cap) {

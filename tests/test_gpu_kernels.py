@@ -372,7 +372,7 @@ def test_deterministic_table_grad(asme, dev, D):
 def test_occurrence_csr_equals_stable_sort(asme, dev, n, cap):
     """asme_occurrence_csr (counting sort + per-range ordering) == a stable sort of the occurrences by slot:
     order, sorted_slot (cap for slot-less occurrences, sorted last) and seg_off, exactly.  Slots with one, two,
-    a few, hundreds (workgroup-ranked ranges) and tens of thousands of occurrences (> 2048: the segmented radix sort
+    a few, hundreds (ranges over 256: the segmented radix sort) and tens of thousands of occurrences (also sorted
     -- the PAD / MASK / small-vocabulary case) and slot-less ones."""
     L = asme._lib
     g = torch.Generator().manual_seed(n + cap)
