@@ -406,7 +406,7 @@ def main():
         module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok,
                                                                               metrics=None, vocab=V)
         module.broadcast_dense_parameters()
-        step_fn = lambda b, i: asme.sharded.train_step(module, opt, b, i)  # noqa: E731
+        step_fn = None  # set below: each step also starts the next batch's id routing (module.prefetch)
     else:
         module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
                                                                table_grad=args.table_grad)
@@ -432,8 +432,30 @@ def main():
         def get_batch(i):
             return batches[i % 2]
 
+    if sharded:
+        ahead = {}
+
+        def batch_at(j):
+            b = ahead.pop(j, None)
+            return b if b is not None else get_batch(j)
+
+        last = args.warmup + args.steps - 1
+
+        def step_fn(b_unused, i, j=None):  # j: absolute batch index (warm-up i, timed warmup + i)
+            cur = batch_at(j)
+            nxt = None
+            if j < last and j != args.warmup - 1:  # (no prefetch across the warm-up / timed boundary)
+                nxt = ahead[j + 1] = get_batch(j + 1)
+            asme.sharded.train_step(module, opt, cur, i, next_batch=nxt)
+
+        def run(j, i):
+            step_fn(None, i, j)
+    else:
+        def run(j, i):
+            step_fn(get_batch(j), i)
+
     for i in range(args.warmup):
-        step_fn(get_batch(i), i)
+        run(i, i)
     torch.cuda.synchronize()
 
     # per-kernel device time of the dominant kernel (HIP events on the launching stream)
@@ -459,7 +481,7 @@ def main():
     asme.ops.SparseTablePlan.release = _release
     for i in range(args.steps):
         with timer if i >= args.steps - instrumented_steps(args.steps) else contextlib.nullcontext():
-            step_fn(get_batch(args.warmup + i), i)
+            run(args.warmup + i, i)
     # lazily deferred zero-gradient Adam updates of the item table are part of the work: apply them all
     # (exact dense-Adam state) inside the timed region, timed on its own
     f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -102,6 +102,13 @@ class RowShardExchange:
         """route the requester's unique global ids to their owners (count: int32 (1,) device tensor, only
         unique[:count] are live -- the dedup count, read on the device; the per-owner counts below are the step's
         one host sync)"""
+        return self.request_end(self.request_begin(unique, count))
+
+    def request_begin(self, unique: torch.Tensor, count: Optional[torch.Tensor] = None):
+        """first half of request(): owner bucketing and the exchange of the per-owner counts are enqueued and the
+        counts are copied to pinned host memory without waiting; request_end() reads them.  Issued a step ahead
+        (ShardedSequenceNextItemPredictionTrainingModule.prefetch), the host's read of the split sizes RCCL needs
+        no longer drains the GPU's queue."""
         W = self.world
         if unique.is_cuda:  # stable owner bucketing in one counting-sort pass (asme_bucket_by_owner)
             order, send_local, send_counts_t, pos = ops.bucket_by_owner(unique, W, count)
@@ -116,9 +123,23 @@ class RowShardExchange:
             pos[order] = torch.arange(len(order), dtype=order.dtype)
         recv_counts_t = torch.empty_like(send_counts_t)
         _all_to_all(recv_counts_t, send_counts_t, group=self.group)
-        counts = torch.stack([send_counts_t, recv_counts_t]).cpu()  # one host sync per step
-        sc, rc = counts[0].tolist(), counts[1].tolist()
-        recv_local = torch.empty(sum(rc), dtype=torch.int64, device=unique.device)
+        counts = torch.stack([send_counts_t, recv_counts_t])
+        event = None
+        if counts.is_cuda:
+            host = torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
+            host.copy_(counts, non_blocking=True)
+            event = torch.cuda.Event()
+            event.record()
+        else:
+            host = counts
+        return (order, send_local, pos, host, event, unique.device)
+
+    def request_end(self, pending) -> ExchangeState:
+        order, send_local, pos, host, event, dev = pending
+        if event is not None:
+            event.synchronize()  # the step's one host sync
+        sc, rc = host[0].tolist(), host[1].tolist()
+        recv_local = torch.empty(sum(rc), dtype=torch.int64, device=dev)
         _all_to_all(recv_local, send_local[:sum(sc)], rc, sc, group=self.group)
         return ExchangeState(order[:sum(sc)], sc, rc, recv_local, pos)
 
@@ -158,6 +179,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         self._req_map: Optional[torch.Tensor] = None
         self._own_map: Optional[torch.Tensor] = None
         self._pending = None
+        self._prefetched = None  # (id-set keys, requester plan, request_begin state) of the next step
 
     def broadcast_dense_parameters(self, src: int = 0):
         """make the replicated (non-table) parameters identical on every rank"""
@@ -171,16 +193,48 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
             self._req_map = torch.full((self.vocab,), -1, dtype=torch.int32, device=dev)
             self._own_map = torch.full((max(1, self.exchange.local_rows),), -1, dtype=torch.int32, device=dev)
 
+    @staticmethod
+    def _keys(id_sets):
+        return tuple((x.data_ptr(), tuple(x.shape)) for x in id_sets)
+
+    def prefetch(self, batch):
+        """Start the routing of the NEXT step's ids now: its dedup, owner bucketing and the exchange of the
+        per-owner counts are enqueued, and the counts copied to the host asynchronously.  Called after the
+        current step's forward (sharded.train_step's next_batch), the host reads those split sizes while the GPU
+        still runs the current step's backward, instead of draining the queue at the next step's start.  The
+        batch's id tensors must be the ones the next training_step receives.  Collective: every rank calls it at
+        the same point."""
+        self.cancel_prefetch()
+        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME))
+        id_sets = [batch[ITEM_SEQ_ENTRY_NAME], batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]]
+        self._maps(self.model.item_table().device)
+        req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
+        self._prefetched = (self._keys(id_sets), id_sets, req, self.exchange.request_begin(req.unique, req.count))
+
+    def cancel_prefetch(self):
+        """drop a prefetched request that will not be used (its counts exchange is complete on every rank)"""
+        if self._prefetched is not None:
+            self._prefetched[2].release()
+            self._prefetched = None
+
     def _fetch(self, id_sets, train: bool):
         """dedup the ids of `id_sets`, route them to their owners, gather the (caught-up) rows and return
         (exchange state, owner plan or None, compact rows in send order, each id set remapped to them)"""
         shard = self.model.item_table()
         self._maps(shard.device)
-        # 1. requester: dedup every id of the step
-        req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
-        # 2. route ids to owners (the dedup count stays on the device); owners bring their rows up to date (lazy
-        # Adam: staged in slot order, or caught up in the table) and gather them
-        st = self.exchange.request(req.unique, req.count)
+        pre, self._prefetched = self._prefetched, None
+        if pre is not None and pre[0] == self._keys(id_sets):
+            # 1.-2. dedup and the counts exchange were issued a step ahead (prefetch)
+            req = pre[2]
+            st = self.exchange.request_end(pre[3])
+        else:
+            if pre is not None:
+                pre[2].release()
+            # 1. requester: dedup every id of the step
+            req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
+            # 2. route ids to owners (the dedup count stays on the device); owners bring their rows up to date
+            # (lazy Adam: staged in slot order, or caught up in the table) and gather them
+            st = self.exchange.request(req.unique, req.count)
         own = None
         src, src_ids = shard.detach(), st.recv_local
         if train:
@@ -288,8 +342,12 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
                                   "catalog_ranks / sharded.catalog_topk")
 
 
-def train_step(module, optimizer, batch, batch_idx: int = 0):
+def train_step(module, optimizer, batch, batch_idx: int = 0, next_batch=None):
+    """one sharded training step; with next_batch (the batch the following call will receive) the next step's id
+    routing is started after this step's forward (module.prefetch), overlapping its host sync with the backward"""
     out = module.training_step(batch, batch_idx)
+    if next_batch is not None:
+        module.prefetch(next_batch)
     loss = out["loss"]
     loss.backward()
     module.after_backward()

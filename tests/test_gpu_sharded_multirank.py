@@ -83,9 +83,13 @@ def _worker(rank, world, port, cfg, q):
         opt = module.configure_optimizers()
         per = B // world
         losses = []
-        for s, b in enumerate(batches):
-            part = {k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()}
-            losses.append(float(asme.sharded.train_step(module, opt, part, s)))
+        parts = [{k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()} for b in batches]
+        for s, part in enumerate(parts):
+            # the next step's id routing started after this step's forward (module.prefetch), except after step 1
+            # (step 2 routes its ids inline)
+            nxt = parts[s + 1] if s + 1 < len(parts) and s != 1 else None
+            losses.append(float(asme.sharded.train_step(module, opt, part, s, next_batch=nxt)))
+        module.prefetch(parts[0])  # a prefetch nobody consumes: the next _fetch (evaluation) must discard it
         opt.flush()
         got = {k: v.detach().cpu() for k, v in model.state_dict().items()}
         errs = {}
