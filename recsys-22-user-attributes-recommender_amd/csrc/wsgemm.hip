@@ -58,9 +58,20 @@ struct WsEpi {
 };
 
 __device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s ^ (r & 15)); }
-__device__ __forceinline__ void bstore(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+// Output stores of the wide launches (N >= kNtMinN: the QKV projection, the FFN's first GEMM and its GELU form) carry
+// the non-temporal hint (aux bit 1, nt): measured alone (tools/probe/ab_ws.py, same process) N = 512 185 -> 148 us,
+// GELU forward 318 -> 286 us, N = 384 120 -> 105 us; the N = 128 launches are unchanged or slower with it (K = 384
+// input gradient 116 -> 121 us), so they keep the default policy.  (sc1 stores: no change.)
+#ifndef ASME_WS_NT_MIN_N
+#define ASME_WS_NT_MIN_N 384
+#endif
+constexpr int kNtMinN = ASME_WS_NT_MIN_N;
+__device__ __forceinline__ void bstore(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
     const u32v4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 0);
+    if (nt)  // (wave-uniform)
+        __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 2);
+    else
+        __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 0);
 }
 __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     const u32v4 u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
@@ -128,6 +139,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         return X + (m < M ? m : M - 1) * ep.ldx + ep.kofs + 8 * g;
     };
     const __amdgpu_buffer_rsrc_t yr = rsrc(Y, M * N * 4);
+    const bool nt_out = N >= kNtMinN;
     // the second operand stream of the epilogue: the activation factor (GELU forward writes / backward reads it) or,
     // for WS_ACCUM (second K half), Y itself -- read at the tile boundary like the factor, so the epilogue's
     // read-modify-write never drains the X ring (a load right before the store made the wave wait for vmcnt(0))
@@ -182,10 +194,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             const float4 v = *reinterpret_cast<const float4*>(stg + (idx / NB4) * SROW + 4 * (idx % NB4));
             const uint32_t off = staged_off(ct, srow0);
             if constexpr (EPI == WS_STORE) {
-                bstore(v, yr, off);
+                bstore(v, yr, off, nt_out);
             } else if constexpr (EPI == WS_ACCUM) {
                 const float4 o = pre[ct];
-                bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off);
+                bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off, nt_out);
             } else if constexpr (EPI == WS_GELU_DROP) {
                 // (a lane holds one 4-element chunk here: its own half of the chunk pair's Philox block)
                 float u[4] = {1.f, 1.f, 1.f, 1.f};
@@ -195,21 +207,21 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                 gelu_erf_and_grad(v.y, gl[1], gd[1]);
                 gelu_erf_and_grad(v.z, gl[2], gd[2]);
                 gelu_erf_and_grad(v.w, gl[3], gd[3]);
-                bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off);
-                bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off);
+                bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off, nt_out);
+                bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off, nt_out);
             } else {
                 const float4 f = pre[ct];
-                bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off);
+                bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off, nt_out);
             }
             return;
         }
         const uint32_t off = soff + ct * 64;
         float4 v = stash[ct];
         if constexpr (EPI == WS_STORE) {
-            bstore(v, yr, off);
+            bstore(v, yr, off, nt_out);
         } else if constexpr (EPI == WS_ACCUM) {
             const float4 o = pre[ct];
-            bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off);
+            bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off, nt_out);
         } else if constexpr (EPI == WS_GELU_DROP) {
             float u[4] = {1.f, 1.f, 1.f, 1.f};
             if (ep.p > 0.f) {
@@ -224,11 +236,11 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             gelu_erf_and_grad(v.y, gl[1], gd[1]);
             gelu_erf_and_grad(v.z, gl[2], gd[2]);
             gelu_erf_and_grad(v.w, gl[3], gd[3]);
-            bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off);
-            bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off);
+            bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off, nt_out);
+            bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off, nt_out);
         } else {
             const float4 f = pre[ct];
-            bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off);
+            bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off, nt_out);
         }
     };
     floatx4 acc[CT];
