@@ -449,9 +449,15 @@ __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restric
 #pragma unroll
             for (int j = 0; j < NP; ++j) {
                 const int64_t off = orow * D + 2 * lane + 128 * j;
-                *reinterpret_cast<float2*>(op + off) = make_float2(P[sl][j].x, P[sl][j].y);
-                *reinterpret_cast<float2*>(om + off) = make_float2(M[sl][j].x, M[sl][j].y);
-                *reinterpret_cast<float2*>(ov + off) = make_float2(Vv[sl][j].x, Vv[sl][j].y);
+                if (STAGE) {  // (read again by this step's gathers)
+                    *reinterpret_cast<float2*>(op + off) = make_float2(P[sl][j].x, P[sl][j].y);
+                    *reinterpret_cast<float2*>(om + off) = make_float2(M[sl][j].x, M[sl][j].y);
+                    *reinterpret_cast<float2*>(ov + off) = make_float2(Vv[sl][j].x, Vv[sl][j].y);
+                } else {
+                    table_store2(op + off, P[sl][j].x, P[sl][j].y);
+                    table_store2(om + off, M[sl][j].x, M[sl][j].y);
+                    table_store2(ov + off, Vv[sl][j].x, Vv[sl][j].y);
+                }
             }
         }
     }
@@ -540,9 +546,9 @@ __global__ __launch_bounds__(256) void lazy_apply_staged_v4_kernel(
     const AdamHyper hp = hist[step];
     adam_elem4(P, G, M, Vv, hp);
     const int64_t off = r * D + c;
-    *reinterpret_cast<float4*>(p + off) = P;
-    *reinterpret_cast<float4*>(m + off) = M;
-    *reinterpret_cast<float4*>(v + off) = Vv;
+    table_store4(p + off, P);
+    table_store4(m + off, M);
+    table_store4(v + off, Vv);
     if (lane % LPR == 0) last_step[r] = step;
 }
 

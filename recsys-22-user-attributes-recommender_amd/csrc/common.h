@@ -173,6 +173,27 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// Stores of item-table rows (the optimizer's p / m / v write-back): a row is not read again until a later step
+// touches it, so they carry the non-temporal hint instead of displacing the step's working set from the L2 / MALL.
+#ifndef ASME_TABLE_NT
+#define ASME_TABLE_NT 1
+#endif
+__device__ __forceinline__ void table_store4(float* p, const float4& v) {
+#if ASME_TABLE_NT
+    __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w}, reinterpret_cast<floatx4*>(p));
+#else
+    *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+__device__ __forceinline__ void table_store2(float* p, float a, float b) {
+#if ASME_TABLE_NT
+    typedef float floatx2_t __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(floatx2_t{a, b}, reinterpret_cast<floatx2_t*>(p));
+#else
+    *reinterpret_cast<float2*>(p) = make_float2(a, b);
+#endif
+}
+
 struct Bf3 {
     bf16x8 h, m, l;
 };

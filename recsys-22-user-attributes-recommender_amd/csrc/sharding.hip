@@ -495,9 +495,9 @@ __device__ __forceinline__ void apply_grad4(const TableApply& A, int64_t s, int 
     adam_elem4(P, G, M, V, hp);
     const int64_t r = A.rows[s];
     const int64_t off = r * dim + c0;
-    *reinterpret_cast<float4*>(A.p + off) = P;
-    *reinterpret_cast<float4*>(A.m + off) = M;
-    *reinterpret_cast<float4*>(A.v + off) = V;
+    table_store4(A.p + off, P);
+    table_store4(A.m + off, M);
+    table_store4(A.v + off, V);
     if (c0 == 0) A.last_step[r] = A.step;
 }
 
