@@ -23,7 +23,7 @@ namespace {
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kMaxSpecial = 8;
-constexpr int kSessLds = 512;  // session items staged in LDS per wave (4 KiB)
+constexpr int kSessLds = 2048;  // session items staged in LDS per workgroup (16 KiB)
 
 __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
 
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void last_item_mask_kernel(const int64_t* __re
 }
 
 // ------------------------------------------------------------------------------------- pos / neg sampler
-// One wave per session.  x, pos: the collated s[:-1], s[1:]; neg: for each kept position one id drawn uniformly
+// One workgroup per session.  x, pos: the collated s[:-1], s[1:]; neg: for each kept position one id drawn uniformly
 // from [0, V) and redrawn (next Philox counter) while it is special or occurs ANYWHERE in the full session (the
 // exclusion set of the reference is the whole session, not the truncated window).  err bit 0: a session with
 // no admissible id (the reference's multinomial raises), bit 1: a session shorter than 2 (AssertionError).
@@ -100,35 +100,34 @@ __global__ __launch_bounds__(256) void posneg_kernel(const int64_t* __restrict__
                                                      int64_t pad, uint64_t seed, int64_t* __restrict__ x,
                                                      int64_t* __restrict__ pos, int64_t* __restrict__ neg,
                                                      int64_t* __restrict__ out_len, int* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (b >= B) return;
+    // one workgroup per session; its waves take the 64-position chunks in turn (one wave per session left a
+    // 1,024-session batch with one wave per SIMD and every latency exposed)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t b = blockIdx.x;
+    if (b >= B) return;  // (workgroup-uniform)
     const int64_t s = batch_idx[b];
     const bool ok = s >= 0 && s < n_sessions;
     const int64_t beg = ok ? offsets[s] : 0, end = ok ? offsets[s + 1] : 0;
     const int64_t m = end - beg;  // session length (x, pos, neg have m - 1 entries before truncation)
     if (m < 2) {
-        if (lane == 0 && err) atomicOr(err, 2);
-        for (int64_t i = lane; i < L; i += 64) x[b * L + i] = pos[b * L + i] = neg[b * L + i] = pad;
-        if (lane == 0 && out_len) out_len[b] = 0;
+        if (threadIdx.x == 0 && err) atomicOr(err, 2);
+        for (int64_t i = threadIdx.x; i < L; i += blockDim.x) x[b * L + i] = pos[b * L + i] = neg[b * L + i] = pad;
+        if (threadIdx.x == 0 && out_len) out_len[b] = 0;
         return;
     }
     const int64_t n = (m - 1) < L ? (m - 1) : L;  // kept positions: the last n of the m - 1
     const int64_t first = m - 1 - n;              // index (into x) of the first kept position
-    // the session (the exclusion set) staged in this wave's LDS slice when it fits (else scanned in place)
-    __shared__ int64_t sess_lds[kWavesPerBlock][kSessLds];
-    int64_t* sl = sess_lds[threadIdx.x >> 6];
+    // the session (the exclusion set) staged in LDS when it fits (else scanned in place)
+    __shared__ int64_t sl[kSessLds];
     const bool in_lds = m <= kSessLds;
     if (in_lds)
-        for (int64_t j = lane; j < m; j += 64) sl[j] = flat[beg + j];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int64_t* scan = in_lds ? sl : flat + beg;
+        for (int64_t j = threadIdx.x; j < m; j += blockDim.x) sl[j] = flat[beg + j];
+    __syncthreads();
     int64_t sp[kMaxSpecial];
 #pragma unroll
     for (int k = 0; k < kMaxSpecial; ++k) sp[k] = k < n_special ? special[k] : -1;
     bool any_fail = false;
-    for (int64_t i0 = 0; i0 < L; i0 += 64) {
+    for (int64_t i0 = 64 * wave; i0 < L; i0 += 64 * kWavesPerBlock) {
         const int64_t i = i0 + lane;
         const bool live = i < n;
         int64_t cand = pad;
@@ -144,7 +143,27 @@ __global__ __launch_bounds__(256) void posneg_kernel(const int64_t* __restrict__
                 bool bad = false;
 #pragma unroll
                 for (int k = 0; k < kMaxSpecial; ++k) bad = bad || cand == sp[k];
-                for (int64_t j = 0; j < m && !bad; ++j) bad = scan[j] == cand;
+                // eight independent reads per trip (indices clamped to the session, no short circuit), from the LDS
+                // copy by LDS instructions: with one wave per SIMD every dependent round trip of the one-at-a-time
+                // scan through a generic pointer was exposed (66 us per 1,024-session batch)
+                auto scan8 = [&](const int64_t* src) {
+                    for (int64_t j = 0; j < m && !bad; j += 8) {
+                        int64_t v8[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) v8[u] = src[j + u < m ? j + u : m - 1];
+                        __builtin_amdgcn_sched_barrier(0);  // all eight reads issued before the first compare
+                        bool hit = false;
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) hit |= v8[u] == cand;
+                        bad = hit;
+                    }
+                };
+                if (!bad) {
+                    if (in_lds)
+                        scan8(sl);
+                    else
+                        scan8(flat + beg);
+                }
                 need = bad && ++attempt < 4096u;
                 if (bad && !need) {
                     any_fail = true;
@@ -159,7 +178,7 @@ __global__ __launch_bounds__(256) void posneg_kernel(const int64_t* __restrict__
         }
     }
     if (__ballot(any_fail) && lane == 0 && err) atomicOr(err, 1);
-    if (lane == 0 && out_len) out_len[b] = n;
+    if (threadIdx.x == 0 && out_len) out_len[b] = n;
 }
 
 // ------------------------------------------------------------------------------------------------ cloze
@@ -256,8 +275,7 @@ ASME_API int asme_posneg_sample(const int64_t* flat, const int64_t* offsets, int
     ASME_CHECK_ARG(n_special >= 0 && n_special <= kMaxSpecial && (n_special == 0 || special_ids),
                    "asme_posneg_sample: at most 8 special ids");
     if (batch == 0) return 0;
-    const dim3 grid((unsigned)((batch + kWavesPerBlock - 1) / kWavesPerBlock));
-    hipLaunchKernelGGL(posneg_kernel, grid, dim3(64 * kWavesPerBlock), 0, (hipStream_t)stream, flat, offsets,
+    hipLaunchKernelGGL(posneg_kernel, dim3((unsigned)batch), dim3(64 * kWavesPerBlock), 0, (hipStream_t)stream, flat, offsets,
                        n_sessions, batch_idx, batch, seq_len, vocab, special_ids, n_special, pad, seed, x, pos, neg,
                        out_len, err_flag);
     ASME_LAUNCH_CHECK("asme_posneg_sample");
