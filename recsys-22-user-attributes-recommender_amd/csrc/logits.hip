@@ -434,13 +434,18 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
 }
 
 // one block: lse[q] = merge of the chunks; out[0] = mean over valid rows of lse - s_t (NaN if none), out[1] = count
-__global__ __launch_bounds__(1024) void lce_finish_kernel(const float* __restrict__ part, int64_t n, int nchunks,
-                                                          const int64_t* __restrict__ targets, int64_t ignore,
-                                                          int64_t V, const float* __restrict__ tlogit,
-                                                          float* __restrict__ lse, float* __restrict__ out) {
-    __shared__ float sa[1024], sc[1024];
+// The forward's finish, in two launches (one 1,024-thread block had merged every row's chunk partials alone:
+// 0.19 ms per C3 step for 37k rows x 53 chunks): lce_rows_kernel merges each row's partials into its lse and sums
+// its block's (loss, count) in a fixed tree; lce_finish_kernel adds the block sums in a fixed order.
+constexpr int kLceRows = 256;
+__global__ __launch_bounds__(kLceRows) void lce_rows_kernel(const float* __restrict__ part, int64_t n, int nchunks,
+                                                            const int64_t* __restrict__ targets, int64_t ignore,
+                                                            int64_t V, const float* __restrict__ tlogit,
+                                                            float* __restrict__ lse, float* __restrict__ bsum) {
+    __shared__ float sa[kLceRows], sc[kLceRows];
+    const int64_t q = (int64_t)blockIdx.x * kLceRows + threadIdx.x;
     float acc = 0.f, cnt = 0.f;
-    for (int64_t q = threadIdx.x; q < n; q += blockDim.x) {
+    if (q < n) {
         float m = -INFINITY, s = 0.f;
         for (int k = 0; k < nchunks; ++k) {
             const float m2 = part[((int64_t)k * n + q) * 2], s2 = part[((int64_t)k * n + q) * 2 + 1];
@@ -452,17 +457,40 @@ __global__ __launch_bounds__(1024) void lce_finish_kernel(const float* __restric
         const float l = m + logf(s);
         lse[q] = l;
         if (valid_target(targets[q], ignore, V)) {
-            acc += l - tlogit[q];
-            cnt += 1.f;
+            acc = l - tlogit[q];
+            cnt = 1.f;
         }
     }
     sa[threadIdx.x] = acc;
     sc[threadIdx.x] = cnt;
     __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            sa[threadIdx.x] += sa[threadIdx.x + s];
-            sc[threadIdx.x] += sc[threadIdx.x + s];
+    for (int h = kLceRows / 2; h > 0; h >>= 1) {
+        if (threadIdx.x < h) {
+            sa[threadIdx.x] += sa[threadIdx.x + h];
+            sc[threadIdx.x] += sc[threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        bsum[2 * blockIdx.x] = sa[0];
+        bsum[2 * blockIdx.x + 1] = sc[0];
+    }
+}
+__global__ __launch_bounds__(1024) void lce_finish_kernel(const float* __restrict__ bsum, int64_t nblocks,
+                                                          float* __restrict__ out) {
+    __shared__ float sa[1024], sc[1024];
+    float acc = 0.f, cnt = 0.f;
+    for (int64_t q = threadIdx.x; q < nblocks; q += blockDim.x) {
+        acc += bsum[2 * q];
+        cnt += bsum[2 * q + 1];
+    }
+    sa[threadIdx.x] = acc;
+    sc[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+        if (threadIdx.x < h) {
+            sa[threadIdx.x] += sa[threadIdx.x + h];
+            sc[threadIdx.x] += sc[threadIdx.x + h];
         }
         __syncthreads();
     }
@@ -587,7 +615,8 @@ int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 ASME_API int64_t asme_linear_xent_fwd_workspace(int64_t n, int64_t V, int64_t dim) {
     (void)dim;
     const Plan p = make_plan<M_STATS>(n, V, device_cus());
-    return align256(planes_bytes(n)) + align256(planes_bytes(V)) + align256(p.nchunks * n * 2 * 4) + align256(n * 4);
+    return align256(planes_bytes(n)) + align256(planes_bytes(V)) + align256(p.nchunks * n * 2 * 4) + align256(n * 4) +
+           align256(((n + kLceRows - 1) / kLceRows) * 2 * 4 + 8);
 }
 
 // lse[q] (n) and out = {mean loss over the valid rows, their count}; H (n x dim), W (V x dim), dim <= 128
@@ -630,8 +659,12 @@ ASME_API int asme_linear_xent_fwd(const float* H, int64_t ld_h, int64_t n, int64
         rc = launch_kb<M_STATS>(a, p.sblocks, s);
         if (rc != 0) return rc;
     }
-    hipLaunchKernelGGL(lce_finish_kernel, dim3(1), dim3(1024), 0, s, part, n, p.nchunks, targets, ignore_index, V,
-                       tlogit, lse, out);
+    float* bsum = tlogit + align256(n * 4) / 4;
+    const int64_t nb = (n + kLceRows - 1) / kLceRows;
+    if (nb > 0)
+        hipLaunchKernelGGL(lce_rows_kernel, dim3((unsigned)nb), dim3(kLceRows), 0, s, part, n, p.nchunks, targets,
+                           ignore_index, V, tlogit, lse, bsum);
+    hipLaunchKernelGGL(lce_finish_kernel, dim3(1), dim3(1024), 0, s, bsum, nb, out);
     ASME_LAUNCH_CHECK("asme_linear_xent_fwd");
 }
 

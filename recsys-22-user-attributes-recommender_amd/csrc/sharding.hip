@@ -613,7 +613,25 @@ __global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restric
     const int64_t cl = (seg_off[s + 1] - 1) / kChunk;
     for (int c0 = 4 * lane; c0 < dim; c0 += 128) {
         float4 acc = *reinterpret_cast<const float4*>(tail + cf * dim + c0);
-        for (int64_t q = cf + 1; q <= cl; ++q) add4(acc, *reinterpret_cast<const float4*>(head + q * dim + c0));
+        if (cl - cf <= 8) {
+            for (int64_t q = cf + 1; q <= cl; ++q) add4(acc, *reinterpret_cast<const float4*>(head + q * dim + c0));
+        } else {
+            // a hot slot (PAD, MASK: tens of thousands of occurrences, > 1,000 chunk partials): eight interleaved
+            // partial sums (loads in flight), combined in a fixed tree -- still one fixed order (deterministic)
+            float4 pr[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pr[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            int64_t q = cf + 1;
+            for (; q + 7 <= cl; q += 8)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) add4(pr[u], *reinterpret_cast<const float4*>(head + (q + u) * dim + c0));
+            for (; q <= cl; ++q) add4(pr[0], *reinterpret_cast<const float4*>(head + q * dim + c0));
+#pragma unroll
+            for (int w = 1; w < 8; w *= 2)
+#pragma unroll
+                for (int u = 0; u < 8; u += 2 * w) add4(pr[u], pr[u + w]);
+            add4(acc, pr[0]);
+        }
         if constexpr (APPLY)
             apply_grad4(A, s, dim, c0, scale4(acc, out_scale));
         else

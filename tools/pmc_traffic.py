@@ -38,6 +38,7 @@ MAP = [
     # the fused logits + CE head (csrc/logits.hip): the engine's mode names the call; the operand splits that open
     # a call are attributed to the call of the engine launch that follows them (see per_call)
     (r"logits_engine_kernel<0", "asme_linear_xent_fwd", True),
+    (r"lce_rows_kernel", "asme_linear_xent_fwd", False),
     (r"lce_finish_kernel", "asme_linear_xent_fwd", False),
     (r"logits_engine_kernel<1", "asme_linear_xent_bwd", True),
     (r"logits_engine_kernel<2", "asme_linear_xent_bwd", False),

@@ -14,7 +14,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-
     python bench.py --workload $WL --items $ITEMS --steps 5 --warmup 2 --cpu-baseline 0 > "$OUT/kt.log" 2>&1 || exit $?
 echo "kernel trace done"
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "attn|weight_grad|sum_slabs|ws_gemm|residual|logits_engine|split_planes|lce_finish|sum_parts" \
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "attn|weight_grad|sum_slabs|ws_gemm|residual|logits_engine|split_planes|lce_rows|lce_finish|sum_parts" \
       -d "$OUT/pmc_$C" -o run --output-format csv -- \
       python bench.py --workload $WL --items $ITEMS --steps 2 --warmup 1 --cpu-baseline 0 > "$OUT/pmc_$C.log" 2>&1 || exit $?
   echo "pmc $C done"
