@@ -376,24 +376,25 @@ __global__ __launch_bounds__(256) void csr_scatter_kernel(const int64_t* __restr
 // array: static indices only), longer ones appended to longs[1..] (longs[0] = their count)
 __global__ void csr_order_kernel(const int32_t* __restrict__ seg_off, int64_t n, int64_t cap,
                                  int32_t* __restrict__ order, int32_t* __restrict__ longs, int32_t* __restrict__ huge,
-                                 int32_t* __restrict__ hbeg, int32_t* __restrict__ hend) {
+                                 int32_t* __restrict__ hbeg, int32_t* __restrict__ hend, int32_t* __restrict__ hidx) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > cap) return;
     const int32_t b = seg_off[k];
     const int len = (k < cap ? seg_off[k + 1] : (int32_t)n) - b;
-    if (len < 2) return;
+    int32_t hi = -1;  // the key's huge-range index (every key written: no fill)
+    if (len > kLongSeg) {  // (hbeg / hend of unused segments stay 0: empty)
+        hi = atomicAdd(huge, 1);
+        hbeg[hi] = b;
+        hend[hi] = b + len;
+    }
+    hidx[k] = hi;
+    if (len < 2 || hi >= 0) return;
     if (len == 2) {
         const int32_t x = order[b], y = order[b + 1];
         if (x > y) {
             order[b] = y;
             order[b + 1] = x;
         }
-        return;
-    }
-    if (len > kLongSeg) {  // (hbeg / hend of unused segments stay 0: empty)
-        const int t = atomicAdd(huge, 1);
-        hbeg[t] = b;
-        hend[t] = b + len;
         return;
     }
     if (len > kShortSeg) {
@@ -437,13 +438,111 @@ __global__ __launch_bounds__(256) void csr_long_kernel(const int32_t* __restrict
     }
 }
 
-// the radix-sorted huge ranges back into place
+// Huge ranges without a sort (the first kHugeFast of them; a hot key's list is long but the keys are few): a
+// stable placement over the occurrence array.  (6) per block of kHugeOcc occurrences, the count of each huge key,
+// (7) per huge key an exclusive scan of those counts over the blocks (+ the range start), (8) each block walks its
+// occurrences in index order -- four rounds of 256, every wave groups its lanes by key with ballots -- and an
+// occurrence of huge key j goes to base[j][block] + (earlier occurrences of j in the block).  The range then lists
+// its occurrences in increasing order, the arrays the segmented radix sort gave (a single block sorting the 37k
+// MASK occurrences of a cloze batch took 0.25 ms).  Huge keys past kHugeFast (a batch with more than 64 keys
+// on > 256 occurrences each) still go to the segmented radix sort.
+constexpr int kHugeFast = 64;
+constexpr int kHugeOcc = 1024;  // occurrences per placement block (256 threads x 4 rounds)
+inline int64_t huge_blocks(int64_t n) { return (n + kHugeOcc - 1) / kHugeOcc; }
+
+__global__ __launch_bounds__(256) void csr_huge_count_kernel(const int64_t* __restrict__ inverse, int64_t n,
+                                                             int64_t cap, const int32_t* __restrict__ hidx,
+                                                             const int32_t* __restrict__ huge,
+                                                             int32_t* __restrict__ cntm, int64_t nblk_h) {
+    const int nh = min(*huge, kHugeFast);
+    if (nh == 0) return;
+    __shared__ int32_t c[kHugeFast];
+    if (threadIdx.x < kHugeFast) c[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * kHugeOcc;
+    for (int r = 0; r < kHugeOcc / 256; ++r) {
+        const int64_t i = b0 + r * 256 + threadIdx.x;
+        const int j = i < n ? hidx[occ_key(inverse, i, cap)] : -1;
+        if (j >= 0 && j < kHugeFast) atomicAdd(&c[j], 1);  // (counts only: order does not matter here)
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nh) cntm[(int64_t)threadIdx.x * nblk_h + blockIdx.x] = c[threadIdx.x];
+}
+
+// one workgroup per huge key: base[j][b] = hbeg[j] + sum of its counts over blocks < b (in place)
+__global__ __launch_bounds__(256) void csr_huge_scan_kernel(const int32_t* __restrict__ huge,
+                                                            const int32_t* __restrict__ hbeg,
+                                                            int32_t* __restrict__ cntm, int64_t nblk_h) {
+    const int j = blockIdx.x;
+    if (j >= min(*huge, kHugeFast)) return;
+    __shared__ int32_t s[256];
+    int32_t* row = cntm + (int64_t)j * nblk_h;
+    int32_t carry = hbeg[j];
+    for (int64_t c0 = 0; c0 < nblk_h; c0 += 256) {
+        const int64_t b = c0 + threadIdx.x;
+        const int32_t v = b < nblk_h ? row[b] : 0;
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (int w = 1; w < 256; w *= 2) {  // inclusive Hillis-Steele scan
+            const int32_t a = threadIdx.x >= (unsigned)w ? s[threadIdx.x - w] : 0;
+            __syncthreads();
+            s[threadIdx.x] += a;
+            __syncthreads();
+        }
+        if (b < nblk_h) row[b] = carry + s[threadIdx.x] - v;
+        carry += s[255];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void csr_huge_place_kernel(const int64_t* __restrict__ inverse, int64_t n,
+                                                             int64_t cap, const int32_t* __restrict__ hidx,
+                                                             const int32_t* __restrict__ huge,
+                                                             const int32_t* __restrict__ cntm, int64_t nblk_h,
+                                                             int32_t* __restrict__ order) {
+    const int nh = min(*huge, kHugeFast);
+    if (nh == 0) return;
+    __shared__ int32_t run[kHugeFast];      // this block's occurrences of key j placed so far (+ its base)
+    __shared__ int32_t wc[4][kHugeFast];    // per wave of the current round: occurrences of key j
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if ((int)threadIdx.x < nh) run[threadIdx.x] = cntm[(int64_t)threadIdx.x * nblk_h + blockIdx.x];
+    const uint64_t below = (1ull << lane) - 1;
+    const int64_t b0 = (int64_t)blockIdx.x * kHugeOcc;
+    for (int r = 0; r < kHugeOcc / 256; ++r) {
+        for (int t = threadIdx.x; t < 4 * kHugeFast; t += 256) (&wc[0][0])[t] = 0;
+        __syncthreads();
+        const int64_t i = b0 + r * 256 + threadIdx.x;
+        int j = i < n ? hidx[occ_key(inverse, i, cap)] : -1;
+        if (j >= kHugeFast) j = -1;
+        int rank = 0;
+        uint64_t todo = __ballot(j >= 0);
+        while (todo) {  // lanes grouped by key, lowest lane's key first
+            const int jj = __shfl(j, __ffsll((unsigned long long)todo) - 1);
+            const uint64_t m = __ballot(j == jj);
+            if (j == jj) rank = __popcll(m & below);
+            if (lane == __ffsll((unsigned long long)m) - 1) wc[wave][jj] = __popcll(m);
+            todo &= ~m;
+        }
+        __syncthreads();
+        if (j >= 0) {
+            int p = run[j] + rank;
+            for (int w = 0; w < wave; ++w) p += wc[w][j];
+            order[p] = (int32_t)i;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < nh) run[threadIdx.x] += wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] +
+                                                        wc[3][threadIdx.x];
+        __syncthreads();
+    }
+}
+
+// the radix-sorted huge ranges (those past the first kHugeFast) back into place
 __global__ __launch_bounds__(256) void csr_huge_copy_kernel(const int32_t* __restrict__ huge,
                                                             const int32_t* __restrict__ hbeg,
                                                             const int32_t* __restrict__ hend,
                                                             const int32_t* __restrict__ sorted,
                                                             int32_t* __restrict__ order) {
-    if ((int)blockIdx.x >= *huge) return;
+    if ((int)blockIdx.x + kHugeFast >= *huge) return;
     const int32_t b = hbeg[blockIdx.x], e = hend[blockIdx.x];
     for (int32_t i = b + (int32_t)threadIdx.x; i < e; i += 256) order[i] = sorted[i];
 }
@@ -646,18 +745,20 @@ size_t csr_up(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t csr_temp_bytes(int64_t n) {
     size_t scan = 0, seg = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (int32_t*)nullptr, (int32_t*)nullptr, (int)(n + 1));
-    (void)hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, seg, (const int32_t*)nullptr, (int32_t*)nullptr, (int)n,
-                                                     (int)max_huge(n), (const int32_t*)nullptr,
-                                                     (const int32_t*)nullptr, 0, 32);
+    if (max_huge(n) > kHugeFast)
+        (void)hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, seg, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                         (int)n, (int)(max_huge(n) - kHugeFast),
+                                                         (const int32_t*)nullptr, (const int32_t*)nullptr, 0, 32);
     return scan > seg ? scan : seg;
 }
 }  // namespace
 
 ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
     // per-key counts (n + 1), huge-range count + bounds (1 + 2 max_huge), long-range list (n + 2), rank / sort
-    // scratch (n), scan / segmented-sort temp
+    // scratch (n), key -> huge index (n + 1), huge-key counts per placement block, scan / segmented-sort temp
     return (int64_t)(csr_up((size_t)(n + 1) * 4) + csr_up((size_t)(1 + 2 * max_huge(n)) * 4) +
-                     csr_up((size_t)(n + 2) * 4) + csr_up((size_t)n * 4) + csr_up(csr_temp_bytes(n)));
+                     csr_up((size_t)(n + 2) * 4) + csr_up((size_t)n * 4) + csr_up((size_t)(n + 1) * 4) +
+                     csr_up((size_t)kHugeFast * huge_blocks(n) * 4) + csr_up(csr_temp_bytes(n)));
 }
 
 // inverse (n int64 slots < cap <= n) -> order (n int32 occurrence indices grouped by slot, increasing within a
@@ -678,7 +779,10 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     int32_t* hend = hbeg + nh;
     int32_t* longs = (int32_t*)((char*)huge + csr_up((size_t)(1 + 2 * nh) * 4));
     int32_t* tmp = (int32_t*)((char*)longs + csr_up((size_t)(n + 2) * 4));
-    void* temp = (char*)tmp + csr_up((size_t)n * 4);
+    int32_t* hidx = (int32_t*)((char*)tmp + csr_up((size_t)n * 4));
+    int32_t* cntm = (int32_t*)((char*)hidx + csr_up((size_t)(n + 1) * 4));
+    const int64_t nblk_h = huge_blocks(n);
+    void* temp = (char*)cntm + csr_up((size_t)kHugeFast * nblk_h * 4);
     size_t temp_bytes = (size_t)workspace_bytes - ((char*)temp - ws);
     // counts of keys 0..cap, the huge-range count and bounds, the long-range counter: zeroed together (contiguous)
     if (hipMemsetAsync(cnt, 0, (char*)longs - ws + 4, s) != hipSuccess)
@@ -689,15 +793,24 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     hipLaunchKernelGGL(csr_scatter_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, seg_off, cnt, order,
                        sorted_slot);
     hipLaunchKernelGGL(csr_order_kernel, dim3(nblk(cap + 1)), dim3(256), 0, s, seg_off, n, cap, order, longs, huge,
-                       hbeg, hend);
+                       hbeg, hend, hidx);
     hipLaunchKernelGGL(csr_long_kernel, dim3(64), dim3(256), 0, s, seg_off, n, cap, longs, order, tmp);
-    if (n > kLongSeg) {  // a huge range is possible: sort them (occurrence indices < n: only the bits n needs)
-        int bits = 1;
-        while (bits < 31 && ((int64_t)1 << bits) < n) ++bits;
-        if (hipcub::DeviceSegmentedRadixSort::SortKeys(temp, temp_bytes, order, tmp, (int)n, (int)nh, hbeg, hend, 0,
-                                                       bits, s) != hipSuccess)
-            return hip_status(hipErrorUnknown, "asme_occurrence_csr: huge-range sort");
-        hipLaunchKernelGGL(csr_huge_copy_kernel, dim3((unsigned)nh), dim3(256), 0, s, huge, hbeg, hend, tmp, order);
+    if (n > kLongSeg) {  // a huge range is possible: stable placement of the first kHugeFast, sort the rest
+        hipLaunchKernelGGL(csr_huge_count_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
+                           cntm, nblk_h);
+        hipLaunchKernelGGL(csr_huge_scan_kernel, dim3(kHugeFast), dim3(256), 0, s, huge, hbeg, cntm, nblk_h);
+        hipLaunchKernelGGL(csr_huge_place_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
+                           cntm, nblk_h, order);
+        if (nh > kHugeFast) {  // occurrence indices < n: only the bits n needs
+            int bits = 1;
+            while (bits < 31 && ((int64_t)1 << bits) < n) ++bits;
+            if (hipcub::DeviceSegmentedRadixSort::SortKeys(temp, temp_bytes, order, tmp, (int)n, (int)(nh - kHugeFast),
+                                                           hbeg + kHugeFast, hend + kHugeFast, 0, bits,
+                                                           s) != hipSuccess)
+                return hip_status(hipErrorUnknown, "asme_occurrence_csr: huge-range sort");
+            hipLaunchKernelGGL(csr_huge_copy_kernel, dim3((unsigned)(nh - kHugeFast)), dim3(256), 0, s, huge,
+                               hbeg + kHugeFast, hend + kHugeFast, tmp, order);
+        }
     }
     ASME_LAUNCH_CHECK("asme_occurrence_csr");
 }

@@ -1,5 +1,9 @@
-set -o pipefail
+set -u
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1; echo "tests rc=$?" >> gpurun_out/t.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-timeout -k 10 300 python bench.py > gpurun_out/b1.log 2>&1 || exit 1
+export TMPDIR=/tmp
+for wi in bert4rec:27000 kebert4rec:13000; do w=${wi%%:*}; it=${wi##*:}
+timeout -k 10 300 python bench.py --workload $w --items $it --steps 20 --warmup 3 --cpu-baseline 0 > gpurun_out/b_$w.json 2> gpurun_out/b_$w.err || exit $?
+python -c "import json;d=json.loads(open('gpurun_out/b_$w.json').read().strip().splitlines()[-1]);print('$w',d['value'],d['ms_per_step'])"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_b4r -o run --output-format csv -- python bench.py --workload bert4rec --items 27000 --steps 5 --warmup 2 --cpu-baseline 0 > gpurun_out/kt_b4r.log 2>&1 || exit $?
+echo kt done
