@@ -199,9 +199,25 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                 const float4 o = pre[ct];
                 bstore(make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w), yr, off, nt_out);
             } else if constexpr (EPI == WS_GELU_DROP) {
-                // (a lane holds one 4-element chunk here: its own half of the chunk pair's Philox block)
+                // A lane holds one 4-element chunk per feature tile; its partner lane ^ 4 holds the other chunk of
+                // the same Philox block (chunk bit 2 == lane bit 2: N / 4 and n0 / 4 are multiples of 8).  So at
+                // the even tile the bit-2-clear lane generates its tile-ct block, the bit-2-set lane the tile-ct+1
+                // block, and one exchange gives both lanes both tiles' decisions: one Philox block per lane per
+                // tile pair instead of one per tile (the second tile's half kept in `pend`).
                 float u[4] = {1.f, 1.f, 1.f, 1.f};
-                if (ep.p > 0.f) gelu_keep_factors(gelu_keep_bits4(ep.seed, (uint64_t)(off >> 4), thr), keep_k, u);
+                if (ep.p > 0.f) {
+                    if ((ct & 1) == 0) {
+                        const int sel = (threadIdx.x >> 2) & 1;
+                        const int idx = 64 * (ct + sel) + (threadIdx.x & 63), row = idx / NB4, c4 = idx % NB4;
+                        const uint64_t chunk = (uint64_t)(((srow0 + row) * N + n0 + 4 * c4) >> 2);
+                        const uint32_t b8 = gelu_keep_bits8(ep.seed, chunk, thr);
+                        const uint32_t x = (uint32_t)__shfl_xor((int)b8, 4, 64);
+                        gelu_keep_factors(sel ? (x >> 4) : (b8 & 0xFu), keep_k, u);
+                        pend = sel ? (b8 >> 4) : (x & 0xFu);
+                    } else {
+                        gelu_keep_factors(pend, keep_k, u);
+                    }
+                }
                 float gl[4], gd[4];
                 gelu_erf_and_grad(v.x, gl[0], gd[0]);
                 gelu_erf_and_grad(v.y, gl[1], gd[1]);
