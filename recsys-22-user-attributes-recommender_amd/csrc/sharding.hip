@@ -329,6 +329,7 @@ constexpr int kShortSeg = 16;
 #endif
 constexpr int kLongSeg = ASME_LONG_SEG;  // (a 2,048-long range took ~100 us in one workgroup)
 inline int64_t max_huge(int64_t n) { return n / (kLongSeg + 1) + 1; }
+constexpr int kHugeFast = 256;  // huge ranges placed by the stable ballot scatter (below); the rest are long ranges
 
 __device__ __forceinline__ int32_t occ_key(const int64_t* __restrict__ inverse, int64_t i, int64_t cap) {
     const int64_t k = inverse[i];
@@ -382,13 +383,18 @@ __global__ void csr_order_kernel(const int32_t* __restrict__ seg_off, int64_t n,
     const int32_t b = seg_off[k];
     const int len = (k < cap ? seg_off[k + 1] : (int32_t)n) - b;
     int32_t hi = -1;  // the key's huge-range index (every key written: no fill)
-    if (len > kLongSeg) {  // (hbeg / hend of unused segments stay 0: empty)
+    if (len > kLongSeg) {
         hi = atomicAdd(huge, 1);
-        hbeg[hi] = b;
-        hend[hi] = b + len;
+        if (hi < kHugeFast) {
+            hbeg[hi] = b;
+            hend[hi] = b + len;
+        } else {  // past the stable placement's capacity: ranked by a workgroup like the long ranges
+            longs[1 + atomicAdd(longs, 1)] = (int32_t)k;
+            hi = -1;
+        }
     }
     hidx[k] = hi;
-    if (len < 2 || hi >= 0) return;
+    if (len < 2 || hi >= 0 || len > kLongSeg) return;
     if (len == 2) {
         const int32_t x = order[b], y = order[b + 1];
         if (x > y) {
@@ -444,9 +450,8 @@ __global__ __launch_bounds__(256) void csr_long_kernel(const int32_t* __restrict
 // occurrences in index order -- four rounds of 256, every wave groups its lanes by key with ballots -- and an
 // occurrence of huge key j goes to base[j][block] + (earlier occurrences of j in the block).  The range then lists
 // its occurrences in increasing order, the arrays the segmented radix sort gave (a single block sorting the 37k
-// MASK occurrences of a cloze batch took 0.25 ms).  Huge keys past kHugeFast (a batch with more than 64 keys
-// on > 256 occurrences each) still go to the segmented radix sort.
-constexpr int kHugeFast = 64;
+// MASK occurrences of a cloze batch took 0.25 ms).  Huge keys past kHugeFast (a batch with more than 256 keys
+// on > 256 occurrences each) are ranked by the long-range workgroups instead (correct at any length, quadratic).
 constexpr int kHugeOcc = 1024;  // occurrences per placement block (256 threads x 4 rounds)
 inline int64_t huge_blocks(int64_t n) { return (n + kHugeOcc - 1) / kHugeOcc; }
 
@@ -534,17 +539,6 @@ __global__ __launch_bounds__(256) void csr_huge_place_kernel(const int64_t* __re
                                                         wc[3][threadIdx.x];
         __syncthreads();
     }
-}
-
-// the radix-sorted huge ranges (those past the first kHugeFast) back into place
-__global__ __launch_bounds__(256) void csr_huge_copy_kernel(const int32_t* __restrict__ huge,
-                                                            const int32_t* __restrict__ hbeg,
-                                                            const int32_t* __restrict__ hend,
-                                                            const int32_t* __restrict__ sorted,
-                                                            int32_t* __restrict__ order) {
-    if ((int)blockIdx.x + kHugeFast >= *huge) return;
-    const int32_t b = hbeg[blockIdx.x], e = hend[blockIdx.x];
-    for (int32_t i = b + (int32_t)threadIdx.x; i < e; i += 256) order[i] = sorted[i];
 }
 
 constexpr int kMaxContrib = 4;
@@ -743,19 +737,15 @@ __global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restric
 namespace {
 size_t csr_up(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t csr_temp_bytes(int64_t n) {
-    size_t scan = 0, seg = 0;
+    size_t scan = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (int32_t*)nullptr, (int32_t*)nullptr, (int)(n + 1));
-    if (max_huge(n) > kHugeFast)
-        (void)hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, seg, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                                         (int)n, (int)(max_huge(n) - kHugeFast),
-                                                         (const int32_t*)nullptr, (const int32_t*)nullptr, 0, 32);
-    return scan > seg ? scan : seg;
+    return scan;
 }
 }  // namespace
 
 ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
     // per-key counts (n + 1), huge-range count + bounds (1 + 2 max_huge), long-range list (n + 2), rank / sort
-    // scratch (n), key -> huge index (n + 1), huge-key counts per placement block, scan / segmented-sort temp
+    // scratch (n), key -> huge index (n + 1), huge-key counts per placement block, scan temp
     return (int64_t)(csr_up((size_t)(n + 1) * 4) + csr_up((size_t)(1 + 2 * max_huge(n)) * 4) +
                      csr_up((size_t)(n + 2) * 4) + csr_up((size_t)n * 4) + csr_up((size_t)(n + 1) * 4) +
                      csr_up((size_t)kHugeFast * huge_blocks(n) * 4) + csr_up(csr_temp_bytes(n)));
@@ -795,22 +785,12 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     hipLaunchKernelGGL(csr_order_kernel, dim3(nblk(cap + 1)), dim3(256), 0, s, seg_off, n, cap, order, longs, huge,
                        hbeg, hend, hidx);
     hipLaunchKernelGGL(csr_long_kernel, dim3(64), dim3(256), 0, s, seg_off, n, cap, longs, order, tmp);
-    if (n > kLongSeg) {  // a huge range is possible: stable placement of the first kHugeFast, sort the rest
+    if (n > kLongSeg) {  // a huge range is possible: stable placement
         hipLaunchKernelGGL(csr_huge_count_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
                            cntm, nblk_h);
         hipLaunchKernelGGL(csr_huge_scan_kernel, dim3(kHugeFast), dim3(256), 0, s, huge, hbeg, cntm, nblk_h);
         hipLaunchKernelGGL(csr_huge_place_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
                            cntm, nblk_h, order);
-        if (nh > kHugeFast) {  // occurrence indices < n: only the bits n needs
-            int bits = 1;
-            while (bits < 31 && ((int64_t)1 << bits) < n) ++bits;
-            if (hipcub::DeviceSegmentedRadixSort::SortKeys(temp, temp_bytes, order, tmp, (int)n, (int)(nh - kHugeFast),
-                                                           hbeg + kHugeFast, hend + kHugeFast, 0, bits,
-                                                           s) != hipSuccess)
-                return hip_status(hipErrorUnknown, "asme_occurrence_csr: huge-range sort");
-            hipLaunchKernelGGL(csr_huge_copy_kernel, dim3((unsigned)(nh - kHugeFast)), dim3(256), 0, s, huge,
-                               hbeg + kHugeFast, hend + kHugeFast, tmp, order);
-        }
     }
     ASME_LAUNCH_CHECK("asme_occurrence_csr");
 }

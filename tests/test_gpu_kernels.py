@@ -368,13 +368,13 @@ def test_deterministic_table_grad(asme, dev, D):
 
 
 @pytest.mark.parametrize("n,cap", [(1, 1), (7, 7), (5000, 5000), (70000, 70000), (3000, 2000), (5000, 1),
-                                   (204800, 60000), (100000, 150), (100000, 300), (1500, 1)])
+                                   (204800, 60000), (100000, 150), (100000, 300), (1500, 1), (204800, 1200)])
 def test_occurrence_csr_equals_stable_sort(asme, dev, n, cap):
     """asme_occurrence_csr (counting sort + per-range ordering) == a stable sort of the occurrences by slot:
     order, sorted_slot (cap for slot-less occurrences, sorted last) and seg_off, exactly.  Slots with one, two,
     a few, hundreds and tens of thousands of occurrences (ranges over 256 -- the PAD / MASK / small-vocabulary
-    case: the stable ballot placement for the first 64 of them, the segmented radix sort past that; cap = 150 / 300
-    give ~50 / ~100 such ranges) and slot-less ones."""
+    case: the stable ballot placement for the first 256 of them, the long-range workgroup ranking past that;
+    cap = 150 / 300 / 1200 give ~50 / ~100 / ~400 such ranges) and slot-less ones."""
     L = asme._lib
     g = torch.Generator().manual_seed(n + cap)
     u = max(1, cap // 3)
