@@ -65,21 +65,19 @@ __global__ void flag_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t 
     flags[i] = (id >= 0 && id < V && map[id] == (int32_t)i) ? 1 : 0;
 }
 
+// compaction, and the map rewritten to slots on the way (map[unique[s]] = s): each distinct id is written by its
+// one representative occurrence, and nothing reads the map between the flag pass and the inverse pass
 __global__ void compact_kernel(const int64_t* __restrict__ ids, int64_t n, const int32_t* __restrict__ flags,
                                const int32_t* __restrict__ scan, int64_t* __restrict__ unique,
-                               int32_t* __restrict__ count) {
+                               int32_t* __restrict__ count, int32_t* __restrict__ map) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (flags[i]) unique[scan[i]] = ids[i];
+    if (flags[i]) {
+        const int64_t id = ids[i];
+        unique[scan[i]] = id;
+        map[id] = scan[i];
+    }
     if (i == n - 1) *count = scan[i] + flags[i];
-}
-
-// after compaction: map[unique[s]] = s
-__global__ void slot_kernel(const int64_t* __restrict__ unique, const int32_t* __restrict__ count,
-                            int32_t* __restrict__ map, int64_t cap) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= cap || s >= *count) return;
-    map[unique[s]] = (int32_t)s;
 }
 
 __global__ void inverse_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V, const int32_t* __restrict__ map,
@@ -249,8 +247,7 @@ ASME_API int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_
     hipLaunchKernelGGL(flag_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, vocab, map, flags);
     if (hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, flags, scan, (int)n, s) != hipSuccess)
         return hip_status(hipErrorUnknown, "asme_dedup_ids: scan");
-    hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, flags, scan, unique, count);
-    hipLaunchKernelGGL(slot_kernel, dim3(nblk(n)), dim3(256), 0, s, unique, count, map, n);
+    hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, flags, scan, unique, count, map);
     if (inverse) hipLaunchKernelGGL(inverse_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, vocab, map, inverse);
     ASME_LAUNCH_CHECK("asme_dedup_ids");
 }
