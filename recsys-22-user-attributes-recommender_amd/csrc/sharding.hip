@@ -455,10 +455,13 @@ inline int64_t huge_blocks(int64_t n) { return (n + kHugeOcc - 1) / kHugeOcc; }
 __global__ __launch_bounds__(256) void csr_huge_count_kernel(const int64_t* __restrict__ inverse, int64_t n,
                                                              int64_t cap, const int32_t* __restrict__ hidx,
                                                              const int32_t* __restrict__ huge,
-                                                             int32_t* __restrict__ cntm, int64_t nblk_h) {
+                                                             const int32_t* __restrict__ hbeg,
+                                                             int32_t* __restrict__ cntm, int64_t nblk_h,
+                                                             int32_t* __restrict__ ticket) {
     const int nh = min(*huge, kHugeFast);
     if (nh == 0) return;
     __shared__ int32_t c[kHugeFast];
+    __shared__ int last;
     if (threadIdx.x < kHugeFast) c[threadIdx.x] = 0;
     __syncthreads();
     const int64_t b0 = (int64_t)blockIdx.x * kHugeOcc;
@@ -469,31 +472,30 @@ __global__ __launch_bounds__(256) void csr_huge_count_kernel(const int64_t* __re
     }
     __syncthreads();
     if ((int)threadIdx.x < nh) cntm[(int64_t)threadIdx.x * nblk_h + blockIdx.x] = c[threadIdx.x];
-}
-
-// one workgroup per huge key: base[j][b] = hbeg[j] + sum of its counts over blocks < b (in place)
-__global__ __launch_bounds__(256) void csr_huge_scan_kernel(const int32_t* __restrict__ huge,
-                                                            const int32_t* __restrict__ hbeg,
-                                                            int32_t* __restrict__ cntm, int64_t nblk_h) {
-    const int j = blockIdx.x;
-    if (j >= min(*huge, kHugeFast)) return;
-    __shared__ int32_t s[256];
-    int32_t* row = cntm + (int64_t)j * nblk_h;
-    int32_t carry = hbeg[j];
-    for (int64_t c0 = 0; c0 < nblk_h; c0 += 256) {
-        const int64_t b = c0 + threadIdx.x;
-        const int32_t v = b < nblk_h ? row[b] : 0;
-        s[threadIdx.x] = v;
-        __syncthreads();
-        for (int w = 1; w < 256; w *= 2) {  // inclusive Hillis-Steele scan
-            const int32_t a = threadIdx.x >= (unsigned)w ? s[threadIdx.x - w] : 0;
-            __syncthreads();
-            s[threadIdx.x] += a;
-            __syncthreads();
+    // (7) by the last block to finish (a ticket, no waiting): per huge key, base[j][b] = hbeg[j] + its counts over
+    // blocks < b, in place -- one wave per key, 64 blocks per wave-scan step
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int j = wave; j < nh; j += 4) {
+        int32_t* row = cntm + (int64_t)j * nblk_h;
+        int32_t carry = hbeg[j];
+        for (int64_t c0 = 0; c0 < nblk_h; c0 += 64) {
+            const int64_t b = c0 + lane;
+            const int32_t v = b < nblk_h ? __hip_atomic_load(row + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            int32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (b < nblk_h) row[b] = carry + x - v;
+            carry += __shfl(x, 63, 64);
         }
-        if (b < nblk_h) row[b] = carry + s[threadIdx.x] - v;
-        carry += s[255];
-        __syncthreads();
     }
 }
 
@@ -741,9 +743,9 @@ size_t csr_temp_bytes(int64_t n) {
 }  // namespace
 
 ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
-    // per-key counts (n + 1), huge-range count + bounds (1 + 2 max_huge), long-range list (n + 2), rank / sort
+    // per-key counts (n + 1), huge-range count + bounds + scan ticket (2 + 2 max_huge), long-range list (n + 2), rank / sort
     // scratch (n), key -> huge index (n + 1), huge-key counts per placement block, scan temp
-    return (int64_t)(csr_up((size_t)(n + 1) * 4) + csr_up((size_t)(1 + 2 * max_huge(n)) * 4) +
+    return (int64_t)(csr_up((size_t)(n + 1) * 4) + csr_up((size_t)(2 + 2 * max_huge(n)) * 4) +
                      csr_up((size_t)(n + 2) * 4) + csr_up((size_t)n * 4) + csr_up((size_t)(n + 1) * 4) +
                      csr_up((size_t)kHugeFast * huge_blocks(n) * 4) + csr_up(csr_temp_bytes(n)));
 }
@@ -764,7 +766,8 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     int32_t* huge = (int32_t*)(ws + csr_up((size_t)(n + 1) * 4));
     int32_t* hbeg = huge + 1;
     int32_t* hend = hbeg + nh;
-    int32_t* longs = (int32_t*)((char*)huge + csr_up((size_t)(1 + 2 * nh) * 4));
+    int32_t* ticket = hend + nh;  // (zeroed with the counts)
+    int32_t* longs = (int32_t*)((char*)huge + csr_up((size_t)(2 + 2 * nh) * 4));
     int32_t* tmp = (int32_t*)((char*)longs + csr_up((size_t)(n + 2) * 4));
     int32_t* hidx = (int32_t*)((char*)tmp + csr_up((size_t)n * 4));
     int32_t* cntm = (int32_t*)((char*)hidx + csr_up((size_t)(n + 1) * 4));
@@ -784,8 +787,7 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     hipLaunchKernelGGL(csr_long_kernel, dim3(64), dim3(256), 0, s, seg_off, n, cap, longs, order, tmp);
     if (n > kLongSeg) {  // a huge range is possible: stable placement
         hipLaunchKernelGGL(csr_huge_count_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
-                           cntm, nblk_h);
-        hipLaunchKernelGGL(csr_huge_scan_kernel, dim3(kHugeFast), dim3(256), 0, s, huge, hbeg, cntm, nblk_h);
+                           hbeg, cntm, nblk_h, ticket);
         hipLaunchKernelGGL(csr_huge_place_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
                            cntm, nblk_h, order);
     }
