@@ -115,6 +115,10 @@ def parse():
                     help="gpu (default): every step samples a fresh batch from sessions in HBM with the GPU pos/neg "
                          "sampler (asme_posneg_sample) inside the timed step; resident: two pre-built device batches "
                          "alternating (rows touched one or two steps earlier: less lazy catch-up per step)")
+    ap.add_argument("--legs", default="bert4rec:27000,kebert4rec:13000",
+                    help="with the sasrec-neg headline: the other BASELINE workloads run in the same invocation and "
+                         "reported under \"workloads\" of the one JSON line (name:items, comma-separated; "
+                         "C3 BERT4Rec |I| = 27,000, C5 KeBERT4Rec |I| = 13,000; 'none' to skip)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -128,6 +132,18 @@ def parse():
                     help="sequences per CPU-baseline step of the BERT4Rec / KeBERT4Rec workloads")
     ap.add_argument("--sampler-sessions", type=int, default=16, help="sessions for the CPU sampler rate")
     return ap.parse_args()
+
+
+def parse_legs(spec: str):
+    if not spec or spec == "none":
+        return []
+    out = []
+    for part in spec.split(","):
+        name, _, items = part.partition(":")
+        if name not in ("bert4rec", "kebert4rec"):
+            raise SystemExit(f"--legs: unknown workload {name!r}")
+        out.append((name, int(items) if items else {"bert4rec": 27000, "kebert4rec": 13000}[name]))
+    return out
 
 
 def synthetic_batch(B, L, V, seed, dev, kind="uniform"):
@@ -220,7 +236,7 @@ def cpu_baseline(args, V):
                       f"(this job's CPU share; the machine has {os.cpu_count()}), torch CPU fp32, {cpu_model_name()}"}
 
 
-def cpu_baseline_masked(args, model, V, kebert, n_genre):
+def cpu_baseline_masked(args, model, V, kebert, n_genre, workload):
     """CPU restatement (oracle/asme_oracle.py bert4rec_logits / kebert4rec_logits, reference op order) of the C3 / C5
     step timed on the host cores: the model's own initial parameters (reference state_dict keys) copied to the CPU,
     the reference's full (B, L, |V|) logits + CrossEntropyLoss(ignore_index) (masked_training_module.py:93-111),
@@ -251,7 +267,7 @@ def cpu_baseline_masked(args, model, V, kebert, n_genre):
         loss.backward()
         opt.step()
         times.append(time.perf_counter() - t0)
-        print(f"[cpu_baseline] {args.workload} B={B} step {i + 1}/{args.cpu_warmup + args.cpu_steps}: "
+        print(f"[cpu_baseline] {workload} B={B} step {i + 1}/{args.cpu_warmup + args.cpu_steps}: "
               f"{times[-1]:.2f} s", file=sys.stderr, flush=True)
     per_step = sum(times[args.cpu_warmup:]) / args.cpu_steps
     name = "KeBERT4Rec" if kebert else "BERT4Rec"
@@ -262,13 +278,15 @@ def cpu_baseline_masked(args, model, V, kebert, n_genre):
                       f"{per_step:.2f} s/step on {threads} threads, torch CPU fp32, dropout off, {cpu_model_name()}"}
 
 
-def bench_bert4rec(args, asme, dev, world, rank):
+def bench_bert4rec(args, asme, dev, world, rank, workload, items):
     """BASELINE config C3: BERT4Rec (tied head), cloze masking p = 0.2 / last-item-only 0.1, B per GPU, full
-    catalogue CE over |V| = items + 3.  Every step builds its batch on the GPU (collate + asme_cloze_mask) from
-    sessions in HBM inside the timed region; data parallel over ranks (flat all_reduce of the gradients)."""
-    V = args.items + 3
+    catalogue CE over |V| = items + 3 (C5: KeBERT4Rec with a category side attribute).  Every step builds its
+    batch on the GPU (collate + asme_cloze_mask) from sessions in HBM inside the timed region; data parallel over
+    ranks (dataparallel.GradientAllReduce: bucketed RCCL all-reduce overlapped with the backward).  Returns the
+    leg's result (rank 0 prints it, alone or inside the headline line's "workloads")."""
+    V = items + 3
     B, L, d = args.batch, args.seq_len, args.dim
-    kebert = args.workload == "kebert4rec"
+    kebert = workload == "kebert4rec"
     n_genre = 64  # synthetic side attribute: category of the item, content_embedding (SURVEY §8 C5)
     with torch.device(dev):
         if kebert:
@@ -282,7 +300,7 @@ def bench_bert4rec(args, asme, dev, world, rank):
             model = asme.BERT4RecModel(transformer_hidden_size=d, num_transformer_heads=args.heads,
                                        num_transformer_layers=args.layers, item_vocab_size=V, max_seq_length=L,
                                        transformer_dropout=args.dropout)
-    tok = asme.tokenization.Tokenizer(args.items)
+    tok = asme.tokenization.Tokenizer(items)
     module = asme.MaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None)
     module.train()
     opt, sched = asme.modules.split_optimizers(module.configure_optimizers())
@@ -342,10 +360,10 @@ def bench_bert4rec(args, asme, dev, world, rank):
             "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4),
             "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
             "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0)}
-    lb = committed_profile("logits_mfma_busy.json", {"workload": args.workload, "rows": 36966, "items": V, "dim": d})
+    lb = committed_profile("logits_mfma_busy.json", {"workload": workload, "rows": 36966, "items": V, "dim": d})
     # HBM traffic per launch from the committed rocprofv3 PMC pass over this workload (tools/pmc_traffic.py)
-    tp = committed_profile(f"pmc_traffic_{args.workload}.json", {"batch": B, "seq_len": L, "items": args.items,
-                                                                   "dim": d, "layers": args.layers})
+    tp = committed_profile(f"pmc_traffic_{workload}.json", {"batch": B, "seq_len": L, "items": items,
+                                                              "dim": d, "layers": args.layers})
     rooflines = roofline_entries(timer.summary(), work, tp.get("bytes_per_launch", {}),
                                  lb.get("mfma_busy") if B == 1024 and L == 200 else None)
     name = "KeBERT4Rec" if kebert else "BERT4Rec"
@@ -356,16 +374,15 @@ def bench_bert4rec(args, asme, dev, world, rank):
               "data": "synthetic sessions, GPU cloze masking inside the step, random-init weights",
               "config": {"workload": ("kebert4rec cloze train step (BASELINE C5)" if kebert
                                       else "bert4rec cloze train step (BASELINE C3)"), "model": name,
-                         "global_batch": B * world, "batch_per_gpu": B, "seq_len": L, "items": args.items,
+                         "global_batch": B * world, "batch_per_gpu": B, "seq_len": L, "items": items,
                          "dim": d, "heads": H, "layers": args.layers, "dropout": args.dropout,
                          "fused_xent": asme.modules.FUSED_XENT, "parallelism": f"dp{world}"},
               "roofline": rooflines[0] if rooflines else None, "rooflines": rooflines, "cpu_baseline": None}
     if rank == 0 and world == 1 and args.cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_masked(args, model, V, kebert, n_genre)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist.is_initialized():
-        dist.destroy_process_group()
+        result["cpu_baseline"] = cpu_baseline_masked(args, model, V, kebert, n_genre, workload)
+    if reducer is not None:
+        reducer.remove()
+    return result
 
 
 def main():
@@ -392,7 +409,12 @@ def main():
 
     torch.manual_seed(rank)
     if args.workload in ("bert4rec", "kebert4rec"):
-        return bench_bert4rec(args, asme, dev, world, rank)
+        result = bench_bert4rec(args, asme, dev, world, rank, args.workload, args.items)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
     sharded = world > 1 or args.sharded
     # N > 1: the item table is row-sharded over the ranks (RCCL all-to-all of ids / rows / row grads,
     # one all_reduce of the replicated dense gradients); N = 1: the whole table on the one GPU
@@ -572,9 +594,19 @@ def main():
         "flush_ms": round(flush_ms, 3),
         "cpu_baseline": None,
     }
+    asme.ops.SparseTablePlan.release = _orig_release
+    del model, module, opt, batches
+    torch.cuda.empty_cache()
+    # the other BASELINE workloads, measured in the same run (same contract: warm-up, barrier + synchronize around
+    # exactly --steps steps, max over ranks) and reported inside this one JSON line
+    legs = parse_legs(args.legs)
+    if legs:
+        result["workloads"] = {}
+        for leg, items in legs:
+            torch.manual_seed(rank)
+            result["workloads"][leg] = bench_bert4rec(args, asme, dev, world, rank, leg, items)
+            torch.cuda.empty_cache()
     if rank == 0 and world == 1 and args.cpu_baseline:
-        del model, module, opt, batches
-        torch.cuda.empty_cache()
         result["cpu_baseline"] = cpu_baseline(args, V)
     if rank == 0:
         print(json.dumps(result), flush=True)

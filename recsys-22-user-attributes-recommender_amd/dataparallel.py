@@ -21,6 +21,7 @@ for tests and 1-GPU rehearsals).
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Dict, List, Optional
 
 import torch
@@ -69,6 +70,7 @@ class GradientAllReduce:
                 self._bucket_of[id(p)] = b
         self._hooks = [p.register_post_accumulate_grad_hook(self._ready) for b in self.buckets for p in b.params]
         self._next = 0
+        self._sync = True
         self._reset()
 
     def _reset(self):
@@ -83,8 +85,26 @@ class GradientAllReduce:
         self._hooks = []
 
     # ------------------------------------------------------------------------------------------ backward
+    @contextlib.contextmanager
+    def no_sync(self):
+        """gradient accumulation (the reference trainer's accumulate_grad_batches, trainer_builder.py:25): the
+        backward passes inside only accumulate into .grad; the next backward outside launches the buckets from
+        the accumulated gradients (DDP.no_sync semantics)"""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
     def _ready(self, p: torch.nn.Parameter):
+        if not self._sync:
+            return
         b = self._bucket_of[id(p)]
+        if b.pending <= 0 or b.work is not None:
+            # a second backward before finish(): its gradient would land after the bucket was reduced and
+            # finish() would overwrite the accumulated .grad with the first backward's average
+            raise RuntimeError("GradientAllReduce: a gradient hook fired twice before finish(); run the "
+                               "accumulation micro-batches inside reducer.no_sync()")
         b.pending -= 1
         if b.pending == 0:
             self._launch_ready()

@@ -113,6 +113,11 @@ class _TableGradMixin:
             self._slot_map = torch.full((table.shape[0],), -1, dtype=torch.int32, device=table.device)
         tg = table._asme_table_grad
         if tg.plan is not None and not tg.plan.consumed:
+            if tg.plan.has_gradient():
+                # a backward ran and no optimizer step consumed its rows: gradient accumulation
+                # (accumulate_grad_batches > 1), which the per-step row-sparse plan does not merge
+                raise RuntimeError("table_grad='sparse' takes one backward per optimizer step; use table_grad='dense' "
+                                   "for gradient accumulation")
             tg.plan.release()
         tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map)
 
@@ -236,7 +241,7 @@ def _rows_cross_entropy(model, sequence, rows, targets, pad: int) -> torch.Tenso
     wb = model.head_weight_bias() if hasattr(model, "head_weight_bias") else None
     if wb is not None:
         h = model.encode_rows(sequence, rows)
-        if FUSED_XENT and ops.linear_xent_ok(h, wb[0]):
+        if FUSED_XENT and ops.linear_xent_ok(h, wb[0], wb[1]):
             return ops.linear_cross_entropy(h, wb[0], wb[1], targets, pad)
         return ops.cross_entropy(ops.logits(h, wb[0], wb[1]), targets, pad)
     return ops.cross_entropy(model.forward_rows(sequence, rows), targets, pad)

@@ -329,6 +329,10 @@ class SparseTablePlan:
                                               dtype=torch.float32)
         return self._grad_rows
 
+    def has_gradient(self) -> bool:
+        """a backward registered gradient rows with this plan"""
+        return bool(self._contrib) or self._grad_rows is not None
+
     def n_unique(self) -> int:
         """number of distinct ids (device -> host sync)"""
         return int(self.count.item())
@@ -858,7 +862,11 @@ def gru(x: torch.Tensor, module: torch.nn.GRU) -> torch.Tensor:
     H = module.hidden_size
     hp = -(-H // 16) * 16
     if hp > 128:
-        raise NotImplementedError(f"asme gru: hidden size {H} > 128")
+        # wider than the register-resident W_hh of csrc/narm.hip (the reference configs use 128 and 30): the
+        # library GRU on the same device (MIOpen), as before the kernel existed; a CPU tensor still raises
+        if not x.is_cuda:
+            raise _lib.ASMEKernelError("asme gru: tensors must be on the ROCm device")
+        return module(x)[0]
     h = x
     for k in range(module.num_layers):
         w_ih = getattr(module, f"weight_ih_l{k}")
@@ -1225,11 +1233,13 @@ def cross_entropy(logits, targets, ignore_index: int):
     return _CrossEntropyFn.apply(logits, targets, ignore_index)
 
 
-def linear_xent_ok(hidden: torch.Tensor, weight: torch.Tensor) -> bool:
+def linear_xent_ok(hidden: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> bool:
     """shapes the logits kernels take (asme_linear_xent_*, asme_logits; csrc/logits.hip): hidden width a multiple of
     4 up to 128, weight rows contiguous and 16-B aligned"""
     d = hidden.shape[-1]
+    # (the kernels read the weight / bias as fp32 in place: a bf16 / fp16 head, e.g. under autocast, is not taken)
     return (4 <= d <= 128 and d % 4 == 0 and weight.dim() == 2 and weight.shape[1] == d
+            and weight.dtype == torch.float32 and (bias is None or bias.dtype == torch.float32)
             and weight.stride(1) == 1 and weight.stride(0) % 4 == 0 and weight.data_ptr() % 16 == 0)
 
 
@@ -1266,7 +1276,7 @@ class _LogitsFn(torch.autograd.Function):
 def logits(hidden, weight, bias=None):
     """full-catalogue scores hidden . weight^T (+ bias) on the bf16x6 logits kernel; widths above 128 (NARM's
     2H = 256) on the fp32-MFMA Linear kernel"""
-    if linear_xent_ok(hidden, weight) and hidden.is_cuda:
+    if linear_xent_ok(hidden, weight, bias) and hidden.is_cuda:
         return _LogitsFn.apply(hidden, weight, bias)
     return linear(hidden, weight, bias)
 

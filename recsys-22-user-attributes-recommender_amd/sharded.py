@@ -179,7 +179,8 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         self._req_map: Optional[torch.Tensor] = None
         self._own_map: Optional[torch.Tensor] = None
         self._pending = None
-        self._prefetched = None  # (id-set keys, requester plan, request_begin state) of the next step
+        self._prefetched = None  # (caller's id tensors, normalised id sets, requester plan, request_begin state)
+        self.prefetch_hits = 0   # training steps that consumed a prefetch (tests assert the overlap really ran)
 
     def broadcast_dense_parameters(self, src: int = 0):
         """make the replicated (non-table) parameters identical on every rank"""
@@ -193,43 +194,57 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
             self._req_map = torch.full((self.vocab,), -1, dtype=torch.int32, device=dev)
             self._own_map = torch.full((max(1, self.exchange.local_rows),), -1, dtype=torch.int32, device=dev)
 
-    @staticmethod
-    def _keys(id_sets):
-        return tuple((x.data_ptr(), tuple(x.shape)) for x in id_sets)
+    _ID_KEYS = (ITEM_SEQ_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME)
 
     def prefetch(self, batch):
         """Start the routing of the NEXT step's ids now: its dedup, owner bucketing and the exchange of the
         per-owner counts are enqueued, and the counts copied to the host asynchronously.  Called after the
         current step's forward (sharded.train_step's next_batch), the host reads those split sizes while the GPU
-        still runs the current step's backward, instead of draining the queue at the next step's start.  The
-        batch's id tensors must be the ones the next training_step receives.  Collective: every rank calls it at
-        the same point."""
+        still runs the current backward, instead of draining the queue at the next step's start.
+
+        Contract (collective): every rank calls it at the same point, and the NEXT training_step on every rank
+        receives the very same id tensor objects (int32 or int64, any layout), unmodified in between.  That
+        step always consumes the prefetch -- so every rank runs the same collective sequence -- and raises if its
+        batch is not the prefetched one (a silent re-route on one rank only would misalign the collectives)."""
         self.cancel_prefetch()
-        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME))
-        id_sets = [batch[ITEM_SEQ_ENTRY_NAME], batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]]
+        originals = tuple(batch[k] for k in self._ID_KEYS)
+        batch = self._ids_i64(batch, self._ID_KEYS)
+        id_sets = [batch[k] for k in self._ID_KEYS]
         self._maps(self.model.item_table().device)
         req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
-        self._prefetched = (self._keys(id_sets), id_sets, req, self.exchange.request_begin(req.unique, req.count))
+        self._prefetched = (originals, id_sets, req, self.exchange.request_begin(req.unique, req.count))
 
     def cancel_prefetch(self):
-        """drop a prefetched request that will not be used (its counts exchange is complete on every rank)"""
+        """drop a prefetched request that will not be used (its counts exchange is complete on every rank);
+        collective in effect: every rank must cancel the same prefetch"""
         if self._prefetched is not None:
             self._prefetched[2].release()
             self._prefetched = None
 
-    def _fetch(self, id_sets, train: bool):
+    def _fetch(self, id_sets, train: bool, originals=None):
         """dedup the ids of `id_sets`, route them to their owners, gather the (caught-up) rows and return
-        (exchange state, owner plan or None, compact rows in send order, each id set remapped to them)"""
+        (exchange state, owner plan or None, compact rows in send order, each id set remapped to them).
+        originals: the caller's id tensors before normalisation (a training step): a pending prefetch is
+        consumed, and must be of exactly these tensors"""
         shard = self.model.item_table()
         self._maps(shard.device)
-        pre, self._prefetched = self._prefetched, None
-        if pre is not None and pre[0] == self._keys(id_sets):
-            # 1.-2. dedup and the counts exchange were issued a step ahead (prefetch)
+        pre = None
+        if self._prefetched is not None and originals is None:
+            self.cancel_prefetch()  # an evaluation between prefetch and step: dropped on every rank (collective)
+        elif self._prefetched is not None:
+            pre, self._prefetched = self._prefetched, None
+            if len(pre[0]) != len(originals) or any(a is not b for a, b in zip(pre[0], originals)):
+                pre[2].release()
+                raise RuntimeError("sharded training_step received a batch other than the one passed to prefetch(); "
+                                   "pass the prefetched batch's tensors (or call cancel_prefetch() on every rank)")
+        if pre is not None:
+            # 1.-2. dedup and the counts exchange were issued a step ahead (prefetch); the prefetch normalised
+            # the same tensors, so the plan's registered id sets are the ones this step reads
+            id_sets[:] = pre[1]
             req = pre[2]
             st = self.exchange.request_end(pre[3])
+            self.prefetch_hits += 1
         else:
-            if pre is not None:
-                pre[2].release()
             # 1. requester: dedup every id of the step
             req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
             # 2. route ids to owners (the dedup count stays on the device); owners bring their rows up to date
@@ -250,10 +265,11 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         return st, own, compact, inv
 
     def training_step(self, batch, batch_idx):
-        batch = self._ids_i64(batch, (ITEM_SEQ_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME))
-        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
-        pos, neg = batch[POSITIVE_SAMPLES_ENTRY_NAME], batch[NEGATIVE_SAMPLES_ENTRY_NAME]
-        st, own, compact, (inv_seq, inv_pos, inv_neg) = self._fetch([input_seq, pos, neg], train=True)
+        originals = tuple(batch[k] for k in self._ID_KEYS)
+        batch = self._ids_i64(batch, self._ID_KEYS)
+        id_sets = [batch[k] for k in self._ID_KEYS]
+        st, own, compact, (inv_seq, inv_pos, inv_neg) = self._fetch(id_sets, train=True, originals=originals)
+        input_seq = id_sets[0]
         compact.requires_grad_(True)
         U = compact.shape[0]
         # its gradient: the heads' contributions summed per compact row in a fixed order (no float atomics, no zero fill)

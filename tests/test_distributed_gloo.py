@@ -116,6 +116,31 @@ def _dp_worker(rank, world, port, q):
                 if p.grad is not None:
                     want[n] += p.grad / world
         err = max(float((got[n] - want[n]).abs().max()) for n in got)
+        # gradient accumulation (accumulate_grad_batches = 2): the first micro-batch inside no_sync(), the
+        # second outside; the average over ranks of each rank's accumulated gradient
+        m.zero_grad(set_to_none=True)
+        x2 = [torch.randn(5, 6, generator=g) for _ in range(world)]
+        with red.no_sync():
+            m.loss(xs[rank], use_unused).backward()
+        m.loss(x2[rank], use_unused).backward()
+        red.finish()
+        want2 = {n: torch.zeros_like(p) for n, p in m.named_parameters()}
+        for r in range(world):
+            ref = _Toy()
+            ref.loss(xs[r], r == 0).backward()
+            ref.loss(x2[r], r == 0).backward()
+            for n, p in ref.named_parameters():
+                if p.grad is not None:
+                    want2[n] += p.grad / world
+        err = max(err, max(float((p.grad - want2[n]).abs().max()) for n, p in m.named_parameters()))
+        # a second backward without no_sync() must raise instead of silently averaging only the first
+        m.zero_grad(set_to_none=True)
+        m.loss(xs[rank], True).backward()
+        try:
+            m.loss(xs[rank], True).backward()
+            err = max(err, 1.0)
+        except RuntimeError:
+            pass
         q.put((rank, err, len(red.buckets)))
     except Exception as e:
         q.put((rank, repr(e), 0))

@@ -45,7 +45,7 @@ def _worker(rank, world, port, cfg, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     try:
-        B, L, V, d, h, N, steps = cfg
+        B, L, V, d, h, N, steps, id_dtype = cfg
         torch.manual_seed(0)
         full = _model(asme, V, L, d, h, N)                      # the logical model, identical on every rank
         sd = {k: v.clone() for k, v in full.state_dict().items()}
@@ -83,16 +83,27 @@ def _worker(rank, world, port, cfg, q):
         opt = module.configure_optimizers()
         per = B // world
         losses = []
-        parts = [{k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()} for b in batches]
+        errs = {}
+        # int32 ids (a dataloader's) must hit the prefetch as well: it is keyed on the caller's tensor objects
+        parts = [{k: v[rank * per:(rank + 1) * per].to(dev, id_dtype) for k, v in b.items()} for b in batches]
+        want_hits = 0
         for s, part in enumerate(parts):
             # the next step's id routing started after this step's forward (module.prefetch), except after step 1
             # (step 2 routes its ids inline)
             nxt = parts[s + 1] if s + 1 < len(parts) and s != 1 else None
+            want_hits += nxt is not None
             losses.append(float(asme.sharded.train_step(module, opt, part, s, next_batch=nxt)))
+        errs["prefetch_hit_mismatch"] = abs(module.prefetch_hits - want_hits)
+        # a step given another batch than the prefetched one raises (instead of re-routing on one rank only)
+        module.prefetch(parts[0])
+        try:
+            module.training_step(dict(parts[1]), 0)
+            errs["prefetch_misuse_raises"] = 1
+        except RuntimeError:
+            errs["prefetch_misuse_raises"] = 0
         module.prefetch(parts[0])  # a prefetch nobody consumes: the next _fetch (evaluation) must discard it
         opt.flush()
         got = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-        errs = {}
         for k, v in got.items():
             want = ref_sd[k][rank::world] if k in tables else ref_sd[k]
             errs[k] = float((v - want).abs().max() / (want.abs().max() + 1e-12))
@@ -126,12 +137,16 @@ def _worker(rank, world, port, cfg, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_training_multirank_matches_unsharded(world):
+# (world, d): d = 32 runs every Linear on the general fp32-MFMA kernel, d = 128 (h = 2, d_ff = 512) on the
+# production composition -- the weight-stationary bf16x6 GEMMs, the fused FFN and the split-T weight gradients;
+# W = 8 is the node's shard map (8 ranks on the one GPU, the ids of every owner crossing the exchange)
+@pytest.mark.parametrize("world,d,id_dtype", [(2, 32, torch.int64), (3, 32, torch.int32), (2, 128, torch.int32),
+                                              (8, 128, torch.int64)])
+def test_sharded_training_multirank_matches_unsharded(world, d, id_dtype):
     if not torch.cuda.is_available():
         pytest.skip("no ROCm GPU")
     B = 6 * world
-    cfg = (B, 16, 301, 32, 2, 2, 3)
+    cfg = (B, 16, 301 if d == 32 else 1031, d, 2, 2, 4, id_dtype)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -149,6 +164,7 @@ def test_sharded_training_multirank_matches_unsharded(world):
         for k, e in errs.items():
             if k.endswith("attention.linear_layers.1.bias"):
                 continue  # exact gradient 0 (softmax shift invariance): Adam follows fp32 noise
-            bound = {"eval/rank_mismatches": 0, "eval/predict_step_raises": 0, "eval/ndcg": 1e-6}.get(k, 1e-4)
-            assert e <= bound if k.startswith("eval/") else e < bound, (rank, k, e)
+            exact = {"eval/rank_mismatches": 0, "eval/predict_step_raises": 0, "eval/ndcg": 1e-6,
+                     "prefetch_hit_mismatch": 0, "prefetch_misuse_raises": 0}
+            assert e <= exact[k] if k in exact else e < 1e-4, (rank, k, e)
     assert all(p.exitcode == 0 for p in procs)

@@ -28,8 +28,16 @@ MAP = [
     (r"lazy_row_kernel<\d+, true>", "asme_lazy_adam_stage", True),
     (r"lazy_pipe_kernel<\d+, \d+, \d+, true>", "asme_lazy_adam_stage", True),
     (r"lazy_apply_staged_v4_kernel", "asme_lazy_adam_apply_staged", True),
-    (r"sampled_fwd_kernel", "asme_sampled_logits_fwd", True),
-    (r"sampled_bwd_kernel", "asme_sampled_logits_bwd", True),
+    (r"sampled_fwd4?_kernel", "asme_sampled_logits_fwd", True),
+    (r"sampled_bwd4?_kernel", "asme_sampled_logits_bwd", True),
+    (r"posneg_kernel", "asme_posneg_sample", True),
+    # the sparse table gradient: dedup (claim .. inverse), occurrence CSR (csr_*), ordered sums + Adam (grad_*)
+    (r"claim_kernel", "asme_dedup_ids", True),
+    (r"(flag|compact|inverse|dedup_\w+)_kernel", "asme_dedup_ids", False),
+    (r"csr_count_kernel", "asme_occurrence_csr", True),
+    (r"csr_\w+_kernel", "asme_occurrence_csr", False),
+    (r"grad_chunk_kernel<true>", "asme_table_grad_reduce_apply", True),
+    (r"grad_span_kernel<true>", "asme_table_grad_reduce_apply", False),
     (r"gelu_dropout_fwd_kernel", "asme_gelu_dropout_fwd", True),
     (r"gelu_dropout_bwd_kernel", "asme_gelu_dropout_bwd", True),
     (r"residual_ln_fwd_kernel", "asme_residual_ln_fwd", True),

@@ -11,13 +11,13 @@ export TMPDIR=/tmp
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 echo "bench: $(tail -c 300 $OUT/bench.json)"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
-    python bench.py --steps 5 --warmup 2 --cpu-baseline 0 > "$OUT/kt.log" 2>&1 || exit $?
+    python bench.py --steps 5 --warmup 2 --cpu-baseline 0 --legs none > "$OUT/kt.log" 2>&1 || exit $?
 echo "kernel trace done"
 if [ -n "${PMC:-1}" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "${PMC_REGEX:-asme|attn|emb|lazy|adam|residual|gelu|ln_|weight_grad|sum_slabs|ws_gemm|sampled}" \
+    timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "${PMC_REGEX:-asme|attn|emb|lazy|adam|residual|gelu|ln_|weight_grad|sum_slabs|ws_gemm|sampled|posneg|claim|flag|compact|inverse|dedup|csr_|grad_chunk|grad_span}" \
         -d "$OUT/pmc_$C" -o run --output-format csv -- \
-        python bench.py --steps 2 --warmup 1 --cpu-baseline 0 > "$OUT/pmc_$C.log" 2>&1 || exit $?
+        python bench.py --steps 2 --warmup 1 --cpu-baseline 0 --legs none > "$OUT/pmc_$C.log" 2>&1 || exit $?
     echo "pmc $C done"
   done
 fi
