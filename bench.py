@@ -28,7 +28,8 @@ PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
 # kernels that compute their fp32 products as six bf16 MFMAs of split operands (csrc/common.h, bf16x6): their
 # ceiling is the dense bf16 MFMA peak (2516.6 TF/s = 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz) over 6
 PEAK_BF16X6_TFS = 2516.6 / 6
-BF16X6_KERNELS = {"asme_ws_linear", "asme_linear_weight_grad", "asme_linear_xent_fwd", "asme_linear_xent_bwd", "asme_logits"}
+BF16X6_KERNELS = {"asme_ws_linear", "asme_linear_weight_grad", "asme_linear_xent_fwd", "asme_linear_xent_bwd",
+                  "asme_logits"}
 
 
 def instrumented_steps(steps):
@@ -50,6 +51,19 @@ def committed_profile(name, config):
     with open(path) as f:
         j = json.load(f)
     return j if j.get("config") == config else {}
+
+
+def gemm_work(T, d, ffn):
+    """algorithmic work per launch of the transformer's GEMM calls.  Per block: the forward QKV
+    (d -> 3d), O (d -> d), FFN in (d -> ffn, its epilogue writing the activation and the factor keep * GELU'(pre) the
+    backward needs in place of the pre-activation) and FFN out (ffn -> d), and the same four shapes as input
+    gradients (the GELU one reading the factor), 8 asme_ws_linear calls: bytes in units of T x 4 B = 2 (8d + 3 ffn);
+    the four weight gradients on asme_linear_weight_grad: dY + X = 8d + 2 ffn"""
+    wg_flops = 2.0 * T * (3 * d * d + d * d + ffn * d + d * ffn)
+    ws_bytes = 2 * T * 4.0 * (8 * d + 3 * ffn)
+    wg_bytes = T * 4.0 * (8 * d + 2 * ffn)
+    return {"asme_ws_linear": ("gemm", 2 * wg_flops / 8, ws_bytes / 8),
+            "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4)}
 
 
 def roofline_entries(kstats, work, traffic, busy=None):
@@ -335,7 +349,8 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
     timer = asme._lib.KernelTimer(["asme_attention_fwd", "asme_attention_bwd", "asme_ws_linear",
                                    "asme_linear_weight_grad", "asme_cross_entropy_fwd", "asme_cross_entropy_bwd",
                                    "asme_linear_xent_fwd", "asme_linear_xent_bwd", "asme_cloze_mask",
-                                   "asme_residual_ln_fwd", "asme_residual_ln_bwd"])
+                                   "asme_residual_ln_fwd", "asme_residual_ln_bwd", "asme_embedding_fwd",
+                                   "asme_embedding_bwd"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -351,15 +366,16 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
         elapsed = float(t.item())
     T, H, dk = B * L, args.heads, d // args.heads
     pairs = B * H * L * L  # bidirectional
-    wg_flops = 2.0 * T * (3 * d * d + d * d + 4 * d * d + 4 * d * d)
     ffn = 4 * d
-    ws_bytes, wg_bytes = 2 * T * 4.0 * (8 * d + 3 * ffn), T * 4.0 * (8 * d + 2 * ffn)  # see the SASRec leg
     M = 0.9 * 0.2 * T + 0.1 * B  # expected non-ignored rows of a cloze batch
     work = {"asme_attention_fwd": ("mfma", 4.0 * pairs * dk), "asme_attention_bwd": ("mfma", 10.0 * pairs * dk),
-            "asme_ws_linear": ("gemm", 2 * wg_flops / 8, ws_bytes / 8),
-            "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4),
+            **gemm_work(T, d, ffn),
             "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
-            "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0)}
+            "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0),
+            "asme_residual_ln_fwd": ("hbm", 4 * T * d * 4 + T * 8),
+            "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),
+            "asme_embedding_fwd": ("hbm", T * 8 + 2 * T * d * 4 + T * 16),
+            "asme_embedding_bwd": ("hbm", T * 8 + 3 * T * d * 4 + T * 16)}
     lb = committed_profile("logits_mfma_busy.json", {"workload": workload, "rows": 36966, "items": V, "dim": d})
     # HBM traffic per launch from the committed rocprofv3 PMC pass over this workload (tools/pmc_traffic.py)
     tp = committed_profile(f"pmc_traffic_{workload}.json", {"batch": B, "seq_len": L, "items": items,
@@ -487,7 +503,8 @@ def main():
                                    "asme_lazy_adam_apply", "asme_lazy_adam_stage", "asme_lazy_adam_apply_staged",
                                    "asme_sampled_logits_fwd", "asme_sampled_logits_bwd", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
-                                   "asme_ws_linear", "asme_posneg_sample"])
+                                   "asme_ws_linear", "asme_posneg_sample", "asme_table_grad_reduce_apply",
+                                   "asme_dedup_ids", "asme_occurrence_csr"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -531,19 +548,11 @@ def main():
     # forward = 2 matmul passes (QK^T, PV), the backward = 5 (recomputed S, dP, dV, dK, dQ) -- the kernels
     # spend 2 more (dP and S again in the dK/dV pass), which is overhead, not algorithmic work.
     pairs = B * H * L * (L + 1) / 2.0
-    # weight-gradient GEMMs: 4 per block (QKV, O, FFN in, FFN out), averaged per launch
-    wg_flops = 2.0 * T * (3 * d * d + d * d + ffn * d + d * ffn)
-    # GEMM bytes per block (units of T x 4 B): forward X + Y of QKV (d + 3d), O (d + d), FFN in (d + act 4d + the
-    # activation factor 4d the backward needs in place of the pre-activation), FFN out (4d + d) = 8d + 3 ffn; the
-    # input gradients the same (dY + dX, the GELU one reading the factor); weight gradients dY + X = 8d + 2 ffn
-    ws_bytes = 2 * T * 4.0 * (8 * d + 3 * ffn)
-    wg_bytes = T * 4.0 * (8 * d + 2 * ffn)
     work = {
         "asme_attention_fwd": ("mfma", 2 * 2.0 * pairs * dk),
         "asme_attention_bwd": ("mfma", 5 * 2.0 * pairs * dk),
-        "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4),
-        # forward + input-gradient GEMMs: 8 per block, the same 4 shapes twice, averaged per launch
-        "asme_ws_linear": ("gemm", 2 * wg_flops / 8, ws_bytes / 8),
+        # the GEMM calls per block, averaged per launch (gemm_work)
+        **gemm_work(T, d, ffn),
         "asme_gelu_dropout_fwd": ("hbm", 2 * T * ffn * 4),
         "asme_residual_ln_fwd": ("hbm", 4 * T * d * 4 + T * 8),
         "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),
@@ -562,6 +571,15 @@ def main():
         "asme_adam_rows_step": ("hbm", 6 * V * d * 4 + V * 4 + U * d * 4),
         # session items read once + x / pos / neg written (the in-session membership scans hit the cache)
         "asme_posneg_sample": ("hbm", B * (L + 1) * 8 + 3 * B * L * 8 + B * 8),
+        # the step's n = 3T table ids: read once, the slot map probed per id and written per unique row, the
+        # inverse (n) and the unique ids (U) written
+        "asme_dedup_ids": ("hbm", 3 * T * (8 + 4 + 8) + U * (8 + 4)),
+        # occurrence CSR: the inverse read, order + sorted slot written (int32), the U + 1 segment offsets
+        "asme_occurrence_csr": ("hbm", 3 * T * (8 + 4 + 4) + 4 * (U + 1)),
+        # ordered per-row sums + the lazy Adam step: the three contributions' rows (embedding d_rows, h for the
+        # pos and for the neg ids) + their scales, order / slot per occurrence, the staged p / m / v read, the
+        # table's p / m / v rows + last_step written, the unique ids read
+        "asme_table_grad_reduce_apply": ("hbm", 3 * T * d * 4 + 2 * T * 4 + 3 * T * 8 + 6 * U * d * 4 + U * 12),
     }
     # HBM traffic per launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE, gfx950
     # corrections of MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py) for this exact configuration

@@ -267,13 +267,13 @@ int asme_dedup_reset(const int64_t* unique, const int32_t* count, int64_t cap, i
 int asme_owner_histogram(const int64_t* unique, const int32_t* count, int64_t cap, int world, int32_t* owner,
                          int32_t* counts, void* stream);
 /* stable grouping of n unique ids by owner (id % world, world <= 64): order[j] = index of the j-th id sent,
- * send_local[j] = ids[order[j]] / world, counts[w] (int64) = ids sent to rank w, pos (nullable) = the inverse
+ * send_local[j] (int32) = ids[order[j]] / world, counts[w] (int64) = ids sent to rank w, pos (nullable) = the inverse
  * permutation (pos[order[j]] = j).  n_dev (nullable): only the first min(n, *n_dev) ids take part -- the dedup
  * count stays on the device (no host sync before the exchange).  Workspace: asme_bucket_by_owner_workspace
  * bytes. */
 int64_t asme_bucket_by_owner_workspace(int64_t n, int world);
 int asme_bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, void* workspace,
-                         int64_t ws_bytes, int64_t* order, int64_t* send_local, int64_t* counts, int64_t* pos,
+                         int64_t ws_bytes, int64_t* order, int32_t* send_local, int64_t* counts, int64_t* pos,
                          void* stream);
 /* out[r] = table[ids[r]] (zero row for ids outside [0, vocab)): the owner side of the sharded lookup */
 int asme_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t vocab, int64_t dim, float* out,

@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_
                                                                     const int32_t* __restrict__ n_dev, int W,
                                                                     const int32_t* __restrict__ boff, int64_t nb,
                                                                     int64_t* __restrict__ order,
-                                                                    int64_t* __restrict__ send_local) {
+                                                                    int32_t* __restrict__ send_local) {
     constexpr int kWv = kBkThreads / 64;
     n = live_n(n, n_dev);
     __shared__ int32_t base[kMaxW];
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_
             for (int v = 0; v < wave; ++v) pre += wcnt[v][mine];
             const int64_t pos = (int64_t)base[mine] + pre + rank;
             order[pos] = i;
-            send_local[pos] = id / W;
+            send_local[pos] = (int32_t)(id / W);
         }
         __syncthreads();
         for (int w = threadIdx.x; w < W; w += blockDim.x) {
@@ -275,11 +275,12 @@ ASME_API int64_t asme_bucket_by_owner_workspace(int64_t n, int world) {
 }
 
 // Row-shard request routing: the n unique ids, grouped by owner (id % world) in a stable order.
-// order[j] = index into ids of the j-th id sent; send_local[j] = ids[order[j]] / world (the owner's row);
+// order[j] = index into ids of the j-th id sent; send_local[j] = ids[order[j]] / world (the owner's row, int32: what
+// crosses the fabric; a shard holds < 2^31 rows);
 // counts[w] = ids sent to rank w (int64, world entries); pos[order[j]] = j (nullable: the inverse permutation).
 // n_dev (nullable): only the first *n_dev <= n ids are live (the dedup count on the device: no host sync).
 ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, void* workspace,
-                                  int64_t ws_bytes, int64_t* order, int64_t* send_local, int64_t* counts, int64_t* pos,
+                                  int64_t ws_bytes, int64_t* order, int32_t* send_local, int64_t* counts, int64_t* pos,
                                   void* stream) {
     ASME_CHECK_ARG(ids && workspace && order && send_local && counts, "asme_bucket_by_owner: null pointer");
     ASME_CHECK_ARG(world >= 1 && world <= kMaxW, "asme_bucket_by_owner: world must be in [1, 64]");

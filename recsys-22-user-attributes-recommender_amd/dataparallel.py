@@ -44,11 +44,16 @@ class _Bucket:
 class GradientAllReduce:
     """Bucketed, backward-overlapped gradient averaging over `group` (DDP semantics)."""
 
-    def __init__(self, module: torch.nn.Module, group=None, bucket_bytes: int = 25 << 20):
+    def __init__(self, module: torch.nn.Module, group=None, bucket_bytes: int = 25 << 20,
+                 sharded_table: bool = False):
+        """sharded_table: the item table is a row shard (sharded.py) whose gradient reaches its owner through
+        the all-to-all exchange; it is left out here entirely (only the replicated parameters are averaged)"""
         self.group = group
         self.world = dist.get_world_size(group)
         self.table = module.model.item_table() if hasattr(module, "model") else None
         params = [p for p in module.parameters() if p.requires_grad]
+        if sharded_table and self.table is not None:
+            params = [p for p in params if p is not self.table]
         # a row-sparse table arrives through its plan, not through .grad: reduced last (see finish)
         self.sparse_table = (self.table is not None and getattr(module, "table_grad", "dense") == "sparse"
                              and any(p is self.table for p in params))

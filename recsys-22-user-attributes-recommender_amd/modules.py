@@ -331,7 +331,7 @@ class NextItemPredictionTrainingModule(_TableGradMixin, _Base):
 class MaskedTrainingModule(_TableGradMixin, _Base):
     def __init__(self, model, item_tokenizer, metrics, learning_rate: float = 0.001, beta_1: float = 0.99,
                  beta_2: float = 0.998, weight_decay: float = 0.001, num_warmup_steps: int = 10000,
-                 table_grad: Optional[str] = None):
+                 table_grad: Optional[str] = None, fused_eval: Optional[bool] = None):
         super().__init__()
         self.model = model
         self.learning_rate, self.beta_1, self.beta_2 = learning_rate, beta_1, beta_2
@@ -339,6 +339,10 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         self.num_warmup_steps = num_warmup_steps
         self.item_tokenizer = item_tokenizer
         self.metrics = metrics
+        # fused_eval: rank each masked position's target with asme_catalog_rank from its hidden state and the head
+        # (no (n, |V|) predictions; needs a linear / tied head, one target per sequence and a rank-based metrics
+        # container); None = whenever that holds.  Validation then returns predictions=None.
+        self.fused_eval = fused_eval
         self._init_table_grad(table_grad)
 
     def forward(self, batch, batch_idx: Optional[int] = None) -> torch.Tensor:
@@ -359,15 +363,42 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
 
     def _get_prediction_for_masked_item(self, batch, batch_idx=None) -> torch.Tensor:
         self._flush_table()
-        input_seq = batch[ITEM_SEQ_ENTRY_NAME]
-        target_mask = input_seq.eq(self.item_tokenizer.mask_token_id)
+        rows = self._masked_rows(batch)
+        return self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
+
+    def _masked_rows(self, batch) -> torch.Tensor:
+        target_mask = batch[ITEM_SEQ_ENTRY_NAME].eq(self.item_tokenizer.mask_token_id)
         if target_mask.dim() == 3:
             target_mask = target_mask.max(dim=-1).values
-        rows = torch.nonzero(target_mask.reshape(-1)).squeeze(1)
-        return self.model.forward_rows(build_model_input(self.model, self.item_tokenizer, batch), rows)
+        return torch.nonzero(target_mask.reshape(-1)).squeeze(1)
+
+    def catalog_ranks(self, batch) -> torch.Tensor:
+        """1-based full-catalogue rank (ties to the lower id) of the target of each sequence's masked position
+        (the last-item mask of evaluation, last_item_mask.py:35-44): the masked positions' hidden states against the
+        head through asme_catalog_rank, no (n, |V|) predictions.  masked_training_module.py:80-91 + AllItemsSampler
+        + NDCG's argsort (metrics/common.py:4-27)."""
+        self._flush_table()
+        sequence = build_model_input(self.model, self.item_tokenizer, batch)
+        rows = self._masked_rows(batch)
+        targets = batch[TARGET_ENTRY_NAME]
+        if rows.numel() != targets.numel():
+            raise ValueError("fused masked evaluation needs exactly one masked position per sequence")
+        w, b = self.model.head_weight_bias()
+        return ops.catalog_rank(self.model.encode_rows(sequence, rows), w, targets, b)
+
+    def _use_fused_eval(self, targets) -> bool:
+        if targets.dim() != 1 or self.metrics is None or not hasattr(self.metrics, "update_ranks"):
+            return False
+        if not hasattr(self.model, "head_weight_bias") or self.model.head_weight_bias() is None:
+            return False
+        return True if self.fused_eval is None else bool(self.fused_eval)
 
     def _eval_step(self, batch, batch_idx, is_test: bool = False):
         input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
+        if self._use_fused_eval(targets) and self._masked_rows(batch).numel() == targets.numel():
+            with torch.no_grad():
+                self.metrics.update_ranks(self.catalog_ranks(batch))
+            return build_eval_step_return_dict(input_seq, None, targets)
         prediction = self._get_prediction_for_masked_item(batch, batch_idx)
         loss = ops.cross_entropy(prediction, targets, self.item_tokenizer.pad_token_id)
         self.log(LOG_KEY_TEST_LOSS if is_test else LOG_KEY_VALIDATION_LOSS, loss, prog_bar=True)
@@ -405,6 +436,9 @@ class UBERTMaskedTrainingModule(MaskedTrainingModule):
         super().__init__(model, item_tokenizer, metrics, learning_rate, beta_1, beta_2, weight_decay,
                          num_warmup_steps, table_grad)
         self.user_key_len = len(model.optional_metadata_keys())
+
+    def _use_fused_eval(self, targets) -> bool:
+        return False  # the output carries the user column: predictions come from the overridden row extraction
 
     def _with_user_column(self, x: torch.Tensor, fill) -> torch.Tensor:
         if self.user_key_len == 0:

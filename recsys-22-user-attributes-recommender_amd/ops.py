@@ -529,7 +529,7 @@ def bucket_by_owner(unique: torch.Tensor, world: int, count: Optional[torch.Tens
     dev = u.device
     ws = torch.empty(max(8, int(_lib.load().asme_bucket_by_owner_workspace(n, world))), device=dev, dtype=torch.uint8)
     order = torch.empty(n, device=dev, dtype=torch.int64)
-    send_local = torch.empty(n, device=dev, dtype=torch.int64)
+    send_local = torch.empty(n, device=dev, dtype=torch.int32)
     counts = torch.empty(world, device=dev, dtype=torch.int64)
     pos = torch.empty(n, device=dev, dtype=torch.int64)
     call("asme_bucket_by_owner", ptr(u), n, ptr(count), world, ptr(ws), ws.numel(), ptr(order), ptr(send_local),

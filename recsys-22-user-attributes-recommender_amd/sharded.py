@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from .dataparallel import GradientAllReduce
 from .modules import (ITEM_SEQ_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME,
                       TARGET_ENTRY_NAME, SequenceNextItemPredictionTrainingModule, build_eval_step_return_dict,
                       get_additional_meta_data, get_padding_mask)
@@ -118,7 +119,7 @@ class RowShardExchange:
             owner = unique % W
             order = torch.argsort(owner, stable=True)
             send_counts_t = torch.bincount(owner, minlength=W).to(torch.int64)
-            send_local = (unique.index_select(0, order) // W).contiguous()
+            send_local = (unique.index_select(0, order) // W).to(torch.int32)
             pos = torch.empty_like(order)
             pos[order] = torch.arange(len(order), dtype=order.dtype)
         recv_counts_t = torch.empty_like(send_counts_t)
@@ -139,9 +140,11 @@ class RowShardExchange:
         if event is not None:
             event.synchronize()  # the step's one host sync
         sc, rc = host[0].tolist(), host[1].tolist()
-        recv_local = torch.empty(sum(rc), dtype=torch.int64, device=dev)
-        _all_to_all(recv_local, send_local[:sum(sc)], rc, sc, group=self.group)
-        return ExchangeState(order[:sum(sc)], sc, rc, recv_local, pos)
+        # owner-local rows cross the fabric as int32 (a shard holds < 2^31 rows); widened once on arrival for the
+        # gather / dedup kernels, which take int64 row ids
+        recv32 = torch.empty(sum(rc), dtype=torch.int32, device=dev)
+        _all_to_all(recv32, send_local[:sum(sc)], rc, sc, group=self.group)
+        return ExchangeState(order[:sum(sc)], sc, rc, recv32.to(torch.int64), pos)
 
     def reply_rows(self, st: ExchangeState, rows: torch.Tensor) -> torch.Tensor:
         """owners' rows (aligned with st.recv_local) -> the requester's rows in SEND order: row j belongs to
@@ -181,6 +184,10 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         self._pending = None
         self._prefetched = None  # (caller's id tensors, normalised id sets, requester plan, request_begin state)
         self.prefetch_hits = 0   # training steps that consumed a prefetch (tests assert the overlap really ran)
+        # the replicated parameters average through the bucketed, backward-overlapped all-reduce (DDP semantics);
+        # the shard is excluded (its rows travel to their owners in after_backward)
+        self.reducer = (GradientAllReduce(self, group, sharded_table=True)
+                        if self.exchange.world > 1 else None)
 
     def broadcast_dense_parameters(self, src: int = 0):
         """make the replicated (non-table) parameters identical on every rank"""
@@ -292,10 +299,13 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
 
     @torch.no_grad()
     def after_backward(self):
-        """route the compact table gradient to the owners and average the replicated gradients"""
+        """average the replicated gradients (their buckets were launched during the backward) and route the
+        compact table gradient to the owners.  Collective order, identical on every rank: the bucket all-reduces
+        (hooks, then finish's forced launches), then the gradient all-to-all."""
         st, own, compact, cplan = self._pending
         self._pending = None
-        W = self.exchange.world
+        if self.reducer is not None:
+            self.reducer.finish()
         g = cplan.grad_rows[:compact.shape[0]]
         if compact.grad is not None:  # a head without the plan path returned a dense gradient
             g = g + compact.grad
@@ -305,16 +315,6 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         if len(st.recv_local):
             own.add_rows(st.recv_local, recv)  # ordered per-row sums x 1/W (deterministic)
         shard._asme_table_grad.plan = own
-        dense = [p for p in self.model.parameters() if p is not shard and p.grad is not None]
-        if dense and W > 1:
-            flat = torch.cat([p.grad.reshape(-1) for p in dense])
-            _all_reduce(flat, group=self.group)
-            flat.mul_(1.0 / W)
-            off = 0
-            for p in dense:
-                n = p.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
 
 
     # ---------------------------------------------------------------- evaluation on the sharded table

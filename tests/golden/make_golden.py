@@ -118,11 +118,10 @@ def gen_sasrec_neg(B=4, L=12, d=32, h=2, N=2, NI=57, lengths=(12, 9, 5, 1), suff
     print("sasrec_neg" + suffix, float(loss))
 
 
-def gen_sasrec_cross():
+def gen_sasrec_cross(B=4, L=10, d=32, h=2, N=2, NI=45, lengths=(10, 7, 3, 2), suffix=""):
     """sasrec-cross: NextItemPredictionTrainingModule + SASRecModel(mode=full)
     core/modules/next_item_prediction_training_module.py:141-256
     core/losses/sasrec/sas_rec_losses.py:9-32, core/models/common/layers/layers.py:92-109"""
-    B, L, d, h, N, NI = 4, 10, 32, 2, 2, 45
     tok = S.make_tokenizer(NI)
     S.set_context({"item": tok})
     from asme.core.models.sasrec.sasrec_model import SASRecModel
@@ -136,7 +135,7 @@ def gen_sasrec_cross():
                                               loss_function=SASRecFullSequenceCrossEntropyLoss)
     sd = _sd(model)
     g = torch.Generator().manual_seed(3)
-    lengths = [10, 7, 3, 2]
+    lengths = list(lengths)
     full = _ragged_batch(g, B, L + 1, V, [n + 1 for n in lengths])
     seq = full[:, :L].clone()
     tgt = full[:, 1:].clone()
@@ -158,12 +157,14 @@ def gen_sasrec_cross():
     out = dict(sd)
     out.update(grads)
     out.update(after)
-    out.update(dict(seq=seq.numpy(), target=tgt.numpy(), logits=logits.numpy(), loss=loss.detach().numpy(),
+    head = 16 if suffix else L  # the d = 128 fixture keeps the first 16 positions' logits
+    out.update(dict(seq=seq.numpy(), target=tgt.numpy(), logits=logits[:, :head].numpy(), loss=loss.detach().numpy(),
                     emb_out=hooks["emb_out"].numpy(), enc_out=hooks["enc_out"].numpy(), eval_logits=last.numpy(),
+                    logits_head=np.int64(head),
                     cfg=np.array([B, L, d, h, N, V]), lr=np.float32(1e-3), betas=np.array([0.99, 0.998], np.float32),
                     weight_decay=np.float32(0.0)))
-    np.savez_compressed(os.path.join(HERE, "sasrec_cross.npz"), **out)
-    print("sasrec_cross", float(loss))
+    np.savez_compressed(os.path.join(HERE, f"sasrec_cross{suffix}.npz"), **out)
+    print("sasrec_cross" + suffix, float(loss))
 
 
 def _cloze_batch(g, B, L, V, lengths):
@@ -286,11 +287,10 @@ def gen_kebert4rec(variant: str, B=4, L=10, d=32, h=2, N=2, NI=41, NG=7, NT=9, K
     print("kebert4rec", variant + suffix, float(loss))
 
 
-def gen_ubert4rec(variant: str):
+def gen_ubert4rec(variant: str, B=4, L=10, d=32, h=2, N=2, NI=43, NG=7, NU=6, K=3, lengths=(10, 7, 4, 2), suffix=""):
     """ubert4rec: UBERTMaskedTrainingModule + UBERT4RecModel (the user-attribute model): a user token prepended to
     the item sequence, attribute embeddings, optional segment embedding, causal transformer (bidirectional=False)
     core/models/ubert4rec/ubert4rec_model.py:16-92, components.py:13-203, core/modules/ubert_masked_training_module.py"""
-    B, L, d, h, N, NI, NG, NU, K = 4, 10, 32, 2, 2, 43, 7, 6, 3
     tok = S.make_tokenizer(NI)
     gtok = S.make_tokenizer(NG, "Genre")
     utok = S.make_tokenizer(NU, "User")
@@ -316,7 +316,7 @@ def gen_ubert4rec(variant: str):
     module = UBERTMaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None, num_warmup_steps=0)
     sd = _sd(model)
     g = torch.Generator().manual_seed(11)
-    lengths = [10, 7, 4, 2]
+    lengths = list(lengths)
     seq, tgt = _cloze_batch(g, B, L, V, lengths)
     if variant == "seg":
         genre = torch.randint(3, len(gtok), (B, L), generator=g)
@@ -347,12 +347,14 @@ def gen_ubert4rec(variant: str):
     out = dict(sd)
     out.update(grads)
     out.update(after)
+    head = 16 if suffix else logits.shape[1]
     out.update(dict(seq=seq.numpy(), target=tgt.numpy(), genre=genre.numpy(), user=user.numpy(),
-                    logits=logits.numpy(), loss=loss.detach().numpy(), eval_seq=ev.numpy(), eval_logits=pred.numpy(),
+                    logits=logits[:, :head].numpy(), loss=loss.detach().numpy(), eval_seq=ev.numpy(),
+                    eval_logits=pred.numpy(), logits_head=np.int64(head),
                     cfg=np.array([B, L, d, h, N, V, len(gtok), len(utok)]), lr=np.float32(1e-3),
                     betas=np.array([0.99, 0.998], np.float32)))
-    np.savez_compressed(os.path.join(HERE, f"ubert4rec_{variant}.npz"), **out)
-    print("ubert4rec", variant, float(loss), logits.shape)
+    np.savez_compressed(os.path.join(HERE, f"ubert4rec_{variant}{suffix}.npz"), **out)
+    print("ubert4rec", variant + suffix, float(loss), logits.shape)
 
 
 def gen_narm():
@@ -506,6 +508,79 @@ def gen_ml1m_anchor(train_steps: int = 400):
     print("ml1m anchor NDCG@10 =", float(ndcg))
 
 
+def gen_bert4rec_anchor(train_steps: int = 300):
+    """BERT4Rec NDCG@10 parity anchor through the masked evaluation: the reference BERT4Rec (tied head) trained with
+    the reference MaskedTrainingModule on the ml-1m-shaped synthetic sessions of gen_ml1m_anchor (cloze masking
+    p = 0.2 plus the last item, torch generator draws), evaluated as ASME evaluates it: each user's sequence without
+    its held-out last item, a MASK appended (LastItemMaskProcessor, data/datasets/processors/last_item_mask.py:35-44),
+    predictions at the MASK (masked_training_module.py:80-91), AllItemsSampler + NDCG@10 (core/metrics)."""
+    rng = np.random.default_rng(1234)
+    n_users, n_items, L, d = 6040, 3416, 50, 64
+    tok = S.make_tokenizer(n_items)
+    S.set_context({"item": tok})
+    from asme.core.models.bert4rec.bert4rec_model import BERT4RecModel
+    from asme.core.modules.masked_training_module import MaskedTrainingModule
+    from asme.core.metrics.ndcg import NormalizedDiscountedCumulativeGainMetric
+    from asme.core.metrics.container.metrics_sampler import AllItemsSampler
+    V = len(tok)
+    seqs = _markov_sessions(rng, n_users, n_items, 20, 120)
+    torch.manual_seed(43)
+    model = BERT4RecModel(transformer_hidden_size=d, num_transformer_heads=2, num_transformer_layers=2,
+                          max_seq_length=L, transformer_dropout=0.1)
+    module = MaskedTrainingModule(model=model, metrics=None, num_warmup_steps=0)
+    opts = module.configure_optimizers()
+    opt = opts[0] if isinstance(opts, (list, tuple)) else opts
+    opt = opt[0] if isinstance(opt, (list, tuple)) else opt
+    torch.set_num_threads(8)
+    model.train()
+    g = torch.Generator().manual_seed(78)
+    B = 128
+    for step in range(train_steps):
+        idx = rng.integers(0, n_users, B)
+        seq = torch.zeros(B, L, dtype=torch.long)
+        for r, u in enumerate(idx):
+            s = seqs[u][:-1][-L:]                # train on everything but the held-out last item
+            seq[r, :len(s)] = torch.from_numpy(s)
+        valid = seq != PAD
+        m = (torch.rand(B, L, generator=g) < 0.2) & valid
+        last = valid.sum(1) - 1
+        m[torch.arange(B), last] = True
+        tgt = torch.where(m, seq, torch.zeros_like(seq))
+        inp = torch.where(m, torch.full_like(seq, MASK), seq)
+        opt.zero_grad()
+        loss = module.training_step({"item": inp, "item.target": tgt}, step)["loss"]
+        loss.backward()
+        opt.step()
+        if step % 100 == 0:
+            print("  bert4rec anchor train step", step, float(loss))
+    torch.set_num_threads(1)
+    model.eval()
+    eval_seq = np.zeros((n_users, L), np.int16)
+    targets = np.zeros(n_users, np.int64)
+    for u, s in enumerate(seqs):
+        inp = s[:-1][-(L - 1):]
+        eval_seq[u, :len(inp)] = inp
+        eval_seq[u, len(inp)] = MASK                 # the last-item mask appended
+        targets[u] = s[-1]
+    metric = NormalizedDiscountedCumulativeGainMetric(k=10)
+    per_user = []
+    with torch.no_grad():
+        for i in range(0, n_users, 256):
+            seq = torch.from_numpy(eval_seq[i:i + 256].astype(np.int64))
+            tg = torch.from_numpy(targets[i:i + 256])
+            pred = module.predict_step({"item": seq}, 0)
+            samp = AllItemsSampler().sample(seq, tg, pred)
+            metric.update(samp.sampled_predictions, samp.positive_item_mask, samp.metric_mask)
+            per_user.append(metric._calc_metric(samp.sampled_predictions, samp.positive_item_mask,
+                                                torch.ones_like(samp.positive_item_mask)).numpy())
+    ndcg = metric.compute()
+    out = {f"sd/{k}": v.detach().numpy() for k, v in model.state_dict().items()}
+    out.update(dict(eval_seq=eval_seq, targets=targets, ndcg10=ndcg.numpy(), ndcg10_per_user=np.concatenate(per_user),
+                    cfg=np.array([n_users, L, d, 2, 2, V])))
+    np.savez_compressed(os.path.join(HERE, "bert4rec_anchor.npz"), **out)
+    print("bert4rec anchor NDCG@10 =", float(ndcg))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "metrics", "ml1m"]
     if "models" in which:
@@ -527,6 +602,16 @@ if __name__ == "__main__":
         gen_bert4rec("linear", lengths=(200, 150, 37, 5), adam2=False, **big)
         gen_bert4rec("transpose_embedding", lengths=(200, 150, 37, 5), adam2=False, **big)
         gen_kebert4rec("post", lengths=(200, 120, 77, 9), NG=7, NT=9, K=3, **big)
+    if "d128b" in which:
+        # the same composition for the other model families (round 3): vocabularies of 300 items keep the
+        # fixtures small; d, h, d_ff and L are the production ones
+        big = dict(B=4, L=200, d=128, h=2, N=2, NI=300, suffix="_d128")
+        gen_sasrec_cross(lengths=(200, 143, 40, 6), **big)
+        gen_kebert4rec("pre", lengths=(200, 131, 57, 8), NG=7, NT=9, K=3, **big)
+        gen_ubert4rec("seg", lengths=(200, 160, 33, 4), NG=7, NU=6, K=3, **big)
+        gen_ubert4rec("upscale", lengths=(200, 97, 21, 3), NG=7, NU=6, K=3, **big)
+    if "bert4rec_anchor" in which:
+        gen_bert4rec_anchor()
     if "metrics" in which:
         gen_metrics()
     if "ml1m" in which:

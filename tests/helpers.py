@@ -85,7 +85,8 @@ MODEL_FIXTURES = ["sasrec_neg", "sasrec_cross", "bert4rec_transpose_embedding", 
                   "kebert4rec_pre", "kebert4rec_post", "ubert4rec_seg", "ubert4rec_upscale", "narm"]
 # the benchmarked composition: d = 128, h = 2, d_ff = 512, L = 200 (make_golden.py d128)
 D128_FIXTURES = ["sasrec_neg_d128", "bert4rec_linear_d128", "bert4rec_transpose_embedding_d128",
-                 "kebert4rec_post_d128"]
+                 "kebert4rec_post_d128", "sasrec_cross_d128", "kebert4rec_pre_d128", "ubert4rec_seg_d128",
+                 "ubert4rec_upscale_d128"]
 
 
 def rel_err(a, b):

@@ -633,7 +633,7 @@ def test_bucket_by_owner_matches_stable_argsort(asme, dev, world, n):
     ref = torch.argsort(owner, stable=True)
     assert torch.equal(order, ref)
     assert torch.equal(counts, torch.bincount(owner, minlength=world))
-    assert torch.equal(send_local, unique[ref] // world)
+    assert send_local.dtype == torch.int32 and torch.equal(send_local.long(), unique[ref] // world)
     assert torch.equal(pos[order], torch.arange(n, device=dev))
     # the same ids at the head of a larger buffer with the live count on the device (the sharded step's form)
     padded = torch.cat([unique, torch.randint(0, 10_000_003, (777,), generator=g).to(dev)])

@@ -54,9 +54,12 @@ def test_gru_rejects_unsupported(asme, dev):
         mod = torch.nn.GRU(8, 16, **{"batch_first": True, **kw}).to(dev)
         with pytest.raises(NotImplementedError):
             asme.ops.gru(torch.randn(2, 3, 8, device=dev), mod)
+    # wider than the register-resident kernel: the library GRU on the device (the reference's own nn.GRU)
     mod = torch.nn.GRU(8, 144, batch_first=True).to(dev)
-    with pytest.raises(NotImplementedError):
-        asme.ops.gru(torch.randn(2, 3, 8, device=dev), mod)
+    x = torch.randn(2, 3, 8, device=dev)
+    assert torch.equal(asme.ops.gru(x, mod), mod(x)[0])
+    with pytest.raises(asme._lib.ASMEKernelError):
+        asme.ops.gru(x.cpu(), mod.cpu())
 
 
 @pytest.mark.parametrize("N,S,H", [(1, 1, 8), (7, 9, 24), (33, 200, 128), (4, 300, 130)])
