@@ -117,15 +117,20 @@ int asme_attention_fwd(const float* q, const float* k, const float* v, int64_t l
                        const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
                        int causal, float scale, float p_drop, uint64_t seed, float* out, int64_t ld_out, float* lse,
                        uint8_t* drop_mask, void* stream);
-/* dsum_ws: (batch*heads*seq_len) floats of workspace. dq/dk/dv may be column blocks of one buffer. */
+/* workspace: asme_attention_bwd_workspace() bytes (row sums D_i = dO_i . O_i, then the dS image the resident
+ * path's dK/dV pass stores for its dQ pass: (batch*heads) x Lp x Lp floats, Lp = seq_len rounded up to 16).
+ * dq/dk/dv may be column blocks of one buffer. */
+int64_t asme_attention_bwd_workspace(int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim);
 int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k, int64_t ld_v,
                        const float* out, int64_t ld_out, const float* dout, int64_t ld_dout, const float* lse,
                        const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
-                       int causal, float scale, float p_drop, uint64_t seed, const uint8_t* drop_mask, float* dsum_ws,
+                       int causal, float scale, float p_drop, uint64_t seed, const uint8_t* drop_mask, float* workspace,
                        float* dq, int64_t ld_dq, float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream);
 /* Attention kernel selection: 0 = automatic (one workgroup per (batch, head) with the head's operands
- * resident in LDS whenever 2*ceil(L/16)*16*(dk+4)*4 B fits 160 KiB, else the 64-row streaming kernels),
- * 1 = streaming kernels only.  Returns the previous mode.  Process-wide; for tests and A/B timing. */
+ * resident in LDS whenever 2*ceil(L/16)*16*(dk+4)*4 B fits 160 KiB, else the 64-row streaming kernels; the
+ * resident backward runs dK/dV first, storing dS, then dQ = dS K), 1 = streaming kernels only, 2 = resident
+ * kernels with a dQ pass that recomputes S and dP.  Returns the previous mode.  Process-wide; for tests and A/B
+ * timing. */
 int asme_attention_set_mode(int mode);
 /* Size of the drop_mask buffer for asme_attention_fwd/bwd (p_drop > 0). */
 int64_t asme_attention_dropout_mask_bytes(int64_t batch, int64_t heads, int64_t seq_len);

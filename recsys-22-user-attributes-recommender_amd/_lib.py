@@ -59,6 +59,7 @@ SIGNATURES = {
     "asme_linear_fwd": [p, i64, i64, i64, p, p, i64, p, i64, p],
     "asme_linear_dx": [p, i64, i64, i64, p, i64, p, i64, i32, p],
     "asme_attention_dropout_mask_bytes": [i64, i64, i64],
+    "asme_attention_bwd_workspace": [i64, i64, i64, i64],
     "asme_gelu_dropout_fwd": [p, i64, f32, u64, p, p],
     "asme_dropout": [p, i64, f32, u64, p, p],
     "asme_dropout_rows": [p, i64, i64, f32, u64, p, p],
@@ -103,6 +104,7 @@ SIGNATURES = {
 _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64,
              "asme_linear_weight_grad_workspace": ctypes.c_int64,
              "asme_attention_dropout_mask_bytes": ctypes.c_int64,
+             "asme_attention_bwd_workspace": ctypes.c_int64,
              "asme_catalog_topk_workspace": ctypes.c_int64, "asme_linear_xent_fwd_workspace": ctypes.c_int64,
              "asme_linear_xent_bwd_workspace": ctypes.c_int64, "asme_logits_workspace": ctypes.c_int64, "asme_bucket_by_owner_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
              "asme_table_grad_workspace": ctypes.c_int64}

@@ -894,13 +894,16 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dq_res_kernel(
     }
 }
 
-template <int DK>
+// DS = true (the default path): this pass runs FIRST, computes D_i = rowsum(dO_i * O_i) itself and stores every
+// dS value it forms (query-major, (B*H) x Lp x Lp) for the dQ pass (attn_bwd_dq_ds_kernel), which then needs one
+// product (dQ = dS K) instead of recomputing S and dP.  DS = false: D_i comes from attn_bwd_dq_res_kernel.
+template <int DK, bool DS>
 __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
     int64_t ldv, const float* __restrict__ dout, int64_t lddo, const float* __restrict__ stats,
     const float* __restrict__ dsum, float* __restrict__ dk, int64_t lddk, float* __restrict__ dv, int64_t lddv,
     const uint8_t* __restrict__ key_valid, int H, int L, int causal, float scale, float p_drop, uint64_t seed,
-    const uint8_t* __restrict__ drop_mask) {
+    const uint8_t* __restrict__ drop_mask, const float* __restrict__ o, int64_t ldo, float* __restrict__ ds_out) {
     constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int Lp = res_rows(L);
@@ -923,9 +926,28 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
         const bool ok = i < L;
         mx_s[i] = ok ? stats[((int64_t)bh * L + i) * 2] : 0.f;
         il_s[i] = ok ? stats[((int64_t)bh * L + i) * 2 + 1] : 0.f;
-        dsum_s[i] = ok ? dsum[(int64_t)bh * L + i] : 0.f;
+        if (!DS) dsum_s[i] = ok ? dsum[(int64_t)bh * L + i] : 0.f;
     }
     __syncthreads();
+    if (DS) {
+        // D_i = dO_i . O_i: 16 lanes per query row (a float4 of features each, dO from the LDS image)
+        for (int i = threadIdx.x >> 4; i < Lp; i += kResThreadsKV / 16) {
+            const int c = 4 * (threadIdx.x & 15);
+            float acc = 0.f;
+            if (i < L) {
+                for (int cc = c; cc < DK; cc += 64) {
+                    const float4 a = *reinterpret_cast<const float4*>(Ds + i * S + cc);
+                    const float4 bo = *reinterpret_cast<const float4*>(o + (tok0 + i) * ldo + h * DK + cc);
+                    acc += a.x * bo.x + a.y * bo.y + a.z * bo.z + a.w * bo.w;
+                }
+            }
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 16);
+            if ((threadIdx.x & 15) == 0) dsum_s[i] = acc;
+        }
+        __syncthreads();
+    }
+    float* ds_head = DS ? ds_out + (int64_t)bh * Lp * Lp : nullptr;
     const int last_valid = ctl[0];
     const bool any_valid = last_valid >= 0;
     const int ngroups = Lp / 16;
@@ -992,6 +1014,10 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
                         pd[sub][r] = pv;
                         ds[sub][r] = dsv;
                     }
+                    if (DS) {  // dS[query q4 + r][key kj]: 16 lanes of a group store 64 contiguous bytes per row
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) ds_head[(int64_t)(q4 + r) * Lp + kj] = ds[sub][r];
+                    }
                 }
                 cols_times_weights<DK, NS>(Ds + qb * S, g, c16, pd, dvt);  // dV^T += dO^T P
                 cols_times_weights<DK, NS>(Qs + qb * S, g, c16, ds, dkt);  // dK^T += Q^T dS
@@ -1014,7 +1040,117 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
     }
 }
 
-int g_attention_mode = 0;  // 0 auto, 1 streaming kernels only, 2 resident kernels when they fit
+// dQ = scale * dS K from the dS image attn_bwd_dkdv_res_kernel<DK, true> stored: one workgroup per (batch, head)
+// with K resident in LDS, waves claiming 16-query groups (most keys first under a causal mask).  Lane (g, c16) of
+// a group reads its query's dS row as float4s (keys 4g .. 4g+3 of each 16-key sub-tile: the weights
+// cols_times_weights takes), the next chunk's while the current chunk's MFMAs run.  Only key sub-tiles the dK/dV
+// pass formed are read: keys < min(last valid key + 1, q0 + 16) (causal) or < last valid key + 1.
+constexpr int kDsThreads = 512;
+
+template <int DK, int NT>
+__device__ __forceinline__ void load_one_resident(const float* __restrict__ a, int64_t lda, int L, int Lp,
+                                                  float* __restrict__ As) {
+    constexpr int C4 = DK / 4, S = DK + 4;
+    const int n4 = Lp * C4;
+    for (int base = threadIdx.x; base < n4; base += NT * 8) {
+        float4 ra[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int idx = base + u * NT, row = idx / C4, c = (idx % C4) * 4;
+            ra[u] = (idx < n4 && row < L) ? *reinterpret_cast<const float4*>(a + (int64_t)row * lda + c)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int idx = base + u * NT, row = idx / C4, c = (idx % C4) * 4;
+            if (idx < n4) *reinterpret_cast<float4*>(As + row * S + c) = ra[u];
+        }
+    }
+}
+
+template <int DK>
+__global__ __launch_bounds__(kDsThreads) void attn_bwd_dq_ds_kernel(const float* __restrict__ k, int64_t ldk,
+                                                                    const float* __restrict__ ds,
+                                                                    float* __restrict__ dq, int64_t lddq,
+                                                                    const uint8_t* __restrict__ key_valid, int H,
+                                                                    int L, int causal, float scale) {
+    constexpr int NCT = DK / 16, S = DK + 4;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int Lp = res_rows(L);
+    float* Ks = lds;
+    uint32_t* kvw = reinterpret_cast<uint32_t*>(Ks + Lp * S);
+    int* ctl = reinterpret_cast<int*>(kvw + (Lp + 31) / 32);
+
+    const int bh = blockIdx.x, b = bh / H, h = bh % H;
+    const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+    const int64_t tok0 = (int64_t)b * L;
+
+    stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
+    load_one_resident<DK, kDsThreads>(k + tok0 * ldk + h * DK, ldk, L, Lp, Ks);
+    __syncthreads();
+    const int last_valid = ctl[0];
+    const bool any_valid = last_valid >= 0;
+    const int kend = any_valid ? last_valid + 1 : L;
+    const int ngroups = Lp / 16;
+    const float* ds_head = ds + (int64_t)bh * Lp * Lp;
+
+    for (;;) {
+        const int gi = claim_group(ctl, lane);
+        if (gi >= ngroups) break;
+        const int q0 = (causal ? ngroups - 1 - gi : gi) * 16;
+        const int qi = q0 + c16;
+        const int kmax = (causal && any_valid) ? min(kend, q0 + 16) : kend;
+        const int nsub = (kmax + 15) / 16;
+        const float* wrow = ds_head + (int64_t)qi * Lp + 4 * g;
+        floatx4 acc[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+        float4 cur[kNS], nxt[kNS];
+        auto fetch = [&](int c, float4 (&dst)[kNS]) {
+#pragma unroll
+            for (int sub = 0; sub < kNS; ++sub)
+                dst[sub] = c + sub < nsub ? *reinterpret_cast<const float4*>(wrow + (c + sub) * 16)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        };
+        fetch(0, cur);
+        int c0 = 0;
+        for (; c0 + kNS <= nsub; c0 += kNS) {
+            if (c0 + kNS < nsub) fetch(c0 + kNS, nxt);
+            float w[kNS][4];
+#pragma unroll
+            for (int sub = 0; sub < kNS; ++sub) {
+                w[sub][0] = cur[sub].x;
+                w[sub][1] = cur[sub].y;
+                w[sub][2] = cur[sub].z;
+                w[sub][3] = cur[sub].w;
+            }
+            cols_times_weights<DK, kNS>(Ks + c0 * 16 * S, g, c16, w, acc);
+#pragma unroll
+            for (int sub = 0; sub < kNS; ++sub) cur[sub] = nxt[sub];
+        }
+#pragma unroll
+        for (int sub = 0; sub < kNS - 1; ++sub) {
+            if (c0 + sub < nsub) {
+                float w1[1][4] = {{cur[sub].x, cur[sub].y, cur[sub].z, cur[sub].w}};
+                cols_times_weights<DK, 1>(Ks + (c0 + sub) * 16 * S, g, c16, w1, acc);
+            }
+        }
+        if (qi < L) {
+            float* row = dq + (tok0 + qi) * lddq + h * DK;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+                *reinterpret_cast<float4*>(row + ct * 16 + 4 * g) =
+                    make_float4(acc[ct][0] * scale, acc[ct][1] * scale, acc[ct][2] * scale, acc[ct][3] * scale);
+        }
+    }
+}
+
+inline size_t ds_lds_bytes(int L, int DK) {
+    const size_t Lp = (size_t)res_rows(L);
+    return Lp * (DK + 4) * sizeof(float) + (Lp + 31) / 32 * 4 + 16;
+}
+
+int g_attention_mode = 0;  // 0 auto, 1 streaming kernels only, 2 resident kernels with the recomputing dQ pass
 
 template <class K>
 bool res_prepare(K kernel, size_t lds) {
@@ -1060,13 +1196,23 @@ ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, 
     ASME_LAUNCH_CHECK("asme_attention_fwd");
 }
 
+// workspace of asme_attention_bwd: D_i (batch*heads*seq_len floats), then (256-B aligned) the dS image of the
+// resident path ((batch*heads) x Lp x Lp floats, Lp = seq_len rounded up to 16)
+ASME_API int64_t asme_attention_bwd_workspace(int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim) {
+    (void)head_dim;
+    const int64_t Lp = res_rows((int)seq_len);
+    return ((batch * heads * seq_len * 4 + 255) & ~(int64_t)255) + batch * heads * Lp * Lp * 4;
+}
+
 ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k,
                                 int64_t ld_v, const float* out, int64_t ld_out, const float* dout, int64_t ld_dout,
                                 const float* lse, const uint8_t* key_valid, int64_t batch, int64_t heads,
                                 int64_t seq_len, int64_t head_dim, int causal, float scale, float p_drop,
-                                uint64_t seed, const uint8_t* drop_mask, float* dsum_ws, float* dq, int64_t ld_dq,
+                                uint64_t seed, const uint8_t* drop_mask, float* workspace, float* dq, int64_t ld_dq,
                                 float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream) {
-    ASME_CHECK_ARG(q && k && v && out && dout && lse && dsum_ws && dq && dk && dv, "asme_attention_bwd: null pointer");
+    ASME_CHECK_ARG(q && k && v && out && dout && lse && workspace && dq && dk && dv, "asme_attention_bwd: null pointer");
+    float* dsum_ws = workspace;
+    float* ds_ws = workspace + ((batch * heads * seq_len * 4 + 255) & ~(int64_t)255) / 4;
     ASME_CHECK_ARG(seq_len >= 1 && seq_len <= kMaxL, "asme_attention_bwd: seq_len must be in [1, 1024]");
     ASME_CHECK_ARG(aligned16(dq, ld_dq) && aligned16(dk, ld_dk) && aligned16(dv, ld_dv) && aligned16(q, ld_q) &&
                        aligned16(k, ld_k) && aligned16(v, ld_v) && aligned16(out, ld_out) &&
@@ -1078,16 +1224,26 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
     const dim3 rgrid((unsigned)(batch * heads));
     const size_t lds_dq = res_lds_bytes((int)seq_len, (int)head_dim, false);
     const size_t lds_kv = res_lds_bytes((int)seq_len, (int)head_dim, true);
+    const size_t lds_ds = ds_lds_bytes((int)seq_len, (int)head_dim);
     ASME_DK_DISPATCH(
         head_dim,
-        if (g_attention_mode != 1 && res_prepare(attn_bwd_dq_res_kernel<DK>, lds_dq) &&
-            res_prepare(attn_bwd_dkdv_res_kernel<DK>, lds_kv)) {
+        if (g_attention_mode == 0 && res_prepare(attn_bwd_dkdv_res_kernel<DK, true>, lds_kv) &&
+            res_prepare(attn_bwd_dq_ds_kernel<DK>, lds_ds)) {
+            // dK/dV first (it stores dS), then dQ = dS K: five products instead of seven
+            hipLaunchKernelGGL((attn_bwd_dkdv_res_kernel<DK, true>), rgrid, dim3(kResThreadsKV), lds_kv, s, q, k, v,
+                               ld_q, ld_k, ld_v, dout, ld_dout, lse, dsum_ws, dk, ld_dk, dv, ld_dv, key_valid,
+                               (int)heads, (int)seq_len, causal, scale, p_drop, seed, drop_mask, out, ld_out, ds_ws);
+            hipLaunchKernelGGL(attn_bwd_dq_ds_kernel<DK>, rgrid, dim3(kDsThreads), lds_ds, s, k, ld_k, ds_ws, dq, ld_dq,
+                               key_valid, (int)heads, (int)seq_len, causal, scale);
+        } else if (g_attention_mode != 1 && res_prepare(attn_bwd_dq_res_kernel<DK>, lds_dq) &&
+                   res_prepare(attn_bwd_dkdv_res_kernel<DK, false>, lds_kv)) {
             hipLaunchKernelGGL(attn_bwd_dq_res_kernel<DK>, rgrid, dim3(kResThreads), lds_dq, s, q, k, v, ld_q, ld_k,
                                ld_v, out, ld_out, dout, ld_dout, lse, dsum_ws, dq, ld_dq, key_valid, (int)heads,
                                (int)seq_len, causal, scale, p_drop, seed, drop_mask);
-            hipLaunchKernelGGL(attn_bwd_dkdv_res_kernel<DK>, rgrid, dim3(kResThreadsKV), lds_kv, s, q, k, v, ld_q, ld_k,
-                               ld_v, dout, ld_dout, lse, dsum_ws, dk, ld_dk, dv, ld_dv, key_valid, (int)heads,
-                               (int)seq_len, causal, scale, p_drop, seed, drop_mask);
+            hipLaunchKernelGGL((attn_bwd_dkdv_res_kernel<DK, false>), rgrid, dim3(kResThreadsKV), lds_kv, s, q, k, v,
+                               ld_q, ld_k, ld_v, dout, ld_dout, lse, dsum_ws, dk, ld_dk, dv, ld_dv, key_valid,
+                               (int)heads, (int)seq_len, causal, scale, p_drop, seed, drop_mask, out, ld_out,
+                               nullptr);
         } else {
         hipLaunchKernelGGL(attn_bwd_dq_kernel<DK>, grid, dim3(256), 0, s, q, k, v, ld_q, ld_k, ld_v, out, ld_out, dout,
                            ld_dout, lse, dsum_ws, dq, ld_dq, key_valid, (int)heads, (int)seq_len, causal, scale,
@@ -1104,8 +1260,9 @@ ASME_API int64_t asme_attention_dropout_mask_bytes(int64_t batch, int64_t heads,
     return mask_total_bytes(batch * heads, (int)seq_len);
 }
 
-// 0 = automatic (resident kernels whenever the head's operands fit LDS), 1 = streaming kernels only,
-// 2 = same as 0 (kept distinct for tests).  Returns the previous mode.
+// 0 = automatic (resident kernels whenever the head's operands fit LDS; backward: dK/dV storing dS, then dQ = dS K),
+// 1 = streaming kernels only, 2 = resident kernels with the backward's dQ pass recomputing S and dP (the round-2
+// path, kept for same-process A/B timing).  Returns the previous mode.
 ASME_API int asme_attention_set_mode(int mode) {
     const int prev = g_attention_mode;
     g_attention_mode = mode;

@@ -1067,6 +1067,10 @@ def _mask_bytes(batch: int, heads: int, seq_len: int) -> int:
     return int(_lib.load().asme_attention_dropout_mask_bytes(batch, heads, seq_len))
 
 
+def _attn_bwd_ws_bytes(batch: int, heads: int, seq_len: int, head_dim: int) -> int:
+    return int(_lib.load().asme_attention_bwd_workspace(batch, heads, seq_len, head_dim))
+
+
 class _AttentionFn(torch.autograd.Function):
     """Attention.forward (transformer_layers.py:138-155) on a fused (B, L, 3*H*dk) QKV tensor.
     key_valid (B, L) uint8; causal selects SASRec's tril mask (sequence_representation.py:34-48)."""
@@ -1098,11 +1102,11 @@ class _AttentionFn(torch.autograd.Function):
         dk = Dm // heads
         dout = _f32(dout)
         dqkv = torch.empty_like(qkv)
-        dsum = torch.empty(B * heads * L, device=qkv.device, dtype=torch.float32)
+        ws = torch.empty((_attn_bwd_ws_bytes(B, heads, L, dk) + 3) // 4, device=qkv.device, dtype=torch.float32)
         base, gb = qkv.data_ptr(), dqkv.data_ptr()
         call("asme_attention_bwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(out), Dm,
              ptr(dout), Dm, ptr(lse), ptr(key_valid), B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(mask),
-             ptr(dsum), gb, three_d, gb + 4 * Dm, three_d, gb + 8 * Dm, three_d, stream())
+             ptr(ws), gb, three_d, gb + 4 * Dm, three_d, gb + 8 * Dm, three_d, stream())
         return dqkv, None, None, None, None
 
 

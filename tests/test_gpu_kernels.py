@@ -27,7 +27,7 @@ def _attn_ref(q, k, v, valid, causal):
     return torch.matmul(F.softmax(s, -1), v)
 
 
-@pytest.fixture(params=[0, 1], ids=["auto", "streaming"])
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "streaming", "recompute"])
 def attn_mode(request, asme):
     prev = asme._lib.load().asme_attention_set_mode(request.param)
     yield request.param
@@ -91,10 +91,10 @@ def test_attention_dropout_mask_matches_regeneration(asme, dev, causal, attn_mod
     grads = []
     for m in (mask, None):
         g = torch.zeros_like(qkv)
-        dsum = torch.empty(B * H * L, device=dev)
+        ws = torch.empty(asme.ops._attn_bwd_ws_bytes(B, H, L, dk) // 4 + 1, device=dev)
         gb = g.data_ptr()
         call("asme_attention_bwd", b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(out), D, ptr(dout), D,
-             ptr(stats), ptr(valid), B, H, L, dk, int(causal), scale, 0.25, seed, ptr(m), ptr(dsum), gb, 3 * D,
+             ptr(stats), ptr(valid), B, H, L, dk, int(causal), scale, 0.25, seed, ptr(m), ptr(ws), gb, 3 * D,
              gb + 4 * D, 3 * D, gb + 8 * D, 3 * D, st())
         grads.append(g)
     torch.cuda.synchronize()
@@ -111,7 +111,7 @@ def test_attention_resident_matches_streaming_with_dropout(asme, dev, causal):
     g = torch.randn(B, L, H * dk, device=dev)
     lib = asme._lib.load()
     res = []
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         prev = lib.asme_attention_set_mode(mode)
         x = qkv.clone().requires_grad_(True)
         torch.manual_seed(11)
@@ -119,8 +119,9 @@ def test_attention_resident_matches_streaming_with_dropout(asme, dev, causal):
         out.backward(g)
         lib.asme_attention_set_mode(prev)
         res.append((out.detach(), x.grad))
-    assert _rel(res[0][0], res[1][0]) < 1e-5
-    assert _rel(res[0][1], res[1][1]) < 1e-4
+    for other in res[1:]:
+        assert _rel(res[0][0], other[0]) < 1e-5
+        assert _rel(res[0][1], other[1]) < 1e-4
 
 
 @pytest.mark.parametrize("D", [16, 32, 64, 128, 200])
