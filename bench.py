@@ -29,7 +29,7 @@ PEAK_FP32_MFMA_TFS = 157.3  # dense fp32 MFMA spec
 # ceiling is the dense bf16 MFMA peak (2516.6 TF/s = 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz) over 6
 PEAK_BF16X6_TFS = 2516.6 / 6
 BF16X6_KERNELS = {"asme_ws_linear", "asme_linear_weight_grad", "asme_linear_xent_fwd", "asme_linear_xent_bwd",
-                  "asme_logits"}
+                  "asme_linear_xent_fwd_dh", "asme_linear_xent_bwd_dw", "asme_logits"}
 
 
 def instrumented_steps(steps):
@@ -348,7 +348,8 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
     torch.cuda.synchronize()
     timer = asme._lib.KernelTimer(["asme_attention_fwd", "asme_attention_bwd", "asme_ws_linear",
                                    "asme_linear_weight_grad", "asme_cross_entropy_fwd", "asme_cross_entropy_bwd",
-                                   "asme_linear_xent_fwd", "asme_linear_xent_bwd", "asme_cloze_mask",
+                                   "asme_linear_xent_fwd", "asme_linear_xent_bwd", "asme_linear_xent_fwd_dh",
+                                   "asme_linear_xent_bwd_dw", "asme_cloze_mask",
                                    "asme_residual_ln_fwd", "asme_residual_ln_bwd", "asme_embedding_fwd",
                                    "asme_embedding_bwd"])
     if world > 1:
@@ -371,6 +372,9 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
     work = {"asme_attention_fwd": ("mfma", 4.0 * pairs * dk), "asme_attention_bwd": ("mfma", 10.0 * pairs * dk),
             **gemm_work(T, d, ffn),
             "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
+            # training form: the forward computes the logits and dH (both algorithmic), the backward dW (its logits
+            # recompute is not counted)
+            "asme_linear_xent_fwd_dh": ("mfma", 4.0 * M * V * d), "asme_linear_xent_bwd_dw": ("mfma", 2.0 * M * V * d),
             "asme_cross_entropy_fwd": ("hbm", M * V * 4.0), "asme_cross_entropy_bwd": ("hbm", 2 * M * V * 4.0),
             "asme_residual_ln_fwd": ("hbm", 4 * T * d * 4 + T * 8),
             "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),

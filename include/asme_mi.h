@@ -182,6 +182,18 @@ int asme_linear_xent_bwd(const float* H, int64_t ld_h, int64_t n, int64_t dim, c
                          const float* bias, const int64_t* targets, int64_t ignore_index, const float* lse,
                          const float* stats, const float* dloss, float* dH, float* dW, float* db, float* workspace,
                          int64_t ws_bytes, void* stream);
+/* Training form of the fused CE head (the logits recomputed once instead of twice): the forward also returns
+ * dh_raw (n x dim, row stride ld_dh) = softmax(H W^T + b) W - W[t] per valid row, 0 for ignored rows -- dH before
+ * the upstream scale; the backward scales it (dH = dh_raw * dloss[0] / out[1]) and runs the dW / db pass. */
+int64_t asme_linear_xent_fwd_dh_workspace(int64_t n, int64_t V, int64_t dim);
+int asme_linear_xent_fwd_dh(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
+                            int64_t V, const float* bias, const int64_t* targets, int64_t ignore_index, float* lse,
+                            float* dh_raw, int64_t ld_dh, float* workspace, int64_t ws_bytes, float* out, void* stream);
+int64_t asme_linear_xent_bwd_dw_workspace(int64_t n, int64_t V, int64_t dim);
+int asme_linear_xent_bwd_dw(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
+                            int64_t V, const float* bias, const int64_t* targets, int64_t ignore_index,
+                            const float* lse, const float* stats, const float* dloss, const float* dh_raw, float* dH,
+                            float* dW, float* db, float* workspace, int64_t ws_bytes, void* stream);
 /* Materialised full-catalogue scores (evaluation / predict_step: layers.py:105-109,138-143,
  * sasrec/components.py:46-61): out (n x V, row stride ld_out) = H (n x dim) W^T (V x dim) + bias (nullable),
  * same products as the fused head.  Workspace (bytes) from asme_logits_workspace. */

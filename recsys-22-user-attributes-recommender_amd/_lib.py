@@ -50,6 +50,10 @@ SIGNATURES = {
     "asme_linear_xent_fwd": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, p, i64, p, p],
     "asme_linear_xent_bwd_workspace": [i64, i64, i64],
     "asme_linear_xent_bwd": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, p, p, p, p, p, p, i64, p],
+    "asme_linear_xent_fwd_dh_workspace": [i64, i64, i64],
+    "asme_linear_xent_fwd_dh": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, p, i64, p, i64, p, p],
+    "asme_linear_xent_bwd_dw_workspace": [i64, i64, i64],
+    "asme_linear_xent_bwd_dw": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, p, p, p, p, p, p, p, i64, p],
     "asme_logits_workspace": [i64, i64, i64],
     "asme_logits": [p, i64, i64, i64, p, i64, i64, p, p, i64, p, i64, p],
     "asme_catalog_topk_workspace": [i64, i64, i64],
@@ -106,7 +110,8 @@ _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes"
              "asme_attention_dropout_mask_bytes": ctypes.c_int64,
              "asme_attention_bwd_workspace": ctypes.c_int64,
              "asme_catalog_topk_workspace": ctypes.c_int64, "asme_linear_xent_fwd_workspace": ctypes.c_int64,
-             "asme_linear_xent_bwd_workspace": ctypes.c_int64, "asme_logits_workspace": ctypes.c_int64, "asme_bucket_by_owner_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
+             "asme_linear_xent_bwd_workspace": ctypes.c_int64,
+             "asme_linear_xent_fwd_dh_workspace": ctypes.c_int64, "asme_linear_xent_bwd_dw_workspace": ctypes.c_int64, "asme_logits_workspace": ctypes.c_int64, "asme_bucket_by_owner_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
              "asme_table_grad_workspace": ctypes.c_int64}
 
 _lib: Optional[ctypes.CDLL] = None

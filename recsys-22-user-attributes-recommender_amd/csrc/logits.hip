@@ -29,8 +29,12 @@
 //   dH      stationary = queries, streamed = items: P = exp(s + b - lse) - onehot; dH^T += W^T P^T
 //   dW, db  stationary = items, streamed = queries: P^T the same way;            dW^T += H^T P
 //   logits  stationary = queries, streamed = items: out = s + b
-// Work: 2 (stats) + 4 (dH) + 4 (dW) n|V|d FLOP executed for the 6 of a materialised head; HBM bytes O((n+V)d).
-// Partial slabs of the chunks are summed in a fixed order: deterministic.
+//   fdh     stationary = queries, streamed = items: the training forward with dH folded in -- online (max, sum exp)
+//           per query per chunk and U^T += W^T exp(s + b - running max), rescaled when the running max grows (the
+//           flash-attention forward with the item table as V); a finish pass merges the chunks into lse, the loss
+//           and dH_raw = softmax(s) W - W[t] (0 for ignored rows), and the backward only scales it (x dloss / count)
+// Work: training runs fdh (4 n|V|d FLOP) + dW (4) = 8 n|V|d executed for the 6 of a materialised head (stats + dH +
+// dW: 10); HBM bytes O((n+V)d).  Partial slabs of the chunks are summed in a fixed order: deterministic.
 #include "common.h"
 #include <algorithm>
 
@@ -52,11 +56,11 @@ constexpr int kTS = 64;                  // streamed rows per LDS tile
 // MFMAs fill this wave's softmax VALU) where the pass fits that budget (stats, logits); W = 4 (one wave per SIMD,
 // 512 registers) for the gradient passes, whose stationary fragments + 128-feature accumulators need more
 constexpr int kRowPad = 256;             // plane rows are padded to a multiple of this (>= 32 W, kTS)
-template <int MODE> struct EngineWaves { static constexpr int W = (MODE == 1 || MODE == 2) ? 4 : 8; };
+template <int MODE> struct EngineWaves { static constexpr int W = (MODE == 1 || MODE == 2 || MODE == 4) ? 4 : 8; };
 constexpr int kPlaneTile = kTS * kRowB;  // 16 KiB: one plane of one tile
 constexpr int kTile = 3 * kPlaneTile;    // 48 KiB
 
-enum { M_STATS = 0, M_DH = 1, M_DW = 2, M_LOGITS = 3 };
+enum { M_STATS = 0, M_DH = 1, M_DW = 2, M_LOGITS = 3, M_FDH = 4 };
 
 __host__ __device__ constexpr int64_t pad_rows(int64_t r) { return (r + kRowPad - 1) / kRowPad * kRowPad; }
 
@@ -125,6 +129,7 @@ struct LogitsArgs {
     float* part2;            // stats: target logits [n]; dW: db partials (nchunks, V) or db (nullable)
     float* out;              // logits: (n, ld_out)
     int64_t ld_out;
+    float* upart;            // fdh: (nchunks, n, d) unnormalised softmax-weighted item rows per chunk
 };
 
 __device__ __forceinline__ bool valid_target(int64_t t, int64_t ignore, int64_t V) {
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
     // stationary-row metadata
     float s_lse = 0.f, s_bias = 0.f;
     int s_tgt = -1;
-    if (MODE == M_DH || MODE == M_STATS) {
+    if (MODE == M_DH || MODE == M_STATS || MODE == M_FDH) {
         const int64_t tg = srow < a.n_stat ? a.targets[srow] : -1;
         const bool ok = srow < a.n_stat && valid_target(tg, a.ignore, a.V);
         s_tgt = ok ? (int)tg : -1;
@@ -309,7 +314,53 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
                 }
             }
         };
-        if constexpr (MODE == M_DH || MODE == M_DW) {
+        if constexpr (MODE == M_FDH) {
+            floatx16 xs[2] = {score(0), score(1)};
+            float tmax = -INFINITY;
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    xs[sub][i] += tf[32 * sub + acc_row(i, h)];
+                    tmax = fmaxf(tmax, xs[sub][i]);
+                }
+                const int rel = s_tgt - (int)(r0 + 32 * sub);  // target in this sub-tile and lane half?
+                if ((unsigned)rel < 32u && ((rel >> 2) & 1) == h) {
+                    const int ri = (rel & 3) + 4 * (rel >> 3);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (i == ri) t_logit = xs[sub][i];
+                    have_t = true;
+                }
+            }
+            // one running max per query over both lane halves: both halves' P feed the same accumulators
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+            const float nm = fmaxf(run_max, tmax);
+            const float base = nm == -INFINITY ? 0.f : nm;  // nothing finite yet: P = 0, no NaN
+            const float alpha = run_max == -INFINITY ? 0.f : __expf(run_max - nm);
+#pragma unroll
+            for (int f = 0; f < NFT; ++f)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) y[f][i] *= alpha;
+            run_sum *= alpha;
+            run_max = nm;
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    xs[sub][i] = __expf(xs[sub][i] - base);
+                    run_sum += xs[sub][i];
+                }
+                Bf3 P[2];
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+                    P[s2] = split_bf3(
+                        make_float4(xs[sub][8 * s2], xs[sub][8 * s2 + 1], xs[sub][8 * s2 + 2], xs[sub][8 * s2 + 3]),
+                        make_float4(xs[sub][8 * s2 + 4], xs[sub][8 * s2 + 5], xs[sub][8 * s2 + 6],
+                                    xs[sub][8 * s2 + 7]));
+                grad(sub, P);
+            }
+        } else if constexpr (MODE == M_DH || MODE == M_DW) {
 #if ASME_LOGITS_PIPE
             // one wave per SIMD: software-pipeline the tile's two sub-tiles so the softmax VALU of one runs in the
             // MFMA shadow of the other's products: [S0] [P0 | S1] [G0 | P1] [G1], interleaved by the scheduler
@@ -395,6 +446,27 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
     }
 
     if (MODE == M_LOGITS) return;
+    if (MODE == M_FDH) {
+        run_sum += __shfl_xor(run_sum, 32, 64);  // (the halves share the running max)
+        if (srow < a.n_stat) {
+            if (h == 0) {
+                a.part[((int64_t)chunk_id * a.n_stat + srow) * 2] = run_max;
+                a.part[((int64_t)chunk_id * a.n_stat + srow) * 2 + 1] = run_sum;
+            }
+            if (have_t) a.part2[srow] = t_logit;
+            float* dst = a.upart + ((int64_t)chunk_id * a.n_stat + srow) * a.d;
+#pragma unroll
+            for (int ft = 0; ft < NFT; ++ft)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int f = 32 * ft + 8 * u + 4 * h;
+                    if (f < a.d)
+                        *reinterpret_cast<float4*>(dst + f) =
+                            make_float4(y[ft][4 * u], y[ft][4 * u + 1], y[ft][4 * u + 2], y[ft][4 * u + 3]);
+                }
+        }
+        return;
+    }
     if (MODE == M_STATS) {
         // merge the two lane halves of each query (each holds its own streamed rows)
         const float m2 = __shfl_xor(run_max, 32, 64), s2 = __shfl_xor(run_sum, 32, 64);
@@ -524,6 +596,84 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict_
     }
 }
 
+// fdh finish: one wave per query (lane c holds chunk c's (max, sum); chunks <= 64): lse, the query's loss term into
+// its block's (loss, count) pair (fixed-order tree, then lce_finish_kernel), and
+// dH_raw[q] = sum_c e^(m_c - M) U_c[q] / S - W[t_q]  (0 for an ignored or padding row)
+constexpr int kFdhWaves = 4;
+__global__ __launch_bounds__(kFdhWaves * 64) void fdh_finish_kernel(
+    const float* __restrict__ part, const float* __restrict__ upart, int64_t n, int nchunks, int d,
+    const int64_t* __restrict__ targets, int64_t ignore, int64_t V, const float* __restrict__ tlogit,
+    const float* __restrict__ W, int64_t ld_w, float* __restrict__ lse, float* __restrict__ dh_raw, int64_t ld_dh,
+    float* __restrict__ bsum) {
+    __shared__ float sa[kFdhWaves], sc[kFdhWaves];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * kFdhWaves + wave;
+    float acc_loss = 0.f, cnt = 0.f;
+    if (q < n) {
+        const float mc = lane < nchunks ? part[((int64_t)lane * n + q) * 2] : -INFINITY;
+        const float scv = lane < nchunks ? part[((int64_t)lane * n + q) * 2 + 1] : 0.f;
+        float M = mc;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+        const float w = (mc == -INFINITY || M == -INFINITY) ? 0.f : __expf(mc - M);
+        float S = scv * w;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) S += __shfl_xor(S, o, 64);
+        const float l = M + logf(S);
+        const int64_t tg = targets[q];
+        const bool ok = valid_target(tg, ignore, V);
+        if (lane == 0) {
+            lse[q] = l;
+            if (ok) {
+                acc_loss = l - tlogit[q];
+                cnt = 1.f;
+            }
+        }
+        const float inv = 1.f / S;
+        for (int f = 2 * lane; f < d; f += 128) {
+            float2 u = make_float2(0.f, 0.f);
+            for (int c = 0; c < nchunks; ++c) {
+                const float wc = __shfl(w, c, 64);
+                const float2 v = *reinterpret_cast<const float2*>(upart + ((int64_t)c * n + q) * d + f);
+                u.x += wc * v.x;
+                u.y += wc * v.y;
+            }
+            float2 r = make_float2(0.f, 0.f);
+            if (ok) {
+                const float2 wt = *reinterpret_cast<const float2*>(W + tg * ld_w + f);
+                r = make_float2(u.x * inv - wt.x, u.y * inv - wt.y);
+            }
+            *reinterpret_cast<float2*>(dh_raw + q * ld_dh + f) = r;
+        }
+    }
+    if (lane == 0) {
+        sa[wave] = acc_loss;
+        sc[wave] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a0 = 0.f, c0 = 0.f;
+#pragma unroll
+        for (int k = 0; k < kFdhWaves; ++k) {
+            a0 += sa[k];
+            c0 += sc[k];
+        }
+        bsum[2 * blockIdx.x] = a0;
+        bsum[2 * blockIdx.x + 1] = c0;
+    }
+}
+
+// dH = dH_raw * dloss[0] / stats[1] (the mean's upstream gradient over the valid-row count)
+__global__ __launch_bounds__(256) void scale_rows_kernel(const float* __restrict__ src, int64_t count,
+                                                         const float* __restrict__ dloss, const float* __restrict__ stats,
+                                                         float* __restrict__ dst) {
+    const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i4 >= count) return;
+    const float sc = dloss[0] / stats[1];
+    const float4 v = *reinterpret_cast<const float4*>(src + i4);
+    *reinterpret_cast<float4*>(dst + i4) = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+}
+
 // ------------------------------------------------------------------------------------------------ host
 constexpr size_t kSmem = 2 * kTile + 2 * kTS * 8;
 
@@ -534,7 +684,7 @@ struct Plan {
     int nchunks;
 };
 template <int MODE>
-Plan make_plan(int64_t n_stat, int64_t n_strm, int cus) {
+Plan make_plan(int64_t n_stat, int64_t n_strm, int cus, int64_t chunk_cap = 64) {
     Plan p;
     p.stat_pad = pad_rows(std::max<int64_t>(n_stat, 1));
     p.strm_pad = pad_rows(std::max<int64_t>(n_strm, 1));
@@ -543,7 +693,7 @@ Plan make_plan(int64_t n_stat, int64_t n_strm, int cus) {
     // one workgroup per CU at a time (96 KiB of LDS): pick the chunk count whose grid fills its last round best
     // (the workgroups of a round take about equally long), preferring multiples of 8 (a chunk per XCD, its tiles
     // shared in that XCD's L2) at equal fill; chunks of at least 4 tiles
-    const int64_t max_chunks = std::max<int64_t>(1, std::min<int64_t>(tiles / 4, 64));
+    const int64_t max_chunks = std::max<int64_t>(1, std::min<int64_t>(tiles / 4, chunk_cap));
     double best = -1.0;
     p.chunk = tiles * kTS;
     for (int64_t want = 1; want <= max_chunks; ++want) {
@@ -753,6 +903,144 @@ ASME_API int asme_linear_xent_bwd(const float* H, int64_t ld_h, int64_t n, int64
         if (db) sum(db_part, V, pw.nchunks, V, db);
     }
     ASME_LAUNCH_CHECK("asme_linear_xent_bwd");
+}
+
+// ------------------------------------------------- fused CE with dH in the forward (training), dW in the backward
+// fdh's per-chunk U slabs cost 2 n d 4 B each (written, then merged): at most kFdhChunks chunks
+constexpr int64_t kFdhChunks = 8;
+
+ASME_API int64_t asme_linear_xent_fwd_dh_workspace(int64_t n, int64_t V, int64_t dim) {
+    const Plan p = make_plan<M_FDH>(n, V, device_cus(), kFdhChunks);
+    const int64_t nb = (n + kFdhWaves - 1) / kFdhWaves;
+    return align256(planes_bytes(n)) + align256(planes_bytes(V)) + align256(p.nchunks * n * 2 * 4) + align256(n * 4) +
+           align256(p.nchunks * n * dim * 4) + align256(nb * 2 * 4 + 8);
+}
+
+// The training forward: lse (n), out = {mean loss over the valid rows, their count}, and dh_raw (n x dim, row
+// stride ld_dh) = softmax(H W^T + b) W - W[t] per valid row (0 for ignored rows): dH before the upstream scale,
+// which asme_linear_xent_bwd_dw applies.  H (n x dim), W (V x dim), dim <= 128.
+ASME_API int asme_linear_xent_fwd_dh(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
+                                     int64_t V, const float* bias, const int64_t* targets, int64_t ignore_index,
+                                     float* lse, float* dh_raw, int64_t ld_dh, float* workspace, int64_t ws_bytes,
+                                     float* out, void* stream) {
+    ASME_CHECK_ARG(H && W && targets && lse && dh_raw && workspace && out, "asme_linear_xent_fwd_dh: null pointer");
+    ASME_CHECK_ARG(dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && ld_w % 4 == 0 && ld_dh % 2 == 0 &&
+                       ld_dh >= dim && aligned16(H) && aligned16(W),
+                   "asme_linear_xent_fwd_dh: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    ASME_CHECK_ARG(n >= 0 && V >= 1 && V < (1LL << 31), "asme_linear_xent_fwd_dh: bad shape");
+    ASME_CHECK_ARG(ws_bytes >= asme_linear_xent_fwd_dh_workspace(n, V, dim),
+                   "asme_linear_xent_fwd_dh: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const Plan p = make_plan<M_FDH>(n, V, device_cus(), kFdhChunks);
+    char* w = reinterpret_cast<char*>(workspace);
+    __bf16* hp = reinterpret_cast<__bf16*>(w);
+    __bf16* wp = reinterpret_cast<__bf16*>(w + align256(planes_bytes(n)));
+    float* part = reinterpret_cast<float*>(w + align256(planes_bytes(n)) + align256(planes_bytes(V)));
+    float* tlogit = part + align256(p.nchunks * n * 2 * 4) / 4;
+    float* upart = tlogit + align256(n * 4) / 4;
+    float* bsum = upart + align256(p.nchunks * n * dim * 4) / 4;
+    const int64_t nb = (n + kFdhWaves - 1) / kFdhWaves;
+    if (n > 0) {
+        int rc = split(H, ld_h, n, (int)dim, hp, s);
+        if (rc == 0) rc = split(W, ld_w, V, (int)dim, wp, s);
+        if (rc != 0) return rc;
+        LogitsArgs a{};
+        a.stat = hp;
+        a.strm = wp;
+        a.stat_pad = p.stat_pad;
+        a.strm_pad = p.strm_pad;
+        a.n_stat = n;
+        a.n_strm = V;
+        a.chunk = p.chunk;
+        a.nchunks = p.nchunks;
+        a.d = (int)dim;
+        a.bias = bias;
+        a.targets = targets;
+        a.ignore = ignore_index;
+        a.V = V;
+        a.part = part;
+        a.part2 = tlogit;
+        a.upart = upart;
+        rc = launch_kb<M_FDH>(a, p.sblocks, s);
+        if (rc != 0) return rc;
+        hipLaunchKernelGGL(fdh_finish_kernel, dim3((unsigned)nb), dim3(kFdhWaves * 64), 0, s, part, upart, n,
+                           p.nchunks, (int)dim, targets, ignore_index, V, tlogit, W, ld_w, lse, dh_raw, ld_dh, bsum);
+    }
+    hipLaunchKernelGGL(lce_finish_kernel, dim3(1), dim3(1024), 0, s, bsum, nb, out);
+    ASME_LAUNCH_CHECK("asme_linear_xent_fwd_dh");
+}
+
+ASME_API int64_t asme_linear_xent_bwd_dw_workspace(int64_t n, int64_t V, int64_t dim) {
+    const Plan pw = make_plan<M_DW>(V, n, device_cus());
+    const int64_t dw = pw.nchunks > 1 ? pw.nchunks * V * (dim + 1) : 0;
+    return align256(planes_bytes(n)) + align256(planes_bytes(V)) + align256(dw * 4);
+}
+
+// The backward of asme_linear_xent_fwd_dh: dH (n x dim, contiguous) = dh_raw * dloss[0] / stats[1]; dW (V x dim),
+// db (V, nullable) from the dW pass (the logits recomputed once).  dH, dW, db are overwritten.
+ASME_API int asme_linear_xent_bwd_dw(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W,
+                                     int64_t ld_w, int64_t V, const float* bias, const int64_t* targets,
+                                     int64_t ignore_index, const float* lse, const float* stats, const float* dloss,
+                                     const float* dh_raw, float* dH, float* dW, float* db, float* workspace,
+                                     int64_t ws_bytes, void* stream) {
+    ASME_CHECK_ARG(H && W && targets && lse && stats && dloss && dh_raw && dH && dW,
+                   "asme_linear_xent_bwd_dw: null pointer");
+    ASME_CHECK_ARG(dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && ld_w % 4 == 0 && aligned16(H) &&
+                       aligned16(W) && aligned16(dH) && aligned16(dW) && aligned16(dh_raw),
+                   "asme_linear_xent_bwd_dw: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    ASME_CHECK_ARG(V >= 1 && V < (1LL << 31), "asme_linear_xent_bwd_dw: bad shape");
+    ASME_CHECK_ARG(ws_bytes >= asme_linear_xent_bwd_dw_workspace(n, V, dim),
+                   "asme_linear_xent_bwd_dw: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (hipMemsetAsync(dW, 0, V * dim * sizeof(float), s) != hipSuccess ||
+            (db && hipMemsetAsync(db, 0, V * sizeof(float), s) != hipSuccess))
+            return hip_status(hipGetLastError(), "asme_linear_xent_bwd_dw");
+        return 0;
+    }
+    const int64_t cnt = n * dim;
+    hipLaunchKernelGGL(scale_rows_kernel, dim3((unsigned)((cnt / 4 + 255) / 256)), dim3(256), 0, s, dh_raw, cnt, dloss,
+                       stats, dH);
+    const Plan pw = make_plan<M_DW>(V, n, device_cus());
+    char* w = reinterpret_cast<char*>(workspace);
+    __bf16* hp = reinterpret_cast<__bf16*>(w);
+    __bf16* wp = reinterpret_cast<__bf16*>(w + align256(planes_bytes(n)));
+    float* dw_part = reinterpret_cast<float*>(w + align256(planes_bytes(n)) + align256(planes_bytes(V)));
+    float* db_part = dw_part + (pw.nchunks > 1 ? pw.nchunks * V * dim : 0);
+    int rc = split(H, ld_h, n, (int)dim, hp, s);
+    if (rc == 0) rc = split(W, ld_w, V, (int)dim, wp, s);
+    if (rc != 0) return rc;
+    LogitsArgs a{};
+    a.d = (int)dim;
+    a.bias = bias;
+    a.targets = targets;
+    a.ignore = ignore_index;
+    a.V = V;
+    a.lse = lse;
+    a.dloss = dloss;
+    a.stats = stats;
+    a.stat = wp;
+    a.strm = hp;
+    a.stat_pad = pw.stat_pad;
+    a.strm_pad = pw.strm_pad;
+    a.n_stat = V;
+    a.n_strm = n;
+    a.chunk = pw.chunk;
+    a.nchunks = pw.nchunks;
+    a.part = pw.nchunks > 1 ? dw_part : dW;
+    a.part2 = pw.nchunks > 1 ? (db ? db_part : nullptr) : db;
+    rc = launch_kb<M_DW>(a, pw.sblocks, s);
+    if (rc != 0) return rc;
+    if (pw.nchunks > 1) {
+        auto sum = [&](const float* part, int64_t stride, int64_t nparts, int64_t count, float* out) {
+            const int64_t thr = (count + 3) / 4;
+            hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, part, stride,
+                               (int)nparts, count, out);
+        };
+        sum(dw_part, V * dim, pw.nchunks, V * dim, dW);
+        if (db) sum(db_part, V, pw.nchunks, V, db);
+    }
+    ASME_LAUNCH_CHECK("asme_linear_xent_bwd_dw");
 }
 
 // ------------------------------------------------------------------------------------ materialised scores

@@ -1285,6 +1285,11 @@ def logits(hidden, weight, bias=None):
     return linear(hidden, weight, bias)
 
 
+# the fused CE head's training form (dH accumulated in the forward pass, asme_linear_xent_fwd_dh / _bwd_dw); False
+# runs the two-pass backward (asme_linear_xent_bwd), kept for same-process A/B timing (tools/xent_bench.py) and tests
+XENT_TRAINING_FORM = True
+
+
 class _LinearXentFn(torch.autograd.Function):
     """CrossEntropyLoss(ignore_index)(H W^T + b, targets), mean over non-ignored rows, without the (n, |V|)
     logits (csrc/logits.hip; layers.py:105-109,138-143 + losses.py:77-115)."""
@@ -1298,31 +1303,49 @@ class _LinearXentFn(torch.autograd.Function):
         if t.numel() != n:
             raise ValueError(f"hidden rows ({n}) and targets ({t.numel()}) differ")
         lib = _lib.load()
-        ws = torch.empty(max(4, int(lib.asme_linear_xent_fwd_workspace(n, V, d)) // 4 + 1), device=h.device,
-                         dtype=torch.float32)
         lse = torch.empty(n, device=h.device, dtype=torch.float32)
         out = torch.empty(2, device=h.device, dtype=torch.float32)
-        call("asme_linear_xent_fwd", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
-             ignore_index, ptr(lse), ptr(ws), ws.numel() * 4, ptr(out), stream())
-        ctx.save_for_backward(h, weight, bias, t, lse, out)
+        dh_raw = None
+        if ctx.needs_input_grad[0] and XENT_TRAINING_FORM:
+            # training: dH (before the upstream scale) is accumulated in the same pass as the softmax statistics
+            # (asme_linear_xent_fwd_dh), so the backward recomputes the logits once, for dW only
+            ws = torch.empty(max(4, int(lib.asme_linear_xent_fwd_dh_workspace(n, V, d)) // 4 + 1), device=h.device,
+                             dtype=torch.float32)
+            dh_raw = torch.empty(n, d, device=h.device, dtype=torch.float32)
+            call("asme_linear_xent_fwd_dh", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
+                 ignore_index, ptr(lse), ptr(dh_raw), d, ptr(ws), ws.numel() * 4, ptr(out), stream())
+        else:
+            ws = torch.empty(max(4, int(lib.asme_linear_xent_fwd_workspace(n, V, d)) // 4 + 1), device=h.device,
+                             dtype=torch.float32)
+            call("asme_linear_xent_fwd", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
+                 ignore_index, ptr(lse), ptr(ws), ws.numel() * 4, ptr(out), stream())
+        ctx.save_for_backward(h, weight, bias, t, lse, out, dh_raw)
         ctx.meta = (ignore_index, hidden.shape)
         return out[0]
 
     @staticmethod
     def backward(ctx, dloss):
-        h, weight, bias, t, lse, out = ctx.saved_tensors
+        h, weight, bias, t, lse, out, dh_raw = ctx.saved_tensors
         ignore_index, shape = ctx.meta
         n, d = h.shape
         V = weight.shape[0]
         lib = _lib.load()
-        ws = torch.empty(max(4, int(lib.asme_linear_xent_bwd_workspace(n, V, d)) // 4 + 1), device=h.device,
-                         dtype=torch.float32)
         dh = torch.empty_like(h)
         dw = torch.empty(V, d, device=h.device, dtype=torch.float32)
         db = torch.empty(V, device=h.device, dtype=torch.float32) if bias is not None else None
         dl = _f32(dloss.reshape(1))
-        call("asme_linear_xent_bwd", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
-             ignore_index, ptr(lse), ptr(out), ptr(dl), ptr(dh), ptr(dw), ptr(db), ptr(ws), ws.numel() * 4, stream())
+        if dh_raw is not None:
+            ws = torch.empty(max(4, int(lib.asme_linear_xent_bwd_dw_workspace(n, V, d)) // 4 + 1), device=h.device,
+                             dtype=torch.float32)
+            call("asme_linear_xent_bwd_dw", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
+                 ignore_index, ptr(lse), ptr(out), ptr(dl), ptr(dh_raw), ptr(dh), ptr(dw), ptr(db), ptr(ws),
+                 ws.numel() * 4, stream())
+        else:
+            ws = torch.empty(max(4, int(lib.asme_linear_xent_bwd_workspace(n, V, d)) // 4 + 1), device=h.device,
+                             dtype=torch.float32)
+            call("asme_linear_xent_bwd", ptr(h), d, n, d, ptr(weight), weight.stride(0), V, ptr(bias), ptr(t),
+                 ignore_index, ptr(lse), ptr(out), ptr(dl), ptr(dh), ptr(dw), ptr(db), ptr(ws), ws.numel() * 4,
+                 stream())
         return dh.view(shape), dw, db, None, None
 
 

@@ -105,3 +105,25 @@ def test_linear_xent_vs_materialised_kernels(asme, dev):
     assert abs(l1.item() - l2.item()) / abs(l2.item()) < 1e-5
     for a, c in zip(p1, p2):
         assert _rel(a.grad, c.grad) < 1e-4
+
+
+@pytest.mark.parametrize("h_grad", [True, False])
+def test_linear_xent_training_and_weight_only_paths(asme, dev, h_grad):
+    """hidden requiring grad takes the training form (dH folded into the forward, asme_linear_xent_fwd_dh +
+    asme_linear_xent_bwd_dw); a frozen hidden takes the two-pass backward (asme_linear_xent_bwd): both match fp64,
+    with a dloss other than 1 (the upstream scale is applied in the backward)"""
+    torch.manual_seed(5)
+    n, V, d = 1500, 9001, 128
+    h, W, b = torch.randn(n, d) * 0.4, torch.randn(V, d) * 0.4, torch.randn(V) * 0.2
+    t = torch.randint(0, V, (n,))
+    t[::7] = 0
+    hc, Wc, bc = h.double().requires_grad_(h_grad), W.double().requires_grad_(True), b.double().requires_grad_(True)
+    (3.5 * F.cross_entropy(F.linear(hc, Wc, bc), t, ignore_index=0)).backward()
+    hd, Wd, bd = h.to(dev).requires_grad_(h_grad), W.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+    (3.5 * asme.ops.linear_cross_entropy(hd, Wd, bd, t.to(dev), 0)).backward()
+    if h_grad:
+        assert _rel(hd.grad, hc.grad) < 1e-4
+    else:
+        assert hd.grad is None
+    assert _rel(Wd.grad, Wc.grad) < 1e-4
+    assert _rel(bd.grad, bc.grad) < 1e-4

@@ -45,14 +45,15 @@ MAP = [
     (r"ws_gemm_kernel", "asme_ws_linear", True),
     # the fused logits + CE head (csrc/logits.hip): the engine's mode names the call; the operand splits that open
     # a call are attributed to the call of the engine launch that follows them (see per_call)
+    # (api None: the kernel belongs to the logits call that launched the previous mapped kernel)
     (r"logits_engine_kernel<0", "asme_linear_xent_fwd", True),
-    (r"lce_rows_kernel", "asme_linear_xent_fwd", False),
-    (r"lce_finish_kernel", "asme_linear_xent_fwd", False),
+    (r"logits_engine_kernel<4", "asme_linear_xent_fwd_dh", True),
     (r"logits_engine_kernel<1", "asme_linear_xent_bwd", True),
-    (r"logits_engine_kernel<2", "asme_linear_xent_bwd", False),
-    (r"sum_parts_kernel", "asme_linear_xent_bwd", False),
+    (r"scale_rows_kernel", "asme_linear_xent_bwd_dw", True),
+    (r"logits_engine_kernel<2", None, False),
+    (r"(lce_rows|lce_finish|fdh_finish|sum_parts)_kernel", None, False),
 ]
-PENDING = r"split_planes_kernel"  # belongs to the next logits call
+PENDING = r"split_planes_kernel"  # belongs to the next mapped logits kernel's call
 # calls whose launches have different shapes (the bench's work figure is their mean): mean, not median
 MEAN = {"asme_ws_linear", "asme_linear_weight_grad"}
 
@@ -70,18 +71,23 @@ def per_call(rows, scale):
     calls = collections.defaultdict(list)
     cur = {}
     pending = 0.0
+    last = None
     for _, name, b in rows:
         if re.search(PENDING, name):
             pending += b * scale
             continue
         for rx, api, counts in MAP:
             if re.search(rx, name):
+                if api is None:
+                    if last is None:
+                        break
+                    api = last
                 if counts or api not in cur:
                     calls[api].append(0.0)
                     cur[api] = True
-                calls[api][-1] += b * scale + (pending if counts else 0.0)
-                if counts:
-                    pending = 0.0
+                calls[api][-1] += b * scale + pending
+                pending = 0.0
+                last = api
                 break
     return calls
 
