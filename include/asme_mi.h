@@ -277,10 +277,19 @@ int asme_last_item_mask(const int64_t* items, const int64_t* lengths, int64_t ba
                         void* stream);
 
 /* ---- id dedup & shard bucketing (row-sharded item table) ------------------------ */
+/* ids (n) -> unique (capacity n) in first-occurrence order, inverse (n, nullable: slot per occurrence, -1 for an id
+ * outside [0, vocab)), count (1 int32 on the device; no host sync).  map: vocab int32, all -1 at rest; the call
+ * leaves map[unique[s]] = first occurrence of unique[s] -- asme_dedup_reset restores it.  Three launches.
+ * _segments: the occurrences are nseg (1..4) id arrays read in place (host arrays of pointers / lengths). */
 int64_t asme_dedup_workspace_bytes(int64_t n);
 int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_t* map, void* workspace,
                    int64_t workspace_bytes, int64_t* unique, int64_t* inverse, int32_t* count, void* stream);
+int asme_dedup_ids_segments(int nseg, const int64_t* const* seg_ids, const int64_t* seg_n, int64_t vocab, int32_t* map,
+                            void* workspace, int64_t workspace_bytes, int64_t* unique, int64_t* inverse,
+                            int32_t* count, void* stream);
 int asme_dedup_reset(const int64_t* unique, const int32_t* count, int64_t cap, int32_t* map, void* stream);
+/* rewrite the dedup's map to map[unique[s]] = s (a row -> slot table for asme_adam_rows_step) */
+int asme_dedup_map_slots(const int64_t* unique, const int32_t* count, int64_t cap, int32_t* map, void* stream);
 int asme_owner_histogram(const int64_t* unique, const int32_t* count, int64_t cap, int world, int32_t* owner,
                          int32_t* counts, void* stream);
 /* stable grouping of n unique ids by owner (id % world, world <= 64): order[j] = index of the j-th id sent,

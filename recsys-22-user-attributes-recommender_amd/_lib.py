@@ -94,7 +94,9 @@ SIGNATURES = {
     "asme_linear_weight_grad": [p, i64, p, i64, i64, i64, i64, p, i64, p, p, i32, p],
     "asme_dedup_workspace_bytes": [i64],
     "asme_dedup_ids": [p, i64, i64, p, p, i64, p, p, p, p],
+    "asme_dedup_ids_segments": [i32, p, p, i64, p, p, i64, p, p, p, p],
     "asme_dedup_reset": [p, p, i64, p, p],
+    "asme_dedup_map_slots": [p, p, i64, p, p],
     "asme_owner_histogram": [p, p, i64, i32, p, p, p],
     "asme_bucket_by_owner_workspace": [i64, i32],
     "asme_bucket_by_owner": [p, i64, p, i32, p, i64, p, p, p, p, p],

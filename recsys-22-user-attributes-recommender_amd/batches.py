@@ -83,6 +83,7 @@ class PositiveNegativeSamplerProcessor:
             raise ValueError("at most 8 special token ids")
         self._specials = specials
         self._special_dev: Dict[torch.device, torch.Tensor] = {}
+        self._err_dev: Dict[torch.device, torch.Tensor] = {}
 
     def process_batch(self, store: SessionStore, batch_idx: torch.Tensor, max_seq_length: int,
                       seed: Optional[int] = None) -> Dict[str, torch.Tensor]:
@@ -95,7 +96,11 @@ class PositiveNegativeSamplerProcessor:
         pos = torch.empty_like(x)
         neg = torch.empty_like(x)
         lengths = torch.empty(B, device=dev, dtype=torch.int64)
-        err = torch.zeros(1, device=dev, dtype=torch.int32)
+        # error bits are sticky (a set bit is an error check_errors raises on): one zeroed flag per device, no
+        # zero-fill launch per batch
+        err = self._err_dev.get(dev)
+        if err is None:
+            err = self._err_dev[dev] = torch.zeros(1, device=dev, dtype=torch.int32)
         seed = new_seed(1.0) if seed is None else int(seed)
         call("asme_posneg_sample", ptr(store.flat), ptr(store.offsets), store.n_sessions, ptr(idx), B, L,
              len(self.tokenizer), ptr(self._special_dev[dev]), len(self._specials), self.tokenizer.pad_token_id,
@@ -108,6 +113,8 @@ class PositiveNegativeSamplerProcessor:
         """raise like the reference would (AssertionError for a 1-item session, multinomial failure when no
         id is admissible); syncs the device"""
         e = int(self._err.item()) if getattr(self, "_err", None) is not None else 0
+        if e:
+            self._err.zero_()  # reported once (the flag is shared by the batches of this device)
         if e & 2:
             raise AssertionError("a session of length 1 reached the positive/negative sampler")
         if e & 1:

@@ -6,11 +6,9 @@
 // it runs nn.Embedding with a dense gradient under Lightning DDP.
 //
 // Dedup is deterministic: a |V|-sized int32 map (all -1 at rest) gets atomicMin(i) per occurrence,
-// so each distinct id's representative is its FIRST occurrence; a device exclusive scan over the
-// representative flags assigns compact slots in first-occurrence order.  The map is then rewritten
-// to hold the slot (row_slot for the Adam kernel) and must be reset with asme_dedup_reset.
-#include <hipcub/hipcub.hpp>
-
+// so each distinct id's representative is its FIRST occurrence; ranking the representatives (wave ballots per
+// block, the block counts scanned by the last block to finish) assigns compact slots in first-occurrence order.
+// The map keeps the first occurrences and must be reset with asme_dedup_reset.
 #include "adam_math.h"
 #include "common.h"
 
@@ -45,47 +43,139 @@ __device__ __forceinline__ int hash_insert(BlockHash& t, int32_t key) {  // key 
     }
 }
 
-__global__ __launch_bounds__(256) void claim_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V,
-                                                    int32_t* __restrict__ map) {
+// Cross-workgroup hand-off inside one launch without an L2 writeback: the published values are stored with
+// device-coherent (agent-scope atomic) stores, the storing wave waits for them (vmcnt(0)) before it takes the ticket,
+// and the last workgroup reads them with device-coherent loads.  (__threadfence() here wrote back every dirty L2 line
+// of the XCD once per workgroup: 76 us for the 600 blocks of a 614k-id dedup.)
+__device__ __forceinline__ void publish_i32(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t coherent_i32(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool last_arrival(int32_t* ticket, int64_t arrivals) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's published stores have completed
+    return __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int32_t)(arrivals - 1);
+}
+
+// The id list of one dedup: up to kMaxSegs segments read in place (the step's input, positive and negative id
+// tensors: no concatenated copy), occurrence i = flat position over the segments.
+constexpr int kMaxSegs = 4;
+struct IdSegs {
+    const int64_t* p[kMaxSegs];
+    int64_t start[kMaxSegs + 1];
+    int n;
+};
+__device__ __forceinline__ int64_t seg_id(const IdSegs& S, int64_t i) {
+    const int64_t* p = S.p[0];
+    int64_t o = i;
+#pragma unroll
+    for (int q = 1; q < kMaxSegs; ++q)  // constant indices: the table stays in SGPRs
+        if (q < S.n && i >= S.start[q]) {
+            p = S.p[q];
+            o = i - S.start[q];
+        }
+    return p[o];
+}
+
+// (1) map[id] = min occurrence index (its first occurrence); block 0 also zeroes the slot-scan ticket of (2)
+__global__ __launch_bounds__(256) void claim_kernel(IdSegs S, int64_t n, int64_t V, int32_t* __restrict__ map,
+                                                    int32_t* __restrict__ ticket) {
     __shared__ BlockHash t;
     hash_init(t, INT32_MAX);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t id = i < n ? ids[i] : -1;
+    const int64_t id = i < n ? seg_id(S, i) : -1;
     if (id >= 0 && id < V) atomicMin(&t.val[hash_insert(t, (int32_t)id)], (int32_t)i);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0;
     __syncthreads();
     for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x)
         if (t.key[j] >= 0) atomicMin(reinterpret_cast<unsigned int*>(map + t.key[j]), (unsigned int)t.val[j]);
 }
 
-__global__ void flag_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V, const int32_t* __restrict__ map,
-                            int32_t* __restrict__ flags) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t id = ids[i];
-    flags[i] = (id >= 0 && id < V && map[id] == (int32_t)i) ? 1 : 0;
-}
-
-// compaction, and the map rewritten to slots on the way (map[unique[s]] = s): each distinct id is written by its
-// one representative occurrence, and nothing reads the map between the flag pass and the inverse pass
-__global__ void compact_kernel(const int64_t* __restrict__ ids, int64_t n, const int32_t* __restrict__ flags,
-                               const int32_t* __restrict__ scan, int64_t* __restrict__ unique,
-                               int32_t* __restrict__ count, int32_t* __restrict__ map) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (flags[i]) {
-        const int64_t id = ids[i];
-        unique[scan[i]] = id;
-        map[id] = scan[i];
+// (2) slots in first-occurrence order without a library scan: a block of kDedupBk occurrences ranks its
+// representatives (map[id] == i) by wave ballots -> lpre[i] (rank within the block) and bcnt[b]; the last block to
+// finish (ticket, no waiting) scans bcnt in place into block offsets and writes the count.  slot(r) = bcnt[r / kDedupBk]
+// + lpre[r] for a representative r.
+constexpr int kDedupBk = 1024;
+__global__ __launch_bounds__(256) void dedup_rank_kernel(IdSegs S, int64_t n, int64_t V,
+                                                         const int32_t* __restrict__ map, int32_t* __restrict__ lpre,
+                                                         int32_t* __restrict__ bcnt, int32_t* __restrict__ ticket,
+                                                         int32_t* __restrict__ count) {
+    __shared__ int32_t wsum[4];
+    __shared__ int last;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int64_t b0 = (int64_t)blockIdx.x * kDedupBk;
+    int32_t base = 0;
+    for (int r = 0; r < kDedupBk / 256; ++r) {
+        const int64_t i = b0 + r * 256 + threadIdx.x;
+        bool rep = false;
+        if (i < n) {
+            const int64_t id = seg_id(S, i);
+            rep = id >= 0 && id < V && map[id] == (int32_t)i;
+        }
+        const uint64_t m = __ballot(rep);
+        if (lane == 0) wsum[wave] = __popcll(m);
+        __syncthreads();
+        int32_t pre = base;
+        for (int w = 0; w < wave; ++w) pre += wsum[w];
+        if (rep) lpre[i] = pre + __popcll(m & lt);
+        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
     }
-    if (i == n - 1) *count = scan[i] + flags[i];
+    if (threadIdx.x == 0) {
+        publish_i32(bcnt + blockIdx.x, base);
+        last = last_arrival(ticket, gridDim.x);
+    }
+    __syncthreads();
+    if (!last) return;
+    // exclusive scan of bcnt[0, nb) by this block: 256-entry rounds, one wave-scan per wave + the wave carries
+    const int64_t nb = gridDim.x;
+    __shared__ int32_t wtot[4];
+    int32_t carry = 0;
+    for (int64_t c0 = 0; c0 < nb; c0 += 256) {
+        const int64_t b = c0 + threadIdx.x;
+        const int32_t v = b < nb ? coherent_i32(bcnt + b) : 0;
+        int32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wtot[wave] = x;
+        __syncthreads();
+        int32_t wpre = carry;
+        for (int w = 0; w < wave; ++w) wpre += wtot[w];
+        if (b < nb) bcnt[b] = wpre + x - v;
+        carry += wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *count = carry;
 }
 
-__global__ void inverse_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V, const int32_t* __restrict__ map,
-                               int64_t* __restrict__ inverse) {
+// (3) every occurrence's slot (inverse) through its representative r = map[id]; the representative writes unique
+__global__ __launch_bounds__(256) void dedup_slot_kernel(IdSegs S, int64_t n, int64_t V,
+                                                         const int32_t* __restrict__ map,
+                                                         const int32_t* __restrict__ lpre,
+                                                         const int32_t* __restrict__ boff, int64_t* __restrict__ unique,
+                                                         int64_t* __restrict__ inverse) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int64_t id = ids[i];
-    inverse[i] = (id >= 0 && id < V) ? (int64_t)map[id] : -1;
+    const int64_t id = seg_id(S, i);
+    int64_t slot = -1;
+    if (id >= 0 && id < V) {
+        const int32_t r = map[id];
+        slot = (int64_t)boff[r / kDedupBk] + lpre[r];
+        if (r == (int32_t)i) unique[slot] = id;
+    }
+    if (inverse) inverse[i] = slot;
+}
+
+__global__ void map_slots_kernel(const int64_t* __restrict__ unique, const int32_t* __restrict__ count,
+                                 int32_t* __restrict__ map, int64_t cap) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap || s >= *count) return;
+    map[unique[s]] = (int32_t)s;
 }
 
 __global__ void reset_kernel(const int64_t* __restrict__ unique, const int32_t* __restrict__ count,
@@ -219,37 +309,69 @@ __global__ void invert_perm_kernel(const int64_t* __restrict__ order, int64_t n,
 
 }  // namespace
 
+namespace {
+size_t ws_up(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
+
 ASME_API int64_t asme_dedup_workspace_bytes(int64_t n) {
-    size_t temp = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (int32_t*)nullptr, (int32_t*)nullptr, (int)n);
-    // flags + scan (int32 each) + cub temp, 256-B aligned pieces
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    return (int64_t)(2 * up((size_t)n * sizeof(int32_t)) + up(temp));
+    // per-occurrence rank within its block (int32), per-block counts / offsets, the scan ticket
+    const int64_t nb = (n + kDedupBk - 1) / kDedupBk;
+    return (int64_t)(ws_up((size_t)n * 4) + ws_up((size_t)(nb + 1) * 4));
 }
 
-// ids (n) -> unique (cap >= n) in first-occurrence order, inverse (n) slot per occurrence, count (1 int32 on device).
-// map: |V| int32, all -1 on entry; on exit map[unique[s]] = s (call asme_dedup_reset afterwards).
-ASME_API int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_t* map, void* workspace,
-                            int64_t workspace_bytes, int64_t* unique, int64_t* inverse, int32_t* count,
-                            void* stream) {
-    ASME_CHECK_ARG(ids && map && workspace && unique && count, "asme_dedup_ids: null pointer");
+// ids: nseg (1..4) segments seg_ids[q] of seg_n[q] ids (host arrays), occurrence i = flat position over them.
+// -> unique (cap >= n) in first-occurrence order, inverse (n, nullable) slot per occurrence (-1 for an id outside
+// [0, vocab)), count (1 int32 on the device).  map: |V| int32, all -1 on entry; on exit map[unique[s]] = the first
+// occurrence of unique[s] (call asme_dedup_reset afterwards).  Three launches, no library scan.
+ASME_API int asme_dedup_ids_segments(int nseg, const int64_t* const* seg_ids, const int64_t* seg_n, int64_t vocab,
+                                     int32_t* map, void* workspace, int64_t workspace_bytes, int64_t* unique,
+                                     int64_t* inverse, int32_t* count, void* stream) {
+    ASME_CHECK_ARG(nseg >= 1 && nseg <= kMaxSegs && seg_ids && seg_n, "asme_dedup_ids: 1..4 id segments");
+    IdSegs S{};
+    S.n = nseg;
+    int64_t n = 0;
+    for (int q = 0; q < nseg; ++q) {
+        ASME_CHECK_ARG(seg_n[q] >= 0 && (seg_ids[q] || seg_n[q] == 0), "asme_dedup_ids: bad segment");
+        S.p[q] = seg_ids[q];
+        S.start[q] = n;
+        n += seg_n[q];
+    }
+    for (int q = nseg; q <= kMaxSegs; ++q) S.start[q] = n;
+    ASME_CHECK_ARG(map && workspace && unique && count, "asme_dedup_ids: null pointer");
     ASME_CHECK_ARG(n >= 1 && n < (int64_t)1 << 31, "asme_dedup_ids: n must be in [1, 2^31)");
     ASME_CHECK_ARG(vocab >= 1 && vocab < (int64_t)1 << 31, "asme_dedup_ids: vocab must be in [1, 2^31)");
     ASME_CHECK_ARG(workspace_bytes >= asme_dedup_workspace_bytes(n), "asme_dedup_ids: workspace too small");
     hipStream_t s = (hipStream_t)stream;
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const int64_t nb = (n + kDedupBk - 1) / kDedupBk;
     char* ws = (char*)workspace;
-    int32_t* flags = (int32_t*)ws;
-    int32_t* scan = (int32_t*)(ws + up((size_t)n * 4));
-    void* temp = ws + 2 * up((size_t)n * 4);
-    size_t temp_bytes = (size_t)workspace_bytes - 2 * up((size_t)n * 4);
-    hipLaunchKernelGGL(claim_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, vocab, map);
-    hipLaunchKernelGGL(flag_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, vocab, map, flags);
-    if (hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, flags, scan, (int)n, s) != hipSuccess)
-        return hip_status(hipErrorUnknown, "asme_dedup_ids: scan");
-    hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, flags, scan, unique, count, map);
-    if (inverse) hipLaunchKernelGGL(inverse_kernel, dim3(nblk(n)), dim3(256), 0, s, ids, n, vocab, map, inverse);
+    int32_t* lpre = (int32_t*)ws;
+    int32_t* bcnt = (int32_t*)(ws + ws_up((size_t)n * 4));
+    int32_t* ticket = bcnt + nb;
+    hipLaunchKernelGGL(claim_kernel, dim3(nblk(n)), dim3(256), 0, s, S, n, vocab, map, ticket);
+    hipLaunchKernelGGL(dedup_rank_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, vocab, map, lpre, bcnt, ticket,
+                       count);
+    hipLaunchKernelGGL(dedup_slot_kernel, dim3(nblk(n)), dim3(256), 0, s, S, n, vocab, map, lpre, bcnt, unique,
+                       inverse);
     ASME_LAUNCH_CHECK("asme_dedup_ids");
+}
+
+ASME_API int asme_dedup_ids(const int64_t* ids, int64_t n, int64_t vocab, int32_t* map, void* workspace,
+                            int64_t workspace_bytes, int64_t* unique, int64_t* inverse, int32_t* count,
+                            void* stream) {
+    ASME_CHECK_ARG(ids, "asme_dedup_ids: null pointer");
+    const int64_t* segs[1] = {ids};
+    const int64_t ns[1] = {n};
+    return asme_dedup_ids_segments(1, segs, ns, vocab, map, workspace, workspace_bytes, unique, inverse, count,
+                                   stream);
+}
+
+// map[unique[s]] = s for s < *count: the dedup's map as a row -> slot table (asme_adam_rows_step's row_slot)
+ASME_API int asme_dedup_map_slots(const int64_t* unique, const int32_t* count, int64_t cap, int32_t* map,
+                                  void* stream) {
+    ASME_CHECK_ARG(unique && count && map, "asme_dedup_map_slots: null pointer");
+    if (cap == 0) return 0;
+    hipLaunchKernelGGL(map_slots_kernel, dim3(nblk(cap)), dim3(256), 0, (hipStream_t)stream, unique, count, map, cap);
+    ASME_LAUNCH_CHECK("asme_dedup_map_slots");
 }
 
 ASME_API int asme_dedup_reset(const int64_t* unique, const int32_t* count, int64_t cap, int32_t* map, void* stream) {
@@ -422,11 +544,11 @@ __global__ void csr_order_kernel(const int32_t* __restrict__ seg_off, int64_t n,
 }
 
 // long ranges: one workgroup each; an element's place is the number of smaller occurrence indices in its range
-__global__ __launch_bounds__(256) void csr_long_kernel(const int32_t* __restrict__ seg_off, int64_t n, int64_t cap,
-                                                       const int32_t* __restrict__ longs, int32_t* __restrict__ order,
-                                                       int32_t* __restrict__ tmp) {
+__device__ __forceinline__ void csr_long(const int32_t* __restrict__ seg_off, int64_t n, int64_t cap,
+                                         const int32_t* __restrict__ longs, int32_t* __restrict__ order,
+                                         int32_t* __restrict__ tmp, int blk, int nblocks) {
     const int nl = longs[0];
-    for (int t = blockIdx.x; t < nl; t += gridDim.x) {
+    for (int t = blk; t < nl; t += nblocks) {
         const int64_t k = longs[1 + t];
         const int32_t b = seg_off[k];
         const int len = (k < cap ? seg_off[k + 1] : (int32_t)n) - b;
@@ -453,41 +575,38 @@ __global__ __launch_bounds__(256) void csr_long_kernel(const int32_t* __restrict
 constexpr int kHugeOcc = 1024;  // occurrences per placement block (256 threads x 4 rounds)
 inline int64_t huge_blocks(int64_t n) { return (n + kHugeOcc - 1) / kHugeOcc; }
 
-__global__ __launch_bounds__(256) void csr_huge_count_kernel(const int64_t* __restrict__ inverse, int64_t n,
-                                                             int64_t cap, const int32_t* __restrict__ hidx,
-                                                             const int32_t* __restrict__ huge,
-                                                             const int32_t* __restrict__ hbeg,
-                                                             int32_t* __restrict__ cntm, int64_t nblk_h,
-                                                             int32_t* __restrict__ ticket) {
+__device__ __forceinline__ void csr_huge_count(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
+                                               const int32_t* __restrict__ hidx, const int32_t* __restrict__ huge,
+                                               const int32_t* __restrict__ hbeg, int32_t* __restrict__ cntm,
+                                               int64_t nblk_h, int32_t* __restrict__ ticket, int blk) {
     const int nh = min(*huge, kHugeFast);
     if (nh == 0) return;
     __shared__ int32_t c[kHugeFast];
     __shared__ int last;
     if (threadIdx.x < kHugeFast) c[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t b0 = (int64_t)blockIdx.x * kHugeOcc;
+    const int64_t b0 = (int64_t)blk * kHugeOcc;
     for (int r = 0; r < kHugeOcc / 256; ++r) {
         const int64_t i = b0 + r * 256 + threadIdx.x;
         const int j = i < n ? hidx[occ_key(inverse, i, cap)] : -1;
         if (j >= 0 && j < kHugeFast) atomicAdd(&c[j], 1);  // (counts only: order does not matter here)
     }
     __syncthreads();
-    if ((int)threadIdx.x < nh) cntm[(int64_t)threadIdx.x * nblk_h + blockIdx.x] = c[threadIdx.x];
+    if ((int)threadIdx.x < nh) publish_i32(cntm + (int64_t)threadIdx.x * nblk_h + blk, c[threadIdx.x]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // (7) by the last block to finish (a ticket, no waiting): per huge key, base[j][b] = hbeg[j] + its counts over
     // blocks < b, in place -- one wave per key, 64 blocks per wave-scan step
-    __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+    if (threadIdx.x == 0) last = last_arrival(ticket, nblk_h);
     __syncthreads();
     if (!last) return;
-    __threadfence();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int j = wave; j < nh; j += 4) {
         int32_t* row = cntm + (int64_t)j * nblk_h;
         int32_t carry = hbeg[j];
         for (int64_t c0 = 0; c0 < nblk_h; c0 += 64) {
             const int64_t b = c0 + lane;
-            const int32_t v = b < nblk_h ? __hip_atomic_load(row + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            const int32_t v = b < nblk_h ? coherent_i32(row + b) : 0;
             int32_t x = v;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -498,6 +617,23 @@ __global__ __launch_bounds__(256) void csr_huge_count_kernel(const int64_t* __re
             carry += __shfl(x, 63, 64);
         }
     }
+}
+
+// (5) and (6) in one launch: blocks [0, kLongBlocks) rank the long ranges, the rest count the huge keys
+constexpr int kLongBlocks = 64;
+__global__ __launch_bounds__(256) void csr_long_huge_kernel(const int64_t* __restrict__ inverse,
+                                                            const int32_t* __restrict__ seg_off, int64_t n,
+                                                            int64_t cap, const int32_t* __restrict__ longs,
+                                                            int32_t* __restrict__ order, int32_t* __restrict__ tmp,
+                                                            const int32_t* __restrict__ hidx,
+                                                            const int32_t* __restrict__ huge,
+                                                            const int32_t* __restrict__ hbeg,
+                                                            int32_t* __restrict__ cntm, int64_t nblk_h,
+                                                            int32_t* __restrict__ ticket) {
+    if (blockIdx.x < kLongBlocks)
+        csr_long(seg_off, n, cap, longs, order, tmp, blockIdx.x, kLongBlocks);
+    else
+        csr_huge_count(inverse, n, cap, hidx, huge, hbeg, cntm, nblk_h, ticket, blockIdx.x - kLongBlocks);
 }
 
 __global__ __launch_bounds__(256) void csr_huge_place_kernel(const int64_t* __restrict__ inverse, int64_t n,
@@ -540,6 +676,77 @@ __global__ __launch_bounds__(256) void csr_huge_place_kernel(const int64_t* __re
         __syncthreads();
     }
 }
+
+// Exclusive scan of in[0, n) -> out (single pass, decoupled look-back): a block takes the next tile index from a
+// counter (tiles start in index order, so every predecessor is resident or done), scans its kScanTile values, publishes
+// its total (status 1) and, once its predecessors' prefix is known from their published words, its inclusive prefix
+// (status 2).  Word of tile t = status << 32 | value, in `state` (1 + tiles 64-bit words, zeroed by the caller).
+constexpr int kScanTile = 1024;
+__global__ __launch_bounds__(256) void chained_scan_kernel(const int32_t* __restrict__ in, int64_t n,
+                                                           int32_t* __restrict__ out,
+                                                           unsigned long long* __restrict__ state) {
+    __shared__ int tile_s;
+    __shared__ int32_t wtot[4];
+    __shared__ int32_t prefix_s;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) tile_s = (int)atomicAdd(state, 1ull);
+    __syncthreads();
+    const int64_t tile = tile_s;
+    const int64_t i0 = tile * kScanTile + 4 * threadIdx.x;  // 4 consecutive values per thread
+    int32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = i0 + j < n ? in[i0 + j] : 0;
+    const int32_t tsum = v[0] + v[1] + v[2] + v[3];
+    int32_t x = tsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    int32_t wpre = 0;
+    for (int w = 0; w < wave; ++w) wpre += wtot[w];
+    const int32_t total = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    if (wave == 0) {
+        // the word carries its own value: relaxed device-coherent atomics, no fence.  Look-back 64 predecessors at a
+        // time (lane l: tile j - l), summing up to the nearest one with an inclusive prefix; a window with an
+        // unpublished tile before that one is read again.
+        unsigned long long* word = state + 1;
+        if (lane == 0 && tile > 0)
+            __hip_atomic_store(word + tile, (1ull << 32) | (uint32_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int32_t prefix = 0;
+        for (int64_t j = tile - 1; j >= 0;) {
+            const int64_t k = j - lane;
+            const unsigned long long w =
+                k >= 0 ? __hip_atomic_load(word + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 32);
+            const unsigned st = (unsigned)(w >> 32);
+            const uint64_t inc = __ballot(st == 2), zero = __ballot(st == 0);
+            const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;  // nearest inclusive predecessor
+            const uint64_t upto = first == 64 ? ~0ull : (first == 63 ? ~0ull : ((2ull << first) - 1));
+            if (zero & upto) continue;  // a tile before it has not published yet
+            int32_t v = lane <= first ? (int32_t)(uint32_t)w : 0;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            prefix += v;
+            if (first < 64) break;
+            j -= 64;
+        }
+        if (lane == 0) {
+            __hip_atomic_store(word + tile, (2ull << 32) | (uint32_t)(prefix + total), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            prefix_s = prefix;
+        }
+    }
+    __syncthreads();
+    int32_t run = prefix_s + wpre + x - tsum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (i0 + j < n) out[i0 + j] = run;
+        run += v[j];
+    }
+}
+inline int64_t scan_tiles(int64_t n) { return (n + kScanTile - 1) / kScanTile; }
 
 constexpr int kMaxContrib = 4;
 constexpr int kChunk = 32;  // occurrences per reduction group: bounds the serial work of any group
@@ -736,19 +943,15 @@ __global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restric
 
 namespace {
 size_t csr_up(size_t x) { return (x + 255) & ~(size_t)255; }
-size_t csr_temp_bytes(int64_t n) {
-    size_t scan = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (int32_t*)nullptr, (int32_t*)nullptr, (int)(n + 1));
-    return scan;
-}
 }  // namespace
 
 ASME_API int64_t asme_occurrence_csr_workspace(int64_t n) {
-    // per-key counts (n + 1), huge-range count + bounds + scan ticket (2 + 2 max_huge), long-range list (n + 2), rank / sort
-    // scratch (n), key -> huge index (n + 1), huge-key counts per placement block, scan temp
+    // per-key counts (n + 1), huge-range count + bounds + huge ticket (2 + 2 max_huge), the scan's tile counter and
+    // tile words (1 + tiles, 64-bit), long-range list (n + 2), rank / sort scratch (n), key -> huge index (n + 1),
+    // huge-key counts per placement block
     return (int64_t)(csr_up((size_t)(n + 1) * 4) + csr_up((size_t)(2 + 2 * max_huge(n)) * 4) +
-                     csr_up((size_t)(n + 2) * 4) + csr_up((size_t)n * 4) + csr_up((size_t)(n + 1) * 4) +
-                     csr_up((size_t)kHugeFast * huge_blocks(n) * 4) + csr_up(csr_temp_bytes(n)));
+                     csr_up((size_t)(1 + scan_tiles(n + 1)) * 8) + csr_up((size_t)(n + 2) * 4) +
+                     csr_up((size_t)n * 4) + csr_up((size_t)(n + 1) * 4) + csr_up((size_t)kHugeFast * huge_blocks(n) * 4));
 }
 
 // inverse (n int64 slots < cap <= n) -> order (n int32 occurrence indices grouped by slot, increasing within a
@@ -768,30 +971,30 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     int32_t* hbeg = huge + 1;
     int32_t* hend = hbeg + nh;
     int32_t* ticket = hend + nh;  // (zeroed with the counts)
-    int32_t* longs = (int32_t*)((char*)huge + csr_up((size_t)(2 + 2 * nh) * 4));
+    unsigned long long* scan_state = (unsigned long long*)((char*)huge + csr_up((size_t)(2 + 2 * nh) * 4));
+    int32_t* longs = (int32_t*)((char*)scan_state + csr_up((size_t)(1 + scan_tiles(cap + 1)) * 8));
     int32_t* tmp = (int32_t*)((char*)longs + csr_up((size_t)(n + 2) * 4));
     int32_t* hidx = (int32_t*)((char*)tmp + csr_up((size_t)n * 4));
     int32_t* cntm = (int32_t*)((char*)hidx + csr_up((size_t)(n + 1) * 4));
     const int64_t nblk_h = huge_blocks(n);
-    void* temp = (char*)cntm + csr_up((size_t)kHugeFast * nblk_h * 4);
-    size_t temp_bytes = (size_t)workspace_bytes - ((char*)temp - ws);
-    // counts of keys 0..cap, the huge-range count and bounds, the long-range counter: zeroed together (contiguous)
+    // counts of keys 0..cap, the huge-range count and bounds, the scan's tile words, the long-range counter: zeroed
+    // together (contiguous)
     if (hipMemsetAsync(cnt, 0, (char*)longs - ws + 4, s) != hipSuccess)
         return hip_status(hipGetLastError(), "asme_occurrence_csr: zero");
     hipLaunchKernelGGL(csr_count_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, cnt);
-    if (hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, cnt, seg_off, (int)(cap + 1), s) != hipSuccess)
-        return hip_status(hipErrorUnknown, "asme_occurrence_csr: scan");
+    hipLaunchKernelGGL(chained_scan_kernel, dim3((unsigned)scan_tiles(cap + 1)), dim3(256), 0, s, cnt, cap + 1, seg_off,
+                       scan_state);
     hipLaunchKernelGGL(csr_scatter_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, seg_off, cnt, order,
                        sorted_slot);
     hipLaunchKernelGGL(csr_order_kernel, dim3(nblk(cap + 1)), dim3(256), 0, s, seg_off, n, cap, order, longs, huge,
                        hbeg, hend, hidx);
-    hipLaunchKernelGGL(csr_long_kernel, dim3(64), dim3(256), 0, s, seg_off, n, cap, longs, order, tmp);
-    if (n > kLongSeg) {  // a huge range is possible: stable placement
-        hipLaunchKernelGGL(csr_huge_count_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
-                           hbeg, cntm, nblk_h, ticket);
+    // long ranges ranked and (a huge range is possible) huge keys counted in one launch, then the stable placement
+    const int64_t hblocks = n > kLongSeg ? nblk_h : 0;
+    hipLaunchKernelGGL(csr_long_huge_kernel, dim3((unsigned)(kLongBlocks + hblocks)), dim3(256), 0, s, inverse, seg_off,
+                       n, cap, longs, order, tmp, hidx, huge, hbeg, cntm, nblk_h, ticket);
+    if (n > kLongSeg)
         hipLaunchKernelGGL(csr_huge_place_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
                            cntm, nblk_h, order);
-    }
     ASME_LAUNCH_CHECK("asme_occurrence_csr");
 }
 

@@ -27,6 +27,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from . import modules as _modules
+
 
 def _staged(group, t: torch.Tensor) -> bool:
     return t.is_cuda and dist.get_backend(group) == "gloo"
@@ -194,7 +196,7 @@ def train_step(module, optimizer, scheduler, reducer: GradientAllReduce, batch, 
     slice, backward (gradient buckets all-reduce as they fill), averaged gradients, optimizer + scheduler step."""
     out = module.training_step(batch, batch_idx)
     loss = out["loss"]
-    loss.backward()
+    _modules.backward(loss)
     reducer.finish()
     optimizer.step()
     if scheduler is not None:

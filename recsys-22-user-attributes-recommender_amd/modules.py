@@ -19,7 +19,7 @@ Batch keys: item, item.target, positive_samples, negative_samples (data/datasets
 from __future__ import annotations
 
 import inspect
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -164,7 +164,8 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         meta["positive_samples"], meta["negative_samples"] = pos, neg
         self._plan_table([input_seq, pos, neg])
         pos_logits, neg_logits = self.model(InputSequence(input_seq, padding_mask, meta))
-        item_mask = input_seq.ne(self.item_tokenizer.pad_token_id)
+        # the loss mask is the padding mask of the (B, L) input (the reference recomputes input_seq != pad)
+        item_mask = padding_mask if input_seq.dim() == 2 else input_seq.ne(self.item_tokenizer.pad_token_id)
         loss = self.loss_function(pos_logits, neg_logits, mask=item_mask)
         self.log(LOG_KEY_TRAINING_LOSS, loss)
         return {"loss": loss}
@@ -477,11 +478,24 @@ def split_optimizers(configured):
     raise TypeError(f"unsupported optimizer configuration {type(configured)}")
 
 
+_ONES: Dict[Tuple[torch.device, torch.dtype], torch.Tensor] = {}
+
+
+def backward(loss: torch.Tensor):
+    """loss.backward() with a cached scalar 1 as the seed gradient (autograd's implicit torch.ones_like is a fill
+    launch per step)"""
+    key = (loss.device, loss.dtype)
+    one = _ONES.get(key)
+    if one is None:
+        one = _ONES[key] = torch.ones((), device=loss.device, dtype=loss.dtype)
+    loss.backward(one if loss.dim() == 0 else None)
+
+
 def train_step(module, optimizer, scheduler, batch, batch_idx: int = 0) -> torch.Tensor:
     """One optimisation step as Lightning's automatic optimisation runs it."""
     out = module.training_step(batch, batch_idx)
     loss = out["loss"]
-    loss.backward()
+    backward(loss)
     optimizer.step()
     if scheduler is not None:
         scheduler.step()

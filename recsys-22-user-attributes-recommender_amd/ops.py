@@ -157,8 +157,12 @@ class SparseTablePlan:
         tg = getattr(table, "_asme_table_grad", None) if table is not None else None
         if tg is not None:
             tg.drop_applied()  # the previous step's plan still marks the shared slot map
-        flat = torch.cat([_i64(x).reshape(-1) for x in id_sets])
-        n = flat.numel()
+        # the id sets are read in place as segments of one occurrence list (no concatenated copy)
+        segs = [_i64(x).reshape(-1) for x in id_sets]
+        segs = [x if x.is_contiguous() else x.contiguous() for x in segs]
+        if len(segs) > 4:
+            segs = [torch.cat(segs)]
+        n = sum(x.numel() for x in segs)
         self.vocab, self.dim = table.shape if table is not None else (vocab, dim)
         self.slot_map = slot_map
         self.unique = torch.empty(n, device=dev, dtype=torch.int64)
@@ -169,9 +173,12 @@ class SparseTablePlan:
         if n > 0:
             ws_bytes = int(_lib.load().asme_dedup_workspace_bytes(n))
             ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
-            call("asme_dedup_ids", ptr(flat), n, self.vocab, ptr(slot_map), ptr(ws), ws_bytes, ptr(self.unique),
-                 ptr(inverse), ptr(self.count), stream())
+            k = len(segs)
+            call("asme_dedup_ids_segments", k, (ctypes_vp * k)(*[x.data_ptr() for x in segs]),
+                 (ctypes_i64 * k)(*[x.numel() for x in segs]), self.vocab, ptr(slot_map), ptr(ws), ws_bytes,
+                 ptr(self.unique), ptr(inverse), ptr(self.count), stream())
         self.capacity = n
+        self._slots_mapped = False
         self.grad_scale = 1.0  # factor on every reduced gradient row (the sharded owner: 1/W, DDP averaging)
         self._grad_rows = None
         self._inverse = {}
@@ -222,6 +229,7 @@ class SparseTablePlan:
         self.unique = torch.arange(n_rows, device=dev, dtype=torch.int64)
         self.count = torch.full((1,), n_rows, device=dev, dtype=torch.int32)
         self.capacity = n
+        self._slots_mapped = True  # (no map: slot s == row s)
         self.grad_scale = 1.0
         self._grad_rows = None
         self._inverse, self._offset, self._contrib = {}, {}, []
@@ -336,6 +344,15 @@ class SparseTablePlan:
     def n_unique(self) -> int:
         """number of distinct ids (device -> host sync)"""
         return int(self.count.item())
+
+    def row_slot_map(self) -> torch.Tensor:
+        """the slot map as a row -> slot table (row r's gradient is grad_rows[map[r]], -1: none), rewritten from the
+        dedup's first-occurrence entries once (asme_dedup_map_slots)"""
+        if not self._slots_mapped:
+            call("asme_dedup_map_slots", ptr(self.unique), ptr(self.count), self.capacity, ptr(self.slot_map),
+                 stream())
+            self._slots_mapped = True
+        return self.slot_map
 
     def inverse_of(self, ids: torch.Tensor) -> torch.Tensor:
         key = (ids.data_ptr(), tuple(ids.shape))

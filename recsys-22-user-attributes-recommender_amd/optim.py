@@ -103,7 +103,7 @@ class FusedAdam(torch.optim.Optimizer):
                         tg.lazy.apply(plan, st["step"])
                     else:
                         call("asme_adam_rows_step", ptr(p), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), V, D,
-                             ptr(plan.slot_map), ptr(plan.grad_rows), lr, b1, b2, eps, wd, st["step"], stream())
+                             ptr(plan.row_slot_map()), ptr(plan.grad_rows), lr, b1, b2, eps, wd, st["step"], stream())
                     tg.applied = plan
                     tg.plan = None
                     continue

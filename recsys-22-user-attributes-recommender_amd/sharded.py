@@ -26,6 +26,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from . import modules as _modules
 from . import ops
 from .dataparallel import GradientAllReduce
 from .modules import (ITEM_SEQ_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME,
@@ -293,7 +294,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
             pos_logits, neg_logits = self.model(InputSequence(inv_seq, padding_mask, meta))
         finally:
             emb._table_override = None
-        loss = self.loss_function(pos_logits, neg_logits, mask=input_seq.ne(self.item_tokenizer.pad_token_id))
+        loss = self.loss_function(pos_logits, neg_logits, mask=padding_mask)
         self._pending = (st, own, compact, cplan)
         return {"loss": loss}
 
@@ -365,7 +366,7 @@ def train_step(module, optimizer, batch, batch_idx: int = 0, next_batch=None):
     if next_batch is not None:
         module.prefetch(next_batch)
     loss = out["loss"]
-    loss.backward()
+    _modules.backward(loss)
     module.after_backward()
     optimizer.step()
     optimizer.zero_grad(set_to_none=True)

@@ -1,6 +1,7 @@
 """Kernel-level GPU parity: each HIP kernel (through the C ABI) against a plain PyTorch fp32 reference
 of the same op computed on the CPU (the oracle's building blocks).  Index/mask work must be bit-exact;
 fp32 results within the stated tolerances."""
+import ctypes
 import math
 
 import numpy as np
@@ -287,6 +288,47 @@ def test_fused_adam_matches_oracle(asme, dev):
                  for (p, m, v), g in zip(state, grads)]
     for p, (pr, _, _) in zip(pd, state):
         assert _rel(p, pr) < 1e-5
+
+
+@pytest.mark.parametrize("sizes", [(1,), (1023, 1), (2049, 700, 3), (300000, 204800, 204800, 5)])
+def test_dedup_segments_first_occurrence_order(asme, dev, sizes):
+    """asme_dedup_ids_segments == numpy first-occurrence unique / inverse over the concatenated segments (hot keys,
+    ids outside the table, ragged segment sizes); the map is back to -1 after asme_dedup_reset"""
+    g = torch.Generator().manual_seed(sum(sizes))
+    V = 50_000
+    segs = []
+    for k in sizes:
+        x = torch.randint(0, V, (k,), generator=g)
+        x[::7] = 17  # a hot key
+        if k > 2:
+            x[1] = -5
+            x[2] = V + 3  # outside the table
+        segs.append(x)
+    flat = torch.cat(segs).numpy()
+    ok = (flat >= 0) & (flat < V)
+    _, first = np.unique(flat[ok], return_index=True)
+    uniq_ref = flat[ok][np.sort(first)]
+    slot_of = {int(v): i for i, v in enumerate(uniq_ref)}
+    inv_ref = np.array([slot_of.get(int(v), -1) if 0 <= v < V else -1 for v in flat])
+    L = asme._lib
+    n = flat.size
+    dsegs = [x.to(dev) for x in segs]
+    m = torch.full((V,), -1, dtype=torch.int32, device=dev)
+    ws_bytes = int(L.load().asme_dedup_workspace_bytes(n))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    uniq = torch.empty(n, dtype=torch.int64, device=dev)
+    inv = torch.empty(n, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    k = len(dsegs)
+    L.call("asme_dedup_ids_segments", k, (ctypes.c_void_p * k)(*[x.data_ptr() for x in dsegs]),
+           (ctypes.c_int64 * k)(*[x.numel() for x in dsegs]), V, L.ptr(m), L.ptr(ws), ws_bytes, L.ptr(uniq),
+           L.ptr(inv), L.ptr(cnt), L.stream())
+    c = int(cnt.item())
+    assert c == uniq_ref.size
+    assert np.array_equal(uniq[:c].cpu().numpy(), uniq_ref)
+    assert np.array_equal(inv.cpu().numpy(), inv_ref)
+    L.call("asme_dedup_reset", L.ptr(uniq), L.ptr(cnt), n, L.ptr(m), L.stream())
+    assert int((m != -1).sum()) == 0
 
 
 def test_sparse_table_plan_equals_dense(asme, dev):
