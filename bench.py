@@ -518,13 +518,16 @@ def main():
 
     def _release(plan):  # record the unique-row count of the step (for the byte accounting)
         if plan.dim and not last_unique:
-            last_unique.append(plan.n_unique())
+            last_unique.append(plan.count)  # (read after the timed region: no host sync inside it)
         _orig_release(plan)
 
     asme.ops.SparseTablePlan.release = _release
+    host_s = []  # host time to issue each step (no synchronisation inside a step): a CPU-bound step shows ~= ms_per_step
     for i in range(args.steps):
+        h0 = time.perf_counter()
         with timer if i >= args.steps - instrumented_steps(args.steps) else contextlib.nullcontext():
             run(args.warmup + i, i)
+        host_s.append(time.perf_counter() - h0)
     # lazily deferred zero-gradient Adam updates of the item table are part of the work: apply them all
     # (exact dense-Adam state) inside the timed region, timed on its own
     f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -544,13 +547,18 @@ def main():
     value = B * world * args.steps / elapsed
 
     kstats = timer.summary()
-    U = int(last_unique[0]) if last_unique else min(3 * B * L, V)
+    U = int(last_unique[0].item()) if last_unique else min(3 * B * L, V)
+    # distinct rows the sampled head gathers (positive and negative ids of a step's batch): the head's compulsory
+    # row bytes -- each further occurrence of a row is served from the L2 / MALL, not re-fetched from HBM
+    lb = get_batch(args.warmup + args.steps - 1) if not sharded else None
+    U_pn = (int(torch.unique(torch.cat([lb["positive_samples"].reshape(-1), lb["negative_samples"].reshape(-1)]))
+                .numel()) if lb is not None else 2 * B * L)
     T = B * L
     H, dk = args.heads, d // args.heads
     ffn = 4 * d
     # algorithmic work per launch.  Attention: causal pairs only (L(L+1)/2 per head), the
-    # forward = 2 matmul passes (QK^T, PV), the backward = 5 (recomputed S, dP, dV, dK, dQ) -- the kernels
-    # spend 2 more (dP and S again in the dK/dV pass), which is overhead, not algorithmic work.
+    # forward = 2 matmul passes (QK^T, PV), the backward = 5 (recomputed S, dP, dV, dK in the dK/dV pass, which
+    # stores dS; dQ = dS K) -- the kernels execute exactly these.
     pairs = B * H * L * (L + 1) / 2.0
     work = {
         "asme_attention_fwd": ("mfma", 2 * 2.0 * pairs * dk),
@@ -568,9 +576,10 @@ def main():
         # reads those + the compact gradient (slot order) and writes the table rows (random) + last_step
         "asme_lazy_adam_stage": ("hbm", U * 8 + U * 4 + 6 * U * d * 4),
         "asme_lazy_adam_apply_staged": ("hbm", U * 8 + U * d * 4 + 6 * U * d * 4 + U * 4),
-        # sampled head: h read once, pos and neg rows gathered, two logits written (fwd); + dh written (bwd)
-        "asme_sampled_logits_fwd": ("hbm", T * d * 4 + 2 * T * 8 + 2 * T * d * 4 + 2 * T * 4),
-        "asme_sampled_logits_bwd": ("hbm", T * d * 4 + 2 * T * 8 + 2 * T * d * 4 + 2 * T * 4 + T * d * 4),
+        # sampled head: h read once, the distinct pos / neg rows gathered (U_pn), two logits written (fwd); the bwd
+        # reads h, the rows and the two logit gradients, and writes dh
+        "asme_sampled_logits_fwd": ("hbm", T * d * 4 + 2 * T * 8 + U_pn * d * 4 + 2 * T * 4),
+        "asme_sampled_logits_bwd": ("hbm", T * d * 4 + 2 * T * 8 + U_pn * d * 4 + 2 * T * 4 + T * d * 4),
         "asme_gelu_dropout_bwd": ("hbm", 3 * T * ffn * 4),
         "asme_adam_rows_step": ("hbm", 6 * V * d * 4 + V * 4 + U * d * 4),
         # session items read once + x / pos / neg written (the in-session membership scans hit the cache)
@@ -614,6 +623,8 @@ def main():
         "roofline": roof,
         "rooflines": rooflines,
         "flush_ms": round(flush_ms, 3),
+        # diagnostic: median host time to issue one step's launches (the GPU runs behind the host when it is smaller)
+        "host_issue_ms": round(1000 * sorted(host_s)[len(host_s) // 2], 3),
         "cpu_baseline": None,
     }
     asme.ops.SparseTablePlan.release = _orig_release

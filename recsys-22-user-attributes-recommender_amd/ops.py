@@ -207,11 +207,15 @@ class SparseTablePlan:
         """(rows, row ids) a reader of `ids` gathers from: the staged rows by slot when this step staged them,
         else the table itself by id"""
         if self.staged is not None and self.has(ids):
+            if self._distinct:  # slot s holds ids[s]: the staged rows are the gathered rows themselves
+                return self.staged[0], None
             return self.staged[0], self.inverse_of(ids)
         return table, ids
 
+    _distinct = False
+
     def has(self, ids: torch.Tensor) -> bool:
-        return (ids.data_ptr(), tuple(ids.shape)) in self._inverse
+        return (ids.data_ptr(), tuple(ids.shape)) in (self._offset if self._distinct else self._inverse)
 
     @classmethod
     def identity(cls, n_rows: int, id_sets: Sequence[torch.Tensor], dim: int) -> "SparseTablePlan":
@@ -245,9 +249,57 @@ class SparseTablePlan:
         return self
 
     @classmethod
+    def distinct(cls, table: torch.Tensor, ids: torch.Tensor) -> "SparseTablePlan":
+        """plan over ids known to be distinct (the row-shard owner's requests at one rank): no dedup, slot s ==
+        ids[s]; the rows are staged like any plan's, and a single unscaled gradient contribution (one row per
+        slot) is applied as it is -- no occurrence CSR, no reduction"""
+        self = cls.__new__(cls)
+        ids = _i64(ids).reshape(-1)
+        n = ids.numel()
+        dev = ids.device
+        self.vocab, self.dim = table.shape
+        self.slot_map = None
+        self.unique = ids
+        self.count = torch.tensor([n], dtype=torch.int32).to(dev, non_blocking=True)
+        self.capacity = n
+        self._slots_mapped = True
+        self._distinct = True
+        self.grad_scale = 1.0
+        self._grad_rows = None
+        key = (ids.data_ptr(), tuple(ids.shape))
+        self._flat_inverse = None
+        self._inverse, self._offset, self._contrib = {}, {key: 0}, []
+        self.consumed = False
+        self.staged = None
+        tg = getattr(table, "_asme_table_grad", None)
+        if tg is not None:
+            tg.drop_applied()
+            if tg.lazy is not None:
+                if tg.lazy.stage_ok():
+                    self.staged = tg.lazy.stage(self.unique, self.count, self.capacity)
+                else:
+                    tg.lazy.catch_up(self.unique, self.count, self.capacity)
+        return self
+
+    @classmethod
     def for_ids(cls, vocab: int, id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor) -> "SparseTablePlan":
         """dedup only (no table attached): unique ids in first-occurrence order + inverse per id set"""
         return cls(None, id_sets, slot_map, vocab=vocab, dim=0)
+
+    def adopt_contributions(self, other: "SparseTablePlan"):
+        """take over the gradient contributions of `other`, a plan over the same slots (the one-rank sharded step:
+        the requester's compact identity plan, whose row s is this distinct plan's slot s): its occurrence -> slot
+        map and registered rows, reduced (and applied) by this plan"""
+        if not self._distinct or other.capacity == 0 or other._grad_rows is not None:
+            raise RuntimeError("adopt_contributions: a distinct plan taking an unreduced plan over its slots")
+        self._flat_inverse = other._flat_inverse
+        self.capacity = other.capacity  # occurrences (>= slots): the CSR's length; count stays the slot count
+        self._contrib = other._contrib
+        other._contrib = []
+        self._adopted = True
+        other.release()
+
+    _adopted = False
 
     def add_rows(self, ids: torch.Tensor, rows: torch.Tensor):
         """register the gradient rows (one per occurrence of the registered id set `ids`) of this step;
@@ -275,6 +327,8 @@ class SparseTablePlan:
         order = torch.empty(n, device=dev, dtype=torch.int32)
         slot = torch.empty(n, device=dev, dtype=torch.int32)
         seg_off = torch.empty(n + 1, device=dev, dtype=torch.int32)
+        if self._flat_inverse is None:  # a distinct plan: occurrence s is slot s
+            self._flat_inverse = torch.arange(n, device=dev, dtype=torch.int64)
         call("asme_occurrence_csr", ptr(self._flat_inverse), n, n, ptr(ws), ws_bytes, ptr(order), ptr(slot),
              ptr(seg_off), stream())
         part_bytes = int(lib.asme_table_grad_workspace(n, self.dim))
@@ -292,7 +346,7 @@ class SparseTablePlan:
         """the table gradient reduced and applied as the lazy Adam's real-gradient step in one pass from the staged
         rows (asme_table_grad_reduce_apply); False (nothing done) where the gradient rows are needed as such"""
         if self.staged is None or self._grad_rows is not None or not 1 <= len(self._contrib) <= 4 \
-                or self.capacity == 0:
+                or self.capacity == 0 or (self._distinct and not self._adopted):
             return False
         order, slot, seg_off, parts, part_bytes = self._occurrence_csr()
         k, offs, ns, rows, scales = self._contrib_arrays(sorted(self._contrib, key=lambda c: c[0]))
@@ -330,7 +384,12 @@ class SparseTablePlan:
         """compact (capacity, d) gradient rows, slot s <-> unique[s]: the ordered sums of the registered
         contributions (add_rows / add_scaled), or a zeroed buffer for callers that scatter-add into it"""
         if self._grad_rows is None:
-            if self._contrib:
+            if self._distinct and len(self._contrib) == 1 and self._contrib[0][3] is None \
+                    and self._contrib[0][1] == self.capacity:
+                rows = self._contrib[0][2]  # one row per slot, in slot order: the gradient as it is
+                self._grad_rows = rows if self.grad_scale == 1.0 else rows * self.grad_scale
+                self._contrib = []
+            elif self._contrib:
                 self._grad_rows = self._reduce_contributions()
             else:
                 self._grad_rows = torch.zeros(self.capacity, self.dim, device=self.unique.device,
@@ -356,6 +415,10 @@ class SparseTablePlan:
 
     def inverse_of(self, ids: torch.Tensor) -> torch.Tensor:
         key = (ids.data_ptr(), tuple(ids.shape))
+        if self._distinct and key in self._offset:
+            if key not in self._inverse:
+                self._inverse[key] = torch.arange(ids.numel(), device=ids.device, dtype=torch.int64).view(ids.shape)
+            return self._inverse[key]
         if key not in self._inverse:
             raise KeyError("ids were not registered with the sparse table plan of this step")
         return self._inverse[key]

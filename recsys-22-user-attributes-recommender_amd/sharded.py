@@ -150,6 +150,8 @@ class RowShardExchange:
     def reply_rows(self, st: ExchangeState, rows: torch.Tensor) -> torch.Tensor:
         """owners' rows (aligned with st.recv_local) -> the requester's rows in SEND order: row j belongs to
         unique[st.order[j]] (unique id i is row st.pos[i]; callers remap ids instead of permuting rows)"""
+        if self.world == 1:  # the rank's own rows in request order: no copy
+            return rows.detach().contiguous()
         U = len(st.order)
         got = torch.empty(U, rows.shape[1], dtype=rows.dtype, device=rows.device)
         _all_to_all(got, rows.contiguous(), st.send_counts, st.recv_counts, group=self.group)
@@ -157,6 +159,8 @@ class RowShardExchange:
 
     def push_grads(self, st: ExchangeState, grad_send: torch.Tensor) -> torch.Tensor:
         """requester's gradient rows in send order (aligned with reply_rows) -> owners, aligned with recv_local"""
+        if self.world == 1:
+            return grad_send.contiguous()
         recv = torch.empty(len(st.recv_local), grad_send.shape[1], dtype=grad_send.dtype, device=grad_send.device)
         _all_to_all(recv, grad_send.contiguous(), st.recv_counts, st.send_counts, group=self.group)
         return recv
@@ -261,11 +265,18 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         own = None
         src, src_ids = shard.detach(), st.recv_local
         if train:
-            own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
-            own.grad_scale = 1.0 / self.exchange.world  # DDP gradient averaging, applied in the ordered row sums
+            if self.exchange.world == 1:
+                # one rank: the requests are the requester's unique ids -- distinct, no owner dedup / CSR
+                own = ops.SparseTablePlan.distinct(shard, st.recv_local)
+            else:
+                own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
+                own.grad_scale = 1.0 / self.exchange.world  # DDP averaging, applied in the ordered row sums
             src, src_ids = own.gather_source(shard.detach(), st.recv_local)
         with torch.no_grad():
-            rows = ops.gather_rows(src_ids, src) if len(st.recv_local) else shard.new_empty(0, shard.shape[1])
+            if src_ids is None:  # the staged rows are the requested rows, in request order
+                rows = src[:len(st.recv_local)]
+            else:
+                rows = ops.gather_rows(src_ids, src) if len(st.recv_local) else shard.new_empty(0, shard.shape[1])
         # the compact table stays in send order; the ids are remapped to it (no row permutation)
         compact = self.exchange.reply_rows(st, rows)
         inv = [st.pos.index_select(0, req.inverse_of(x).reshape(-1)).view(x.shape) for x in id_sets]
@@ -307,12 +318,20 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         self._pending = None
         if self.reducer is not None:
             self.reducer.finish()
+        shard = self.model.item_table()
+        if self.exchange.world == 1 and own is not None and own._distinct and compact.grad is None \
+                and cplan.has_gradient() and cplan._grad_rows is None:
+            # one rank: compact row s IS the owner's slot s, so the owner reduces the requester's occurrences
+            # directly and applies the step in the same pass (asme_table_grad_reduce_apply) -- no compact gradient
+            # rows, no exchange
+            own.adopt_contributions(cplan)
+            shard._asme_table_grad.plan = own
+            return
         g = cplan.grad_rows[:compact.shape[0]]
         if compact.grad is not None:  # a head without the plan path returned a dense gradient
             g = g + compact.grad
         recv = self.exchange.push_grads(st, g)
         cplan.release()
-        shard = self.model.item_table()
         if len(st.recv_local):
             own.add_rows(st.recv_local, recv)  # ordered per-row sums x 1/W (deterministic)
         shard._asme_table_grad.plan = own

@@ -16,6 +16,9 @@ import sys
 # kernel-name regex -> (API call, counts-the-call?)
 MAP = [
     (r"attn_fwd(_res)?_kernel", "asme_attention_fwd", True),
+    # the backward: dK/dV (storing dS) first, then dQ = dS K (resident path); the streaming path's dQ pass first
+    (r"attn_bwd_dkdv_res_kernel<\d+, true>", "asme_attention_bwd", True),
+    (r"attn_bwd_dq_ds_kernel", "asme_attention_bwd", False),
     (r"attn_bwd_dq(_res)?_kernel", "asme_attention_bwd", True),
     (r"attn_bwd_dkdv(_res)?_kernel", "asme_attention_bwd", False),
     (r"weight_grad_kernel", "asme_linear_weight_grad", True),
@@ -35,7 +38,7 @@ MAP = [
     (r"claim_kernel", "asme_dedup_ids", True),
     (r"(flag|compact|inverse|dedup_\w+)_kernel", "asme_dedup_ids", False),
     (r"csr_count_kernel", "asme_occurrence_csr", True),
-    (r"csr_\w+_kernel", "asme_occurrence_csr", False),
+    (r"(csr_\w+|chained_scan)_kernel", "asme_occurrence_csr", False),
     (r"grad_chunk_kernel<true>", "asme_table_grad_reduce_apply", True),
     (r"grad_span_kernel<true>", "asme_table_grad_reduce_apply", False),
     (r"gelu_dropout_fwd_kernel", "asme_gelu_dropout_fwd", True),
