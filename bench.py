@@ -332,16 +332,34 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
         reducer = asme.dataparallel.GradientAllReduce(module)
         reducer.broadcast_parameters(module)
 
+    # each step's batch is produced on a side stream one step ahead, and its masked rows selected there
+    # (module.prefetch: torch.nonzero's host read waits for the side stream only) once the current step is enqueued
+    side = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+
+    def make_batch(i):
+        with torch.cuda.stream(side):
+            idx = order[(i * B) % (n_sess - B + 1):][:B]
+            items, lengths = asme.batches.padded_session_batch(store, idx, L)
+            b = cloze.process_batch(items, lengths, seed=1000 + i)
+            if kebert:
+                b["genre"] = torch.where(items > 0, items % (n_genre - 1) + 1, 0)
+        return b
+
+    ahead = {}
+
     def step(i):
-        idx = order[(i * B) % (n_sess - B + 1):][:B]
-        items, lengths = asme.batches.padded_session_batch(store, idx, L)
-        batch = cloze.process_batch(items, lengths, seed=1000 + i)
-        if kebert:
-            batch["genre"] = torch.where(items > 0, items % (n_genre - 1) + 1, 0)
+        batch = ahead.pop(i, None) or make_batch(i)
+        main.wait_stream(side)  # the batch and its prefetched rows
+        for t in list(batch.values()) + list(module._rows_ahead[1:] if module._rows_ahead else []):
+            t.record_stream(main)
+        nxt = ahead[i + 1] = make_batch(i + 1)
         if reducer is not None:
             asme.dataparallel.train_step(module, opt, sched, reducer, batch, i)
         else:
             asme.modules.train_step(module, opt, sched, batch, i)
+        with torch.cuda.stream(side):
+            module.prefetch(nxt)
 
     for i in range(args.warmup):
         step(i)

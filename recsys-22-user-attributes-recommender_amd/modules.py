@@ -356,11 +356,30 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
             raise NotImplementedError("basket (multi-target) masked training is outside the MI355X hot path")
         pad = self.item_tokenizer.pad_token_id
         self._plan_table([batch[ITEM_SEQ_ENTRY_NAME]])
-        rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)
+        ahead, self._rows_ahead = self._rows_ahead, None
+        if ahead is not None and ahead[0] is target:
+            rows, row_targets = ahead[1], ahead[2]
+        else:
+            rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)  # (reads the row count on the host)
+            row_targets = target.reshape(-1).index_select(0, rows)
         loss = _rows_cross_entropy(self.model, build_model_input(self.model, self.item_tokenizer, batch), rows,
-                                   target.reshape(-1).index_select(0, rows), pad)
+                                   row_targets, pad)
         self.log(LOG_KEY_TRAINING_LOSS, loss, prog_bar=False)
         return {"loss": loss}
+
+    _rows_ahead = None
+
+    def prefetch(self, batch):
+        """Select the NEXT training step's masked rows now (torch.nonzero: the host reads their count).  Called on
+        the stream that produced `batch` (a side stream) once the current step is enqueued, the host waits only
+        for that stream's work -- the cloze producer -- never for the main stream's queue, which a nonzero at the
+        start of the step drains.  The next training_step must receive the very same target tensor; the caller
+        makes the main stream wait for the side stream before that step."""
+        target = batch[TARGET_ENTRY_NAME]
+        if target.dim() != 2:
+            return
+        rows = torch.nonzero(target.reshape(-1) != self.item_tokenizer.pad_token_id).squeeze(1)
+        self._rows_ahead = (target, rows, target.reshape(-1).index_select(0, rows))
 
     def _get_prediction_for_masked_item(self, batch, batch_idx=None) -> torch.Tensor:
         self._flush_table()
