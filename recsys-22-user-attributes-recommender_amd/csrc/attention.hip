@@ -930,20 +930,37 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
     }
     __syncthreads();
     if (DS) {
-        // D_i = dO_i . O_i: 16 lanes per query row (a float4 of features each, dO from the LDS image)
-        for (int i = threadIdx.x >> 4; i < Lp; i += kResThreadsKV / 16) {
-            const int c = 4 * (threadIdx.x & 15);
-            float acc = 0.f;
-            if (i < L) {
-                for (int cc = c; cc < DK; cc += 64) {
-                    const float4 a = *reinterpret_cast<const float4*>(Ds + i * S + cc);
-                    const float4 bo = *reinterpret_cast<const float4*>(o + (tok0 + i) * ldo + h * DK + cc);
-                    acc += a.x * bo.x + a.y * bo.y + a.z * bo.z + a.w * bo.w;
-                }
-            }
+        // D_i = dO_i . O_i: 16 lanes per query row (a float4 of features each, dO from the LDS image); a thread's
+        // O loads for four rows are all issued before the first is used (one round trip per four rows: a dependent
+        // load per row cost ~2 us each in this prologue, which nothing overlaps at one workgroup per CU)
+        constexpr int kRowStep = kResThreadsKV / 16, kU = 4, FC = (DK + 63) / 64;
+        const int c = 4 * (threadIdx.x & 15);
+        for (int i0 = threadIdx.x >> 4; i0 < Lp; i0 += kRowStep * kU) {
+            float4 ov[kU][FC];
 #pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 16);
-            if ((threadIdx.x & 15) == 0) dsum_s[i] = acc;
+            for (int u = 0; u < kU; ++u)
+#pragma unroll
+                for (int f = 0; f < FC; ++f) {
+                    const int i = i0 + u * kRowStep, cc = c + 64 * f;
+                    ov[u][f] = (i < L && cc < DK) ? *reinterpret_cast<const float4*>(o + (tok0 + i) * ldo + h * DK + cc)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int i = i0 + u * kRowStep;
+                float acc = 0.f;
+#pragma unroll
+                for (int f = 0; f < FC; ++f) {
+                    const int cc = c + 64 * f;
+                    if (i < Lp && cc < DK) {
+                        const float4 a = *reinterpret_cast<const float4*>(Ds + i * S + cc);
+                        acc += a.x * ov[u][f].x + a.y * ov[u][f].y + a.z * ov[u][f].z + a.w * ov[u][f].w;
+                    }
+                }
+#pragma unroll
+                for (int off = 8; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 16);
+                if ((threadIdx.x & 15) == 0 && i < Lp) dsum_s[i] = acc;
+            }
         }
         __syncthreads();
     }
@@ -1105,33 +1122,39 @@ __global__ __launch_bounds__(kDsThreads) void attn_bwd_dq_ds_kernel(const float*
         floatx4 acc[NCT];
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-        float4 cur[kNS], nxt[kNS];
+        // the dS row slice two chunks ahead: the loads of chunk c + 2 are in flight during chunk c's MFMAs (one
+        // chunk ahead left ~half the pass waiting on them)
+        float4 b0[kNS], b1[kNS], b2[kNS];
         auto fetch = [&](int c, float4 (&dst)[kNS]) {
 #pragma unroll
             for (int sub = 0; sub < kNS; ++sub)
                 dst[sub] = c + sub < nsub ? *reinterpret_cast<const float4*>(wrow + (c + sub) * 16)
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
         };
-        fetch(0, cur);
+        fetch(0, b0);
+        fetch(kNS, b1);
         int c0 = 0;
         for (; c0 + kNS <= nsub; c0 += kNS) {
-            if (c0 + kNS < nsub) fetch(c0 + kNS, nxt);
+            fetch(c0 + 2 * kNS, b2);
             float w[kNS][4];
 #pragma unroll
             for (int sub = 0; sub < kNS; ++sub) {
-                w[sub][0] = cur[sub].x;
-                w[sub][1] = cur[sub].y;
-                w[sub][2] = cur[sub].z;
-                w[sub][3] = cur[sub].w;
+                w[sub][0] = b0[sub].x;
+                w[sub][1] = b0[sub].y;
+                w[sub][2] = b0[sub].z;
+                w[sub][3] = b0[sub].w;
             }
             cols_times_weights<DK, kNS>(Ks + c0 * 16 * S, g, c16, w, acc);
 #pragma unroll
-            for (int sub = 0; sub < kNS; ++sub) cur[sub] = nxt[sub];
+            for (int sub = 0; sub < kNS; ++sub) {
+                b0[sub] = b1[sub];
+                b1[sub] = b2[sub];
+            }
         }
 #pragma unroll
         for (int sub = 0; sub < kNS - 1; ++sub) {
             if (c0 + sub < nsub) {
-                float w1[1][4] = {{cur[sub].x, cur[sub].y, cur[sub].z, cur[sub].w}};
+                float w1[1][4] = {{b0[sub].x, b0[sub].y, b0[sub].z, b0[sub].w}};
                 cols_times_weights<DK, 1>(Ks + (c0 + sub) * 16 * S, g, c16, w1, acc);
             }
         }

@@ -916,20 +916,26 @@ __global__ __launch_bounds__(256) void grad_span_kernel(const int32_t* __restric
         if (cl - cf <= 8) {
             for (int64_t q = cf + 1; q <= cl; ++q) add4(acc, *reinterpret_cast<const float4*>(head + q * dim + c0));
         } else {
-            // a hot slot (PAD, MASK: tens of thousands of occurrences, > 1,000 chunk partials): eight interleaved
-            // partial sums (loads in flight), combined in a fixed tree -- still one fixed order (deterministic)
-            float4 pr[8];
+            // a hot slot (PAD, MASK: tens of thousands of occurrences, > 1,000 chunk partials): kHotWays interleaved
+            // partial sums (as many loads in flight), combined in a fixed tree -- still one fixed order
+            // (deterministic).  8 ways left the 1,150 partials of a C3 batch's MASK row at 62 us (latency-bound).
+            constexpr int kHotWays = 16;
+            float4 pr[kHotWays];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) pr[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int u = 0; u < kHotWays; ++u) pr[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             int64_t q = cf + 1;
-            for (; q + 7 <= cl; q += 8)
+            for (; q + kHotWays - 1 <= cl; q += kHotWays)
+#pragma unroll
+                for (int u = 0; u < kHotWays; ++u)
+                    add4(pr[u], *reinterpret_cast<const float4*>(head + (q + u) * dim + c0));
+            for (; q + 7 <= cl; q += 8)  // the tail: fewer than kHotWays partials, eight in flight
 #pragma unroll
                 for (int u = 0; u < 8; ++u) add4(pr[u], *reinterpret_cast<const float4*>(head + (q + u) * dim + c0));
             for (; q <= cl; ++q) add4(pr[0], *reinterpret_cast<const float4*>(head + q * dim + c0));
 #pragma unroll
-            for (int w = 1; w < 8; w *= 2)
+            for (int w = 1; w < kHotWays; w *= 2)
 #pragma unroll
-                for (int u = 0; u < 8; u += 2 * w) add4(pr[u], pr[u + w]);
+                for (int u = 0; u < kHotWays; u += 2 * w) add4(pr[u], pr[u + w]);
             add4(acc, pr[0]);
         }
         if constexpr (APPLY)
