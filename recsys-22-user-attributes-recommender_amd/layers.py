@@ -411,8 +411,7 @@ class SASRecProjectionComponent(nn.Module):
         mask = sequence.padding_mask
         idx = mask.sum(-1) - 1
         last = representation[torch.arange(representation.shape[0], device=representation.device), idx]
-        if pos.dim() == 2 and pos.shape[1] == table.shape[0] and bool(
-                (pos[0] == torch.arange(table.shape[0], device=pos.device)).all()) and bool((pos == pos[0]).all()):
+        if getattr(pos, "_asme_all_items", False) and pos.dim() == 2 and pos.shape[1] == table.shape[0]:
             return ops.logits(last, table)  # all items, in id order (predict_step's items_to_rank)
         rows = F.embedding(pos, table)  # (N, I, d)
         return torch.bmm(rows, last.unsqueeze(-1)).squeeze(-1)

@@ -176,7 +176,10 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         meta = get_additional_meta_data(self.model, batch)
         padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
         n = len(self.item_tokenizer.get_vocabulary())
-        items = torch.arange(n, dtype=torch.long, device=input_seq.device).repeat([input_seq.shape[0], 1])
+        # the reference's items_to_rank (B, |V|) as a stride-0 view, tagged so the projection scores the whole
+        # catalogue on the logits kernel without inspecting it (no (B, |V|) int64 buffer, no host sync)
+        items = torch.arange(n, dtype=torch.long, device=input_seq.device).expand(input_seq.shape[0], n)
+        items._asme_all_items = True
         meta["positive_samples"] = items
         return self.model(InputSequence(input_seq, padding_mask, meta))
 
