@@ -87,10 +87,14 @@ template <int K, int CT, bool TRANS, int EPI>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ws_gemm_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W, int N, float* __restrict__ Y, WsEpi ep) {
     constexpr int NB = 16 * CT;  // output features per workgroup
+    // k32 blocks of X in flight: the whole 8-block tile for the first K = 256 half of the FFN-out forward (its waves
+    // wait on X most; 256 VGPRs, no spill; tools/ws_ab.py same process 180 -> 173 us per product; the input-gradient
+    // form and K = 384 measured flat or slower with a deeper ring)
+    constexpr int RD = (K == 256 && EPI == WS_STORE && !TRANS) ? 8 : kD;
     constexpr int K8 = K / 8;    // 16-B slots (8 bf16) of a W image row
     constexpr int NKB = K / 32;
     constexpr int PL = NB * K8;  // slots of one bf16 plane
-    static_assert(NKB % kD == 0, "the ring depth must divide the k32 blocks of a tile");
+    static_assert(NKB % RD == 0, "the ring depth must divide the k32 blocks of a tile");
     static_assert(CT % 2 == 0, "GELU-dropout Philox blocks serve feature-tile pairs");
     // row-major staging of the finished tile (per wave, 16 rows x NB, 16-B row pad) so each store instruction
     // writes whole rows (16 lanes x 16 B = 256 B of one row at NB = 64) instead of 16 rows x 64 B (measured:
@@ -156,9 +160,9 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     uint32_t pend = 0;  // GELU-dropout bits of the odd feature tile of the current pair
     const float* rc = xrow(0);
     const float* rn = xrow(1);
-    float4 ring[2 * kD];  // k32 block d of X: ring[2d] (k 8g..8g+3), ring[2d + 1] (k 8g+4..8g+7)
+    float4 ring[2 * RD];  // k32 block d of X: ring[2d] (k 8g..8g+3), ring[2d + 1] (k 8g+4..8g+7)
 #pragma unroll
-    for (int d = 0; d < kD; ++d) {
+    for (int d = 0; d < RD; ++d) {
         ring[2 * d] = *reinterpret_cast<const float4*>(rc + d * 32);
         ring[2 * d + 1] = *reinterpret_cast<const float4*>(rc + d * 32 + 4);
         __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's vmcnt waits assume it
@@ -263,11 +267,11 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     for (int64_t j = 0; j < my_tiles; ++j) {
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-        // kD blocks per trip, unrolled; the trips themselves stay a loop (a fully unrolled K = 384 tile spills)
+        // RD blocks per trip, unrolled; the trips themselves stay a loop (a fully unrolled K = 384 tile spills)
 #pragma unroll 1
-        for (int kq = 0; kq < NKB; kq += kD)
+        for (int kq = 0; kq < NKB; kq += RD)
 #pragma unroll
-        for (int d = 0; d < kD; ++d) {
+        for (int d = 0; d < RD; ++d) {
             const int kb = kq + d;
             const int kbn = kb + 1 == NKB ? 0 : kb + 1;
             // each feature tile's six MFMAs, then its next-block W read into the registers they consumed
@@ -277,13 +281,13 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                 wc[ct] = wload(ct, kbn);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            // refill the slot just consumed: block kb + kD of this tile or of the next one (unconditional,
+            // refill the slot just consumed: block kb + RD of this tile or of the next one (unconditional,
             // so the vmcnt bookkeeping stays exact; past the last tile it re-reads the last one)
-            const float* src = (kb + kD < NKB ? rc : rn) + ((kb + kD) % NKB) * 32;
+            const float* src = (kb + RD < NKB ? rc : rn) + ((kb + RD) % NKB) * 32;
             ring[2 * d] = *reinterpret_cast<const float4*>(src);
             ring[2 * d + 1] = *reinterpret_cast<const float4*>(src + 4);
             // the next block's X terms
-            const int dn = (kb + 1) % kD;
+            const int dn = (kb + 1) % RD;
             xs = split_bf3(ring[2 * dn], ring[2 * dn + 1]);
             // the previous tile's epilogue, spread over the blocks (late in the tile, so the pre-activation
             // loads WS_GELU_BWD issued at the tile boundary have landed)
