@@ -595,9 +595,11 @@ def main():
         "asme_lazy_adam_stage": ("hbm", U * 8 + U * 4 + 6 * U * d * 4),
         "asme_lazy_adam_apply_staged": ("hbm", U * 8 + U * d * 4 + 6 * U * d * 4 + U * 4),
         # sampled head: h read once, the distinct pos / neg rows gathered (U_pn), two logits written (fwd); the bwd
-        # reads h, the rows and the two logit gradients, and writes dh
+        # reads the ids, the rows and the two logit gradients and writes dh -- h only where it also scatters the
+        # table gradient (table_grad="dense"; the sparse plan takes the table's rows from the step's contributions)
         "asme_sampled_logits_fwd": ("hbm", T * d * 4 + 2 * T * 8 + U_pn * d * 4 + 2 * T * 4),
-        "asme_sampled_logits_bwd": ("hbm", T * d * 4 + 2 * T * 8 + U_pn * d * 4 + 2 * T * 4 + T * d * 4),
+        "asme_sampled_logits_bwd": ("hbm", 2 * T * 8 + U_pn * d * 4 + 2 * T * 4 + T * d * 4
+                                    + (T * d * 4 if args.table_grad == "dense" else 0)),
         "asme_gelu_dropout_bwd": ("hbm", 3 * T * ffn * 4),
         "asme_adam_rows_step": ("hbm", 6 * V * d * 4 + V * 4 + U * d * 4),
         # session items read once + x / pos / neg written (the in-session membership scans hit the cache)

@@ -269,6 +269,9 @@ int asme_posneg_sample(const int64_t* flat, const int64_t* offsets, int64_t n_se
 int asme_cloze_mask(const int64_t* items, const int64_t* lengths, int64_t batch, int64_t seq_len, int64_t vocab,
                     int64_t pad, int64_t mask_id, double mask_prob, double last_prob, const float* draws_u,
                     const int64_t* draws_r, uint64_t seed, int64_t* out, int64_t* target, void* stream);
+/* asme_padding_mask: flags[i] = seq[i] != pad over n ids (core/modules/util/module_util.py:13-30 get_padding_mask,
+ *   sequence.ne(pad_token_id)); flags are bytes (a torch.bool tensor), seq 16-B and flags 4-B aligned. */
+int asme_padding_mask(const int64_t* seq, int64_t n, int64_t pad, uint8_t* flags, void* stream);
 /* asme_last_item_mask: LastItemMaskProcessor (last_item_mask.py:35-44) + collate on a collated batch (items
  *   (batch, in_len), lengths): out (batch, out_len_max) = the last min(len, out_len_max - 1) items, MASK, PAD;
  *   out_len (nullable) = the new lengths; requires in_len >= out_len_max - 1 */

@@ -106,6 +106,7 @@ SIGNATURES = {
     "asme_posneg_sample": [p, p, i64, p, i64, i64, i64, p, i32, i64, u64, p, p, p, p, p, p],
     "asme_last_item_mask": [p, p, i64, i64, i64, i64, i64, p, p, p],
     "asme_cloze_mask": [p, p, i64, i64, i64, i64, i64, f64, f64, p, p, u64, p, p, p],
+    "asme_padding_mask": [p, i64, i64, p, p],
 }
 _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes": ctypes.c_int64,
              "asme_linear_weight_grad_workspace": ctypes.c_int64,

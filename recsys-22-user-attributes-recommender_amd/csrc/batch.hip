@@ -228,6 +228,23 @@ __global__ __launch_bounds__(256) void cloze_kernel(const int64_t* __restrict__ 
     }
 }
 
+// ------------------------------------------------------------------------------------------ padding mask
+// out[i] = seq[i] != pad (modules.get_padding_mask, the reference's input.ne(pad_token_id)); four ids per thread,
+// one 4-byte store of their four flags
+__global__ __launch_bounds__(256) void padding_mask_kernel(const int64_t* __restrict__ seq, int64_t n, int64_t pad,
+                                                           uint8_t* __restrict__ out) {
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 + 3 < n) {
+        const longlong2 a = *reinterpret_cast<const longlong2*>(seq + i0);
+        const longlong2 b = *reinterpret_cast<const longlong2*>(seq + i0 + 2);
+        const uint32_t w = (uint32_t)(a.x != pad) | (uint32_t)(a.y != pad) << 8 | (uint32_t)(b.x != pad) << 16 |
+                           (uint32_t)(b.y != pad) << 24;
+        *reinterpret_cast<uint32_t*>(out + i0) = w;
+    } else {
+        for (int64_t i = i0; i < n; ++i) out[i] = seq[i] != pad;
+    }
+}
+
 }  // namespace
 
 ASME_API int asme_session_batch(const int64_t* flat, const int64_t* offsets, int64_t n_sessions,
@@ -293,4 +310,14 @@ ASME_API int asme_cloze_mask(const int64_t* items, const int64_t* lengths, int64
     hipLaunchKernelGGL(cloze_kernel, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, items, lengths, batch,
                        seq_len, vocab, pad, mask_id, mask_prob, last_prob, draws_u, draws_r, seed, out, target);
     ASME_LAUNCH_CHECK("asme_cloze_mask");
+}
+
+// flags[i] = seq[i] != pad for n int64 ids (16-B aligned): the model's padding mask (modules.get_padding_mask)
+ASME_API int asme_padding_mask(const int64_t* seq, int64_t n, int64_t pad, uint8_t* flags, void* stream) {
+    ASME_CHECK_ARG(seq && flags, "asme_padding_mask: null pointer");
+    ASME_CHECK_ARG(((uintptr_t)seq & 15) == 0 && ((uintptr_t)flags & 3) == 0, "asme_padding_mask: alignment");
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(padding_mask_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, (hipStream_t)stream, seq,
+                       n, pad, flags);
+    ASME_LAUNCH_CHECK("asme_padding_mask");
 }

@@ -292,6 +292,10 @@ class IdentitySequenceRepresentationModifierLayer(nn.Module):
     def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
         return encoded
 
+    def forward_rows(self, encoded_rows: torch.Tensor, sequence=None, rows=None, inverse=None) -> torch.Tensor:
+        """the modifier on the selected flattened positions only (models.TransformerEncoderModel.encode_rows)"""
+        return encoded_rows
+
 
 class FFNSequenceRepresentationModifierComponent(nn.Module):
     """LN(GELU(Linear(x))) (ffn_modifier.py:24-26)"""
@@ -303,6 +307,15 @@ class FFNSequenceRepresentationModifierComponent(nn.Module):
     def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
         lin, _, norm = self.transform
         return ops.layer_norm(ops.gelu_dropout(ops.linear(encoded, lin.weight, lin.bias), 0.0), norm)
+
+    def forward_rows(self, encoded_rows: torch.Tensor, sequence=None, rows=None, inverse=None) -> torch.Tensor:
+        """position-wise: the same transform on the selected rows (M, d) alone"""
+        return self.forward(encoded_rows)
+
+
+def _rows_of(x: Optional[torch.Tensor], rows: torch.Tensor, inverse=None) -> Optional[torch.Tensor]:
+    """the flattened positions `rows` of a (B, L, d) per-position tensor"""
+    return None if x is None else ops.select_rows(x.reshape(-1, x.shape[-1]), rows, inverse)
 
 
 def _merge(x: torch.Tensor, ctx: torch.Tensor, fn: str) -> torch.Tensor:
@@ -332,6 +345,13 @@ class PostFusionContextSequenceRepresentationModifierComponent(nn.Module):
         lin, _, norm = self.transform
         return ops.layer_norm(ops.gelu_dropout(ops.linear(x, lin.weight, lin.bias), 0.0), norm)
 
+    def forward_rows(self, encoded_rows: torch.Tensor, sequence=None, rows=None, inverse=None) -> torch.Tensor:
+        """position-wise: the selected rows merged with their positions' attribute sums, then the transform"""
+        x = _merge(encoded_rows, _rows_of(_attribute_sum(self.postfusion_attribute_embeddings, sequence), rows,
+                                          inverse), self.merge_function)
+        lin, _, norm = self.transform
+        return ops.layer_norm(ops.gelu_dropout(ops.linear(x, lin.weight, lin.bias), 0.0), norm)
+
 
 class PostFusionIdentitySequenceRepresentationModifierLayer(nn.Module):
     """x (+|*)= sum attr-emb, no transform (sasrec/components.py:63-106)"""
@@ -348,6 +368,10 @@ class PostFusionIdentitySequenceRepresentationModifierLayer(nn.Module):
 
     def forward(self, encoded: torch.Tensor, sequence=None) -> torch.Tensor:
         return _merge(encoded, _attribute_sum(self.postfusion_attribute_embeddings, sequence), self.merge_function)
+
+    def forward_rows(self, encoded_rows: torch.Tensor, sequence=None, rows=None, inverse=None) -> torch.Tensor:
+        return _merge(encoded_rows, _rows_of(_attribute_sum(self.postfusion_attribute_embeddings, sequence), rows,
+                                             inverse), self.merge_function)
 
 
 # ------------------------------------------------------------------------------------ projections

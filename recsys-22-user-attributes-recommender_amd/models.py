@@ -100,15 +100,25 @@ class TransformerEncoderModel(SequenceRecommenderModel):
         if is_linear and module.bias is not None:
             module.bias.data.zero_()
 
-    def encode_rows(self, sequence, rows: torch.Tensor) -> torch.Tensor:
-        """representations of the flattened positions `rows` only, (M, d)"""
-        rep = self.encode(sequence)
-        return rep.reshape(-1, rep.shape[-1]).index_select(0, rows)
+    def encode_rows(self, sequence, rows: torch.Tensor, inverse: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """representations of the flattened positions `rows` only, (M, d) == encode(sequence).view(-1, d)[rows].
+        The transformer runs on every position; the representation modifier is position-wise (Linear -> GELU -> LN,
+        optionally after merging the position's attribute embeddings), so it runs on the selected rows alone
+        (`forward_rows` of the modifier layers) -- a masked batch selects ~18 % of the positions.  `inverse`: the
+        rows' inverse map (ops.row_inverse), if built ahead."""
+        emb = self._sequence_embedding_layer(sequence)
+        rep = self._sequence_representation_layer(emb, sequence.padding_mask)
+        modifier = self._sequence_representation_modifier_layer
+        rows_fn = getattr(modifier, "forward_rows", None)
+        if rows_fn is None:
+            rep = modifier(rep, sequence)
+        picked = ops.select_rows(rep.reshape(-1, rep.shape[-1]), rows, inverse)
+        return picked if rows_fn is None else rows_fn(picked, sequence, rows, inverse)
 
-    def forward_rows(self, sequence, rows: torch.Tensor) -> torch.Tensor:
+    def forward_rows(self, sequence, rows: torch.Tensor, inverse: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Full-catalogue logits for the flattened positions `rows` only, (M, |V|).  Identical to
         forward(sequence).view(-1, |V|)[rows] without the (B, L, |V|) tensor."""
-        return self._projection_layer(self.encode_rows(sequence, rows), sequence)
+        return self._projection_layer(self.encode_rows(sequence, rows, inverse), sequence)
 
     def head_weight_bias(self):
         """(W (|V|, d), b or None) when the projection is the linear / tied full-catalogue head h W^T + b

@@ -59,8 +59,11 @@ FUSED_EVAL_MIN_ITEMS = 0
 
 
 def get_padding_mask(sequence: torch.Tensor, tokenizer) -> torch.Tensor:
+    """sequence != pad (core/modules/util/module_util.py:13-30); a device int64 batch on asme_padding_mask"""
     if sequence.dim() > 2:
         sequence = sequence.max(dim=2).values
+    if sequence.is_cuda and sequence.dtype == torch.int64:
+        return ops.padding_mask(sequence, tokenizer.pad_token_id)
     return sequence.ne(tokenizer.pad_token_id)
 
 
@@ -238,17 +241,18 @@ def _instantiate_loss(loss_function, item_tokenizer):
 FUSED_XENT: bool = True
 
 
-def _rows_cross_entropy(model, sequence, rows, targets, pad: int) -> torch.Tensor:
+def _rows_cross_entropy(model, sequence, rows, targets, pad: int, inverse=None) -> torch.Tensor:
     """CrossEntropyLoss(ignore_index=pad) of the full-catalogue logits at the flattened positions `rows`
     (masked_training_module.py:93-111 / losses.py:77-115).  With a linear or tied head the logits are never
-    materialised (ops.linear_cross_entropy); otherwise they are, for the selected rows only."""
+    materialised (ops.linear_cross_entropy); otherwise they are, for the selected rows only.  `inverse`: the rows'
+    inverse map (ops.row_inverse) when built ahead."""
     wb = model.head_weight_bias() if hasattr(model, "head_weight_bias") else None
     if wb is not None:
-        h = model.encode_rows(sequence, rows)
+        h = model.encode_rows(sequence, rows, inverse)
         if FUSED_XENT and ops.linear_xent_ok(h, wb[0], wb[1]):
             return ops.linear_cross_entropy(h, wb[0], wb[1], targets, pad)
         return ops.cross_entropy(ops.logits(h, wb[0], wb[1]), targets, pad)
-    return ops.cross_entropy(model.forward_rows(sequence, rows), targets, pad)
+    return ops.cross_entropy(model.forward_rows(sequence, rows, inverse), targets, pad)
 
 
 def _single_target_cross_entropy(model, sequence, targets, pad: int) -> torch.Tensor:
@@ -361,12 +365,12 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         self._plan_table([batch[ITEM_SEQ_ENTRY_NAME]])
         ahead, self._rows_ahead = self._rows_ahead, None
         if ahead is not None and ahead[0] is target:
-            rows, row_targets = ahead[1], ahead[2]
+            rows, row_targets, inverse = ahead[1], ahead[2], ahead[3]
         else:
             rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)  # (reads the row count on the host)
-            row_targets = target.reshape(-1).index_select(0, rows)
+            row_targets, inverse = target.reshape(-1).index_select(0, rows), None
         loss = _rows_cross_entropy(self.model, build_model_input(self.model, self.item_tokenizer, batch), rows,
-                                   row_targets, pad)
+                                   row_targets, pad, inverse)
         self.log(LOG_KEY_TRAINING_LOSS, loss, prog_bar=False)
         return {"loss": loss}
 
@@ -382,7 +386,9 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         if target.dim() != 2:
             return
         rows = torch.nonzero(target.reshape(-1) != self.item_tokenizer.pad_token_id).squeeze(1)
-        self._rows_ahead = (target, rows, target.reshape(-1).index_select(0, rows))
+        # (with the rows' inverse map for the selection's backward, so the main stream never builds it)
+        self._rows_ahead = (target, rows, target.reshape(-1).index_select(0, rows),
+                            ops.row_inverse(rows, target.numel()))
 
     def _get_prediction_for_masked_item(self, batch, batch_idx=None) -> torch.Tensor:
         self._flush_table()

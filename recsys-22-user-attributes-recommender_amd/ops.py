@@ -596,8 +596,56 @@ def gather_rows(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
     ids = _i64(ids).reshape(-1)
     V, D = table.shape
     out = torch.empty(ids.numel(), D, device=table.device, dtype=torch.float32)
-    call("asme_gather_rows", ptr(ids), ids.numel(), ptr(_f32(table)), V, D, ptr(out), stream())
+    if ids.numel():
+        call("asme_gather_rows", ptr(ids), ids.numel(), ptr(_f32(table)), V, D, ptr(out), stream())
     return out
+
+
+def padding_mask(seq: torch.Tensor, pad: int) -> torch.Tensor:
+    """seq != pad as a bool tensor of seq's shape (asme_padding_mask)"""
+    seq = seq.contiguous()
+    if seq.data_ptr() % 16:  # a view at an odd offset: the kernel reads 16-B pairs
+        return seq.ne(pad)
+    out = torch.empty(seq.shape, device=seq.device, dtype=torch.bool)
+    call("asme_padding_mask", ptr(seq), seq.numel(), int(pad), ptr(out), stream())
+    return out
+
+
+def row_inverse(rows: torch.Tensor, n: int) -> torch.Tensor:
+    """inverse[t] = k where rows[k] = t, else -1 (int64, n entries) -- the map select_rows' backward reads"""
+    inv = torch.full((n,), -1, dtype=torch.int64, device=rows.device)
+    inv[rows] = torch.arange(rows.numel(), device=rows.device)
+    return inv
+
+
+class _SelectRowsFn(torch.autograd.Function):
+    """x2[rows] for distinct row indices (the masked / predicted positions of a flattened (B*L, d) representation)
+    on asme_gather_rows.  The backward is the same kernel reading the inverse map: row t of the dense (T, d) input
+    gradient is the gradient of the selected row that came from t, and a zero row (id -1, outside the table)
+    everywhere else -- one launch instead of a zero fill plus an index_add."""
+
+    @staticmethod
+    def forward(ctx, x2, rows, inverse):
+        ctx.save_for_backward(rows, inverse)
+        ctx.n = x2.shape[0]
+        return gather_rows(rows, x2)
+
+    @staticmethod
+    def backward(ctx, g):
+        rows, inverse = ctx.saved_tensors
+        if rows.numel() == 0:
+            return g.new_zeros(ctx.n, g.shape[-1]), None, None
+        if inverse is None:
+            inverse = row_inverse(rows, ctx.n)
+        return gather_rows(inverse, g.contiguous()), None, None
+
+
+def select_rows(x2: torch.Tensor, rows: torch.Tensor, inverse: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x2[rows] (x2: (T, d), rows: distinct indices) with the backward above; `inverse` (row_inverse(rows, T)) may be
+    built ahead, e.g. on the producer's side stream, else the backward builds it"""
+    if x2.shape[-1] > 512:  # wider than asme_gather_rows takes
+        return x2.index_select(0, rows)
+    return _SelectRowsFn.apply(x2.contiguous(), _i64(rows).reshape(-1), inverse)
 
 
 def bucket_by_owner(unique: torch.Tensor, world: int, count: Optional[torch.Tensor] = None):

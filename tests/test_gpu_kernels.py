@@ -741,3 +741,30 @@ def test_dense_table_grad_deterministic_with_hot_id(asme, dev):
     err = (g1.cpu().double() - want).abs().max().item()
     assert err <= 1e-5 * want.abs().max().item() + 1e-6, err
     assert not g1[2].any()  # an id that never occurs
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1023, 204800, 204803])
+def test_padding_mask_equals_ne(asme, dev, n):
+    """asme_padding_mask == sequence.ne(pad) (module_util.py:13-30), bit-exact, ragged tails included"""
+    seq = torch.randint(0, 6, (n,), device=dev, dtype=torch.int64)
+    for pad in (0, 5, -1):
+        got = asme.ops.padding_mask(seq, pad)
+        assert got.dtype == torch.bool and torch.equal(got, seq.ne(pad))
+    b = torch.randint(0, 4, (7, 31), device=dev, dtype=torch.int64)
+    assert torch.equal(asme.modules.get_padding_mask(b, asme.tokenization.Tokenizer(10)), b.ne(0))
+
+
+@pytest.mark.parametrize("T,d,n", [(204800, 128, 36966), (1000, 64, 1), (999, 128, 999), (16, 32, 0)])
+def test_select_rows_forward_backward(asme, dev, T, d, n):
+    """x2[rows] and its backward (dense (T, d) gradient, zero rows elsewhere) on asme_gather_rows, bit-exact against
+    index_select's autograd; with the inverse map built ahead and built by the backward"""
+    x = torch.randn(T, d, device=dev, requires_grad=True)
+    rows = torch.randperm(T, device=dev)[:n].sort().values
+    g = torch.randn(n, d, device=dev)
+    ref = x.index_select(0, rows)
+    (dref,) = torch.autograd.grad(ref, x, g)
+    for inverse in (None, asme.ops.row_inverse(rows, T)):
+        out = asme.ops.select_rows(x, rows, inverse)
+        assert torch.equal(out, ref)
+        (dx,) = torch.autograd.grad(out, x, g)
+        assert torch.equal(dx, dref)
