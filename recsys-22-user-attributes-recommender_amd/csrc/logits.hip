@@ -30,9 +30,10 @@
 //   dW, db  stationary = items, streamed = queries: P^T the same way;            dW^T += H^T P
 //   logits  stationary = queries, streamed = items: out = s + b
 //   fdh     stationary = queries, streamed = items: the training forward with dH folded in -- online (max, sum exp)
-//           per query per chunk and U^T += W^T exp(s + b - running max), rescaled when the running max grows (the
-//           flash-attention forward with the item table as V); a finish pass merges the chunks into lse, the loss
-//           and dH_raw = softmax(s) W - W[t] (0 for ignored rows), and the backward only scales it (x dloss / count)
+//           per query per chunk and U^T += W^T exp(s + b - reference max), rescaled when a tile's max passes the
+//           reference by more than 8 (the flash-attention forward with the item table as V); a finish pass merges
+//           the chunks into lse, the loss and dH_raw = softmax(s) W - W[t] (0 for ignored rows), and the backward
+//           only scales it (x dloss / count)
 // Work: training runs fdh (4 n|V|d FLOP) + dW (4) = 8 n|V|d executed for the 6 of a materialised head (stats + dH +
 // dW: 10); HBM bytes O((n+V)d).  Partial slabs of the chunks are summed in a fixed order: deterministic.
 #include "common.h"
@@ -259,19 +260,20 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
         const float* tf = mf + cur * kTS;
         const int* tt = mt + cur * kTS;
         // X = streamed rows 32 sub .. +31 (MFMA rows) x stationary rows (columns): row reads of the tile
+        auto score_a = [&](int sub, int ks) {
+            const int off = swz(32 * sub + r32, 2 * ks + h);
+            Bf3 A;
+            A.h = lds_b128(buf, off);
+            A.m = lds_b128(buf + kPlaneTile, off);
+            A.l = lds_b128(buf + 2 * kPlaneTile, off);
+            return A;
+        };
         auto score = [&](int sub) {
             floatx16 x;
 #pragma unroll
             for (int i = 0; i < 16; ++i) x[i] = 0.f;
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int off = swz(32 * sub + r32, 2 * ks + h);
-                Bf3 A;
-                A.h = lds_b128(buf, off);
-                A.m = lds_b128(buf + kPlaneTile, off);
-                A.l = lds_b128(buf + 2 * kPlaneTile, off);
-                x = mfma32_bf3(A, st[ks], x);
-            }
+            for (int ks = 0; ks < KS; ++ks) x = mfma32_bf3(score_a(sub, ks), st[ks], x);
             return x;
         };
         // P (unscaled) as the split B fragments of the two 16-row k steps:
@@ -297,22 +299,22 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
         // B fragment is P registers 8 s2 .. 8 s2 + 7 (element j = row 16 s2 + 8 (j >> 2) + 4 h + (j & 3)); the A
         // fragment comes from two transposed reads: 16-lane group (h, fh) reads rows 16 s2 + 4 h + q (+8) x
         // features 32 ft + 16 fh + 4 p4 .. +3 (lane 4q + p4 addresses one row), lane receives its feature
-        auto grad = [&](int sub, const Bf3 (&P)[2]) {
+        auto grad_a = [&](int sub, int s2, int ft) {
             const int fh = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+            const int rlo = 32 * sub + 16 * s2 + 4 * h + q, rhi = rlo + 8;
+            const int ch = 4 * ft + 2 * fh + (p4 >> 1);
+            const int olo = swz(rlo, ch) + 8 * (p4 & 1), ohi = swz(rhi, ch) + 8 * (p4 & 1);
+            Bf3 A;
+            A.h = cat8(lds_tr(buf, olo), lds_tr(buf, ohi));
+            A.m = cat8(lds_tr(buf + kPlaneTile, olo), lds_tr(buf + kPlaneTile, ohi));
+            A.l = cat8(lds_tr(buf + 2 * kPlaneTile, olo), lds_tr(buf + 2 * kPlaneTile, ohi));
+            return A;
+        };
+        auto grad = [&](int sub, const Bf3 (&P)[2]) {
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int rlo = 32 * sub + 16 * s2 + 4 * h + q, rhi = rlo + 8;
+            for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-                for (int ft = 0; ft < NFT; ++ft) {
-                    const int ch = 4 * ft + 2 * fh + (p4 >> 1);
-                    const int olo = swz(rlo, ch) + 8 * (p4 & 1), ohi = swz(rhi, ch) + 8 * (p4 & 1);
-                    Bf3 A;
-                    A.h = cat8(lds_tr(buf, olo), lds_tr(buf, ohi));
-                    A.m = cat8(lds_tr(buf + kPlaneTile, olo), lds_tr(buf + kPlaneTile, ohi));
-                    A.l = cat8(lds_tr(buf + 2 * kPlaneTile, olo), lds_tr(buf + 2 * kPlaneTile, ohi));
-                    y[ft] = mfma32_bf3(A, P[s2], y[ft]);
-                }
-            }
+                for (int ft = 0; ft < NFT; ++ft) y[ft] = mfma32_bf3(grad_a(sub, s2, ft), P[s2], y[ft]);
         };
         if constexpr (MODE == M_FDH) {
             floatx16 xs[2] = {score(0), score(1)};
@@ -335,15 +337,22 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
             }
             // one running max per query over both lane halves: both halves' P feed the same accumulators
             tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-            const float nm = fmaxf(run_max, tmax);
-            const float base = nm == -INFINITY ? 0.f : nm;  // nothing finite yet: P = 0, no NaN
-            const float alpha = run_max == -INFINITY ? 0.f : __expf(run_max - nm);
+            // lazy rescale: the reference max moves (and the 64 accumulators are rescaled) only when some query's
+            // tile max exceeds it by more than 8 -- P = exp(s - ref) then stays <= e^8, exact in the bf16x6 split
+            // and far from fp32 overflow; the (ref, sum, U) triple it leaves is the same softmax state.  The rescale
+            // had run every tile (64 multiplies on accumulators held in AGPRs, moved through VGPRs): fwd_dh
+            // 2.71 -> 2.61 ms at the C3 shape (tools/xent_bench.py, same box)
+            if (__ballot(!(tmax <= run_max + 8.f)) != 0ull) {
+                const float nm = fmaxf(run_max, tmax);
+                const float alpha = run_max == -INFINITY ? 0.f : __expf(run_max - nm);
 #pragma unroll
-            for (int f = 0; f < NFT; ++f)
+                for (int f = 0; f < NFT; ++f)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) y[f][i] *= alpha;
-            run_sum *= alpha;
-            run_max = nm;
+                    for (int i = 0; i < 16; ++i) y[f][i] *= alpha;
+                run_sum *= alpha;
+                run_max = nm;
+            }
+            const float base = run_max == -INFINITY ? 0.f : run_max;  // nothing finite yet: P = 0, no NaN
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) {
 #pragma unroll

@@ -127,3 +127,32 @@ def test_linear_xent_training_and_weight_only_paths(asme, dev, h_grad):
         assert hd.grad is None
     assert _rel(Wd.grad, Wc.grad) < 1e-4
     assert _rel(bd.grad, bc.grad) < 1e-4
+
+
+@pytest.mark.parametrize("order", ["rising", "falling", "wide"])
+def test_linear_xent_running_max_moves(asme, dev, order):
+    """the training form's online softmax (running max per query over the item tiles, the accumulators rescaled
+    only when a tile's max exceeds the reference by more than e^8): item biases rising along the catalogue move the
+    maximum at nearly every tile, falling ones never after the first, wide-range logits (|s| up to ~60) mix both --
+    loss, dH, dW, db against fp64"""
+    torch.manual_seed(11)
+    n, V, d = 600, 5003, 128
+    h, W = torch.randn(n, d) * 0.4, torch.randn(V, d) * 0.4
+    if order == "rising":
+        b = torch.linspace(-40.0, 40.0, V)
+    elif order == "falling":
+        b = torch.linspace(40.0, -40.0, V)
+    else:
+        h, b = h * 6.0, torch.randn(V) * 8.0
+    t = torch.randint(0, V, (n,))
+    t[::9] = 0
+    hc, Wc, bc = (x.double().requires_grad_(True) for x in (h, W, b))
+    ref = F.cross_entropy(F.linear(hc, Wc, bc), t, ignore_index=0)
+    ref.backward()
+    hd, Wd, bd = (x.to(dev).requires_grad_(True) for x in (h, W, b))
+    loss = asme.ops.linear_cross_entropy(hd, Wd, bd, t.to(dev), 0)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) / abs(ref.item()) < 1e-5
+    assert _rel(hd.grad, hc.grad) < 1e-4
+    assert _rel(Wd.grad, Wc.grad) < 1e-4
+    assert _rel(bd.grad, bc.grad) < 1e-4
