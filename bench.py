@@ -526,7 +526,7 @@ def main():
                                    "asme_sampled_logits_fwd", "asme_sampled_logits_bwd", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
                                    "asme_ws_linear", "asme_posneg_sample", "asme_table_grad_reduce_apply",
-                                   "asme_dedup_ids", "asme_occurrence_csr"])
+                                   "asme_dedup_ids", "asme_dedup_ids_segments", "asme_occurrence_csr"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -607,6 +607,8 @@ def main():
         # the step's n = 3T table ids: read once, the slot map probed per id and written per unique row, the
         # inverse (n) and the unique ids (U) written
         "asme_dedup_ids": ("hbm", 3 * T * (8 + 4 + 8) + U * (8 + 4)),
+        # (the training step's form: the three id tensors read in place as segments, same bytes)
+        "asme_dedup_ids_segments": ("hbm", 3 * T * (8 + 4 + 8) + U * (8 + 4)),
         # occurrence CSR: the inverse read, order + sorted slot written (int32), the U + 1 segment offsets
         "asme_occurrence_csr": ("hbm", 3 * T * (8 + 4 + 4) + 4 * (U + 1)),
         # ordered per-row sums + the lazy Adam step: the three contributions' rows (embedding d_rows, h for the
@@ -622,7 +624,9 @@ def main():
         with open(tp) as f:
             tj = json.load(f)
         if tj.get("config") == {"batch": B, "seq_len": L, "items": args.items, "dim": d, "layers": args.layers}:
-            traffic = tj.get("bytes_per_launch", {})
+            traffic = dict(tj.get("bytes_per_launch", {}))
+            if "asme_dedup_ids" in traffic:  # tools/pmc_traffic.py attributes the segmented dedup's kernels to it
+                traffic.setdefault("asme_dedup_ids_segments", traffic["asme_dedup_ids"])
     mb = committed_profile("mfma_busy.json", {"batch": B, "seq_len": L, "items": args.items, "dim": d,
                                               "layers": args.layers})
     rooflines = roofline_entries(kstats, work, traffic, mb.get("mfma_busy"))

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void lazy_catch_up_kernel(const int64_t* __res
     const int64_t n = count ? (int64_t)*count : cap;
     if (s >= n || s >= cap) return;
     const int64_t r = rows ? rows[s] : s;
-    const int32_t t0 = last_step[r];
+    const int32_t t0 = lazy_from(last_step[r], upto);
     if (t0 >= upto) return;
     float P[VPL], M[VPL], Vv[VPL];
 #pragma unroll
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void lazy_catch_up_v4_kernel(const int64_t* __
     const int64_t n = count ? (int64_t)*count : cap;
     const bool in_range = s < n && s < cap;
     const int64_t r = in_range ? (rows ? rows[s] : s) : 0;
-    const int32_t t0 = in_range ? last_step[r] : upto;
+    const int32_t t0 = in_range ? lazy_from(last_step[r], upto) : upto;
     // The rows of a wave have different last steps: replay over the wave's whole range with a uniform step
     // counter (hist[t] is then a scalar load, not a per-lane gather) and let each lane apply only its own
     // steps.  All lanes of a row agree, so the per-row result is exactly the per-row replay.
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void lazy_row_kernel(const int64_t* __restrict
         M[j] = float2v{b.x, b.y};
         Vv[j] = float2v{c.x, c.y};
     }
-    const int32_t t0 = __builtin_amdgcn_readfirstlane(last_step[r]);
+    const int32_t t0 = lazy_from(__builtin_amdgcn_readfirstlane(last_step[r]), upto);
     if (!STAGE && t0 >= upto) return;
     for (int32_t t = t0 + 1; t <= upto; ++t) {
         const AdamHyper hp = hist[t];
@@ -402,9 +402,24 @@ __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restric
     if (base >= n) return;  // wave-uniform
     const int nr = (int)(n - base < RPW ? n - base : RPW);
     const int64_t my_r = lane < nr ? (rows ? rows[base + lane] : base + lane) : 0;
-    const int32_t my_t = lane < nr ? last_step[my_r] : upto;
-    auto row_of = [&](int i) -> int64_t {  // slots past the end re-read the last row (never stored)
-        const int k = i < nr ? i : nr - 1;
+    const int32_t my_t = lane < nr ? lazy_from(last_step[my_r], upto) : upto;
+    // the slots this wave works on, in slot order: every slot when staging (each is written to the staged rows),
+    // else only the rows behind `upto` -- current rows and rows at rest are neither read nor written by the flush
+    const uint64_t live = __ballot(lane < nr && (STAGE || my_t < upto));
+    if (live == 0) return;  // wave-uniform
+    const int nl = __popcll(live);
+    int ln[RPW];  // lane (slot - base) of the i-th live slot; past the last one: the last one again (never stored)
+    {
+        uint64_t mm = live;
+        const int last = 63 - __clzll(live);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            ln[i] = mm ? __ffsll((unsigned long long)mm) - 1 : last;
+            mm &= mm - 1;
+        }
+    }
+    auto row_of = [&](int i) -> int64_t {
+        const int k = ln[i];
         if (!rows) return base + k;
         const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_r, k);
         const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)my_r >> 32), k);
@@ -430,8 +445,8 @@ __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restric
     for (int i = 0; i < RPW; ++i) {
         if (i + PF - 1 < RPW) load(i + PF - 1, (i + PF - 1) % PF);
         const int sl = i % PF;
-        const int32_t t0 = __builtin_amdgcn_readlane(my_t, i);
-        if (i < nr && (STAGE || t0 < upto)) {
+        const int32_t t0 = __builtin_amdgcn_readlane(my_t, ln[i]);
+        if (i < nl) {
             for (int32_t t = t0 + 1; t <= upto; ++t) {
                 const AdamHyper hp = hist[t];
 #pragma unroll
@@ -442,7 +457,7 @@ __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restric
                         adam_decay2(P[sl][j], M[sl][j], Vv[sl][j], hp);
                 }
             }
-            const int64_t orow = STAGE ? base + i : row_of(i);
+            const int64_t orow = STAGE ? base + ln[i] : row_of(i);
             float* op = STAGE ? sp : p;
             float* om = STAGE ? sm : m;
             float* ov = STAGE ? sv : v;
@@ -506,7 +521,7 @@ __global__ __launch_bounds__(256) void lazy_stage_v4_kernel(const int64_t* __res
         M = *reinterpret_cast<const float4*>(m + off);
         Vv = *reinterpret_cast<const float4*>(v + off);
     }
-    const int32_t t0 = in_range ? last_step[r] : upto;
+    const int32_t t0 = in_range ? lazy_from(last_step[r], upto) : upto;
     int32_t t_lo = t0;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) t_lo = min(t_lo, __shfl_xor(t_lo, o, 64));

@@ -69,4 +69,13 @@ __device__ __forceinline__ void adam_decay2(float2v& p, float2v& m, float2v& v, 
     p = fma2(bc2(hp.neg_step_size), m * r, p);
 }
 
+// A row AT REST: its moments are exactly +0 and every step it missed ran without weight decay -- a fresh table's
+// rows before their first gradient (the lazy state marks them with last_step = kRestStep while the group's weight
+// decay is 0, ops.LazyTableState).  The dense zero-gradient update of such a row is the identity bit for bit
+// (adam_elem: m' = fma(c, +0 - +0, +0) = +0, v' = fma(b2, +0, +0) = +0, denom = eps, p' = fma(s, +0 * rcp(eps), p)
+// = p), so the row is current at every step: the replay kernels take its last step as `upto` (no replay, nothing
+// read for it by the flush, last_step left at rest until a real gradient step writes it).
+constexpr int32_t kRestStep = -1;
+__device__ __forceinline__ int32_t lazy_from(int32_t last, int32_t upto) { return last < 0 ? upto : last; }
+
 }  // namespace asme

@@ -66,7 +66,11 @@ __device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s 
 #define ASME_WS_NT_MIN_N 384
 #endif
 constexpr int kNtMinN = ASME_WS_NT_MIN_N;
+#ifndef ASME_WS_DIAG
+#define ASME_WS_DIAG 0  // diagnostic builds (tools/ws_ab.py): 1 no MFMA, 2 no stores, 3 no W reads in the loop, 4 no X
+#endif
 __device__ __forceinline__ void bstore(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
+    if (ASME_WS_DIAG == 2) off = kDrop;
     const u32v4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
     if (nt)  // (wave-uniform)
         __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 2);
@@ -277,15 +281,25 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             // each feature tile's six MFMAs, then its next-block W read into the registers they consumed
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
+#if ASME_WS_DIAG != 1
                 acc[ct] = mfma_bf3(wc[ct], xs, acc[ct]);
+#else
+                acc[ct][0] += (float)xs.h[0] + (float)wc[ct].h[0];
+#endif
+#if ASME_WS_DIAG != 3
                 wc[ct] = wload(ct, kbn);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
             }
             // refill the slot just consumed: block kb + RD of this tile or of the next one (unconditional,
             // so the vmcnt bookkeeping stays exact; past the last tile it re-reads the last one)
             const float* src = (kb + RD < NKB ? rc : rn) + ((kb + RD) % NKB) * 32;
+#if ASME_WS_DIAG != 4
             ring[2 * d] = *reinterpret_cast<const float4*>(src);
             ring[2 * d + 1] = *reinterpret_cast<const float4*>(src + 4);
+#else
+            ring[2 * d].x += (float)(uintptr_t)src;
+#endif
             // the next block's X terms
             const int dn = (kb + 1) % RD;
             xs = split_bf3(ring[2 * dn], ring[2 * dn + 1]);

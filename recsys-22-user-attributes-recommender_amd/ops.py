@@ -28,6 +28,8 @@ _EMB_PARTIALS = 2048  # the embedding backward's (2x the waves in flight: 124 ->
 STAGE_ROWS = True
 # reduce the table gradient and apply the staged Adam step in one pass when nothing else needs the gradient rows
 FUSED_APPLY = os.environ.get("ASME_FUSED_APPLY", "1") != "0"
+# a fresh table without weight decay starts with its rows at rest (LazyTableState.start); 0: A/B switch
+REST_ROWS = os.environ.get("ASME_REST_ROWS", "1") != "0"
 
 
 def new_seed(p: float) -> int:
@@ -81,6 +83,9 @@ class TableGrad:
             self.applied = None
 
 
+REST_STEP = -1  # last_step of a row at rest (csrc/adam_math.h kRestStep)
+
+
 class LazyTableState:
     """Exact lazy dense Adam for the item table (asme_lazy_adam_*): rows are caught up to the current
     step only when read (before a forward that gathers them, or in flush()).  Bit-identical to updating
@@ -91,8 +96,20 @@ class LazyTableState:
         self.last_step = torch.zeros(param.shape[0], dtype=torch.int32, device=param.device)
         self.hist = torch.zeros(1024, 8, dtype=torch.float32, device=param.device)
         self.step = 0
+        self.rest = False  # some rows may be at rest (last_step == REST_STEP)
+
+    def start(self, step: int, fresh: bool, wd: float):
+        """every row is current up to `step`; `fresh` (moments just created, all +0) without weight decay: every row
+        starts AT REST (last_step = REST_STEP, csrc/adam_math.h kRestStep) -- its zero-gradient dense update is the
+        identity bit for bit, so no kernel replays, reads or writes it until its first gradient"""
+        self.step = step
+        self.rest = bool(REST_ROWS and fresh and wd == 0.0)
+        self.last_step.fill_(REST_STEP if self.rest else step)
 
     def record(self, step: int, lr, b1, b2, eps, wd):
+        if wd != 0.0 and self.rest:  # rows at rest are current up to the previous step; from now on they decay
+            self.last_step.masked_fill_(self.last_step < 0, self.step)
+            self.rest = False
         cap = self.hist.shape[0]
         while step >= cap:  # a resumed run can start at any step
             cap *= 2

@@ -89,14 +89,14 @@ class FusedAdam(torch.optim.Optimizer):
                     if p.grad is not None:
                         raise RuntimeError("item table got a dense gradient while its sparse plan is active "
                                            "(tied / full-catalogue heads need table_grad='dense')")
+                    fresh = not self.state[p]  # moments created now: all +0
                     st = self._state(p)
                     st["step"] += 1
                     V, D = p.shape
                     if self.lazy_table:
                         if tg.lazy is None:
                             tg.lazy = LazyTableState(p, st["exp_avg"], st["exp_avg_sq"])
-                            tg.lazy.step = st["step"] - 1
-                            tg.lazy.last_step.fill_(st["step"] - 1)  # every row is current up to now
+                            tg.lazy.start(st["step"] - 1, fresh, wd)  # every row is current up to now
                         elif reapply:  # no forward caught these rows up this time
                             tg.lazy.catch_up(plan.unique, plan.count, plan.capacity)
                         tg.lazy.record(st["step"], lr, b1, b2, eps, wd)

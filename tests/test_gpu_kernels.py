@@ -492,6 +492,54 @@ def test_lazy_adam_bit_exact_vs_dense(asme, dev, V, D):
     assert torch.equal(p_lazy.detach(), snapshot)
 
 
+@pytest.mark.parametrize("D", [128, 64])
+def test_lazy_adam_rows_at_rest_bit_exact(asme, dev, D):
+    """A fresh table without weight decay starts AT REST (last_step = REST_STEP): rows never given a gradient are
+    neither replayed nor touched by stage / flush, and the result is still the dense update bitwise -- including
+    the switch to weight decay mid-run (rest rows then decay from the step they were current at)."""
+    torch.manual_seed(7)
+    V, T, steps = 4001, 200, 6
+    base = torch.randn(V, D, device=dev)
+    base[5] = -0.0  # signed zeros survive the identity update
+    p_lazy = torch.nn.Parameter(base.clone())
+    p_lazy._asme_table_grad = asme.ops.TableGrad()
+    p_eager = torch.nn.Parameter(base.clone())
+    p_eager._asme_table_grad = asme.ops.TableGrad()
+    o_lazy = asme.FusedAdam([p_lazy], lr=3e-3, betas=(0.9, 0.998), weight_decay=0.0, lazy_table=True)
+    o_eager = asme.FusedAdam([p_eager], lr=3e-3, betas=(0.9, 0.998), weight_decay=0.0, lazy_table=False)
+    map_l = torch.full((V,), -1, dtype=torch.int32, device=dev)
+    map_e = torch.full((V,), -1, dtype=torch.int32, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    for step in range(steps):
+        if step == 4:  # weight decay switched on: rows at rest become ordinary deferred rows
+            for o in (o_lazy, o_eager):
+                o.param_groups[0]["weight_decay"] = 1e-2
+        ids = torch.randperm(V // 3, device=dev, generator=gen)[:T] + 7  # rows 0..6 and the top 2/3 never touched
+        rows = torch.randn(T, D, device=dev, generator=gen)
+        for p, mp, opt in ((p_lazy, map_l, o_lazy), (p_eager, map_e, o_eager)):
+            plan = asme.ops.SparseTablePlan(p, [ids], mp)
+            if p is p_lazy:
+                src, sid = plan.gather_source(p_lazy.detach(), ids)
+                assert torch.equal(src[sid], p_eager.detach()[ids])
+            asme._lib.call("asme_scatter_add_rows", rows.data_ptr(), plan.inverse_of(ids).data_ptr(), T, D,
+                           plan.grad_rows.data_ptr(), plan.capacity, 1.0, asme._lib.stream())
+            p._asme_table_grad.plan = plan
+            opt.step()
+        if step == 2:  # mid-run flush with rows at rest
+            lazy = p_lazy._asme_table_grad.lazy
+            assert lazy.rest and int((lazy.last_step < 0).sum()) > V // 2
+            o_lazy.flush()
+            assert int((lazy.last_step < 0).sum()) > V // 2  # the flush left them at rest
+            assert torch.equal(p_lazy.detach(), p_eager.detach())
+    o_lazy.flush()
+    assert torch.equal(p_lazy.detach(), p_eager.detach())
+    assert torch.equal(torch.signbit(p_lazy.detach()[5]), torch.signbit(p_eager.detach()[5]))
+    st_l, st_e = o_lazy.state[p_lazy], o_eager.state[p_eager]
+    assert torch.equal(st_l["exp_avg"], st_e["exp_avg"]) and torch.equal(st_l["exp_avg_sq"], st_e["exp_avg_sq"])
+    lazy = p_lazy._asme_table_grad.lazy
+    assert not lazy.rest and bool((lazy.last_step == steps).all())
+
+
 def test_sasrec_sparse_lazy_matches_dense_training(asme, dev):
     """Three SASRec-neg training steps: table_grad='sparse' (dedup + lazy exact Adam) vs 'dense'
     (dense gradient + dense Adam) give the same parameters (fp32 summation order differs)."""
