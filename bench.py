@@ -521,7 +521,8 @@ def main():
     # per-kernel device time of the dominant kernel (HIP events on the launching stream)
     timer = asme._lib.KernelTimer([] if args.kernel_events == "off" else [
                                    "asme_adam_rows_step", "asme_attention_fwd", "asme_attention_bwd",
-                                   "asme_embedding_fwd", "asme_embedding_bwd", "asme_lazy_adam_catch_up",
+                                   "asme_embedding_fwd", "asme_embedding_bwd", "asme_embedding_ln_fwd",
+                                   "asme_embedding_ln_bwd", "asme_lazy_adam_catch_up",
                                    "asme_lazy_adam_apply", "asme_lazy_adam_stage", "asme_lazy_adam_apply_staged",
                                    "asme_sampled_logits_fwd", "asme_sampled_logits_bwd", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
@@ -588,6 +589,10 @@ def main():
         "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),
         "asme_embedding_fwd": ("hbm", T * 8 + 2 * T * d * 4 + T * 16),
         "asme_embedding_bwd": ("hbm", T * 8 + 3 * T * d * 4 + T * 16),
+        # + block 0's input LayerNorm: its output row and (mean, rstd) written; the backward reads the LN output's
+        # gradient and the statistics too (the unfused LayerNorm pass re-read the embedding output instead)
+        "asme_embedding_ln_fwd": ("hbm", T * 8 + 3 * T * d * 4 + T * 16 + T * 8),
+        "asme_embedding_ln_bwd": ("hbm", T * 8 + 4 * T * d * 4 + T * 16 + T * 8),
         "asme_lazy_adam_apply": ("hbm", U * 8 + U * d * 4 + 6 * U * d * 4 + U * 4),
         "asme_lazy_adam_catch_up": ("hbm", U * 8 + 6 * U * d * 4 + 2 * U * 4),
         # staged form: the same rows read (random) and written to the compact staging rows (slot order); the apply

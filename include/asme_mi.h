@@ -58,6 +58,25 @@ int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, co
                        const uint8_t* keep_mask, const float* dout, const float* stats, float* d_rows,
                        float* d_extra, float* partials, int64_t n_partials, void* stream);
 int asme_embedding_bwd_partials_count(void);
+/* asme_embedding_fwd + the first transformer block's input LayerNorm (transformer_layers.py:251-258, the
+ * SublayerConnection norm of block 0, which TransformerLayer applies to the embedding output) on the same rows:
+ * out = the embedding output (the residual stream), ln3_out = LN3(out), ln3_stats (T, 2) = (mean, rstd).
+ * Replaces asme_embedding_fwd followed by asme_layernorm_fwd on its output.  dim % 4 == 0. */
+int asme_embedding_ln_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
+                          int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float ln1_eps,
+                          float p1, uint64_t seed1, const float* extra, const float* ln2_w, const float* ln2_b,
+                          float ln2_eps, float p2, uint64_t seed2, const float* ln3_w, const float* ln3_b,
+                          float ln3_eps, float* out, float* stats, float* ln3_out, float* ln3_stats,
+                          uint8_t* keep_mask, int* err_flag, void* stream);
+/* Backward of asme_embedding_ln_fwd (replaces asme_layernorm_bwd_add + asme_embedding_bwd): dout = gradient of
+ * `out` through the residual stream, dln = gradient of ln3_out; partials (n_partials, 6 * dim) = column partials
+ * of LN1 w / b, LN2 w / b, LN3 w / b.  ln2_b is required with ln2_w. */
+int asme_embedding_ln_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
+                          int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float p1,
+                          uint64_t seed1, const float* extra, const float* ln2_w, const float* ln2_b, float p2,
+                          uint64_t seed2, const float* ln3_w, const float* ln3_stats, const uint8_t* keep_mask,
+                          const float* dout, const float* dln, const float* stats, float* d_rows, float* d_extra,
+                          float* partials, int64_t n_partials, void* stream);
 /* nn.Embedding dense backward (autograd embedding_dense_backward): grad[ids[r]] += scale * rows[r]
  * (hardware fp32 atomics; ids outside [0, vocab) are skipped). */
 int asme_scatter_add_rows(const float* rows, const int64_t* ids, int64_t n_rows, int64_t dim, float* grad,

@@ -25,6 +25,10 @@ SIGNATURES = {
     "asme_embedding_fwd": [p, i64, i64, p, i64, i64, p, p, p, f32, f32, u64, p, p, p, f32, f32, u64, p, p, p, p, p],
     "asme_embedding_bwd": [p, i64, i64, p, i64, i64, p, p, p, f32, u64, p, p, f32, u64, p, p, p, p, p, p, i64, p],
     "asme_embedding_bwd_partials_count": [],
+    "asme_embedding_ln_fwd": [p, i64, i64, p, i64, i64, p, p, p, f32, f32, u64, p, p, p, f32, f32, u64, p, p, f32, p, p,
+                              p, p, p, p, p],
+    "asme_embedding_ln_bwd": [p, i64, i64, p, i64, i64, p, p, p, f32, u64, p, p, p, f32, u64, p, p, p, p, p, p, p,
+                              p, p, i64, p],
     "asme_scatter_add_rows": [p, p, i64, i64, p, i64, f32, p],
     "asme_scatter_rows": [p, p, p, i64, i64, p, i64, p],
     "asme_position_grad": [p, i64, i64, i64, p, i64, p, i32, p],

@@ -195,13 +195,26 @@ __device__ __forceinline__ uint32_t emb_keep_bits(uint64_t seed, uint64_t chunk,
 
 __host__ __device__ inline uint64_t emb_seed(uint64_t s1, uint64_t s2) { return s1 ^ (s2 * 0x9E3779B97F4A7C15ull); }
 
-template <class R, int kEmbK>  // kEmbK: tokens per lane group
+// LN3 (the fused next LayerNorm): the first transformer block's input norm applied to the embedding output in the
+// same pass (transformer_layers.py:251-258 SublayerConnection: x + dropout(sublayer(norm(x))) of block 0), so the
+// block reads `out3` and keeps `out` as its residual stream: no separate LayerNorm launch re-reading the rows.
+struct EmbLn3 {
+    const float* w;
+    const float* b;
+    float eps;
+    float* out;    // forward: the normalised rows (T, D)
+    float* stats;  // (T, 2): mean, rstd
+    const float* dln;  // backward: gradient of `out` (the gradient of the embedding output itself is `dout`)
+    const float* b2;   // backward: LN2's bias (the embedding output is recomputed through LN2's affine)
+};
+
+template <class R, int kEmbK, bool LN3>  // kEmbK: tokens per lane group
 __global__ __launch_bounds__(256) void emb_fwd4_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float eps1, float p1,
     const float* __restrict__ extra, const float* __restrict__ w2, const float* __restrict__ b2, float eps2,
     float p2, uint64_t seed, float* __restrict__ out, float* __restrict__ stats, uint8_t* __restrict__ keep,
-    int* __restrict__ err) {
+    int* __restrict__ err, EmbLn3 l3) {
     static_assert(R::W == 4, "4-wide layout only");
     const int lane = threadIdx.x & 63, sub = lane % R::LPR;
     const int64_t t0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * R::RPW * kEmbK + lane / R::LPR;
@@ -295,6 +308,14 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
         }
         row_store<R>(out + t * D, sub, D, x[k]);
         if (sub == 0 && stats) *reinterpret_cast<float4*>(stats + t * 4) = make_float4(m1, r1, m2, r2);
+        if constexpr (LN3) {
+            float m3, r3;
+            row_ln_stats<R>(x[k], sub, D, l3.eps, m3, r3);
+            row_normalise<R>(x[k], sub, D, m3, r3, tmp);
+            row_affine<R>(tmp, sub, D, l3.w, l3.b, x[k]);
+            row_store<R>(l3.out + t * D, sub, D, x[k]);
+            if (sub == 0) *reinterpret_cast<float2*>(l3.stats + t * 2) = make_float2(m3, r3);
+        }
     }
 }
 
@@ -306,18 +327,22 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 #else
 #define ASME_EMB_BWD_ATTR
 #endif
-template <class R, int kPass>  // kPass: tokens per lane group per grid-stride pass
+// LN3: `dout` is the gradient of the embedding output through the residual stream, l3.dln that of the fused
+// LayerNorm's output; the output row is recomputed (LN1 / dropout / LN2 affine / dropout, from the stored statistics
+// and keep bits) for the LN3 backward, whose parameter gradients are accumulators 4 and 5 of the partials.
+template <class R, int kPass, bool LN3>  // kPass: tokens per lane group per grid-stride pass
 __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1,
     const float* __restrict__ extra, const float* __restrict__ w2, float p2, uint64_t seed,
     const uint8_t* __restrict__ keep, const float* __restrict__ dout, const float* __restrict__ stats,
-    float* __restrict__ d_rows, float* __restrict__ d_extra, float* __restrict__ partials) {
+    float* __restrict__ d_rows, float* __restrict__ d_extra, float* __restrict__ partials, EmbLn3 l3) {
     static_assert(R::W == 4, "4-wide layout only");
+    constexpr int NACC = LN3 ? 6 : 4;
     const int lane = threadIdx.x & 63, sub = lane % R::LPR, wave = threadIdx.x >> 6;
-    float acc[4][R::NV][R::W];
+    float acc[NACC][R::NV][R::W];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) row_zero<R>(acc[k]);
+    for (int k = 0; k < NACC; ++k) row_zero<R>(acc[k]);
     const bool drop = p1 > 0.f || p2 > 0.f;
     const uint32_t th1 = emb_thresh(p1), th2 = emb_thresh(p2);
     const float k1 = 1.f / (1.f - p1), k2 = 1.f / (1.f - p2);
@@ -325,7 +350,8 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
          tb - lane / R::LPR < T; tb += (int64_t)gridDim.x * kWavesPerBlock * R::RPW * kPass) {
         int64_t id[kPass];
         float4 st[kPass];
-        RowVals<R> x[kPass], g[kPass], q[kPass];
+        float2 st3[kPass];
+        RowVals<R> x[kPass], g[kPass], q[kPass], dl[kPass];
 #pragma unroll
         for (int k = 0; k < kPass; ++k) {
             const int64_t t = tb + (int64_t)k * R::RPW;
@@ -340,6 +366,10 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
             if (pos) row_load<R>(pos + (tt % L) * D, sub, D, q[k]);
             row_load<R>(dout + tt * D, sub, D, g[k]);
             st[k] = *reinterpret_cast<const float4*>(stats + tt * 4);
+            if constexpr (LN3) {
+                row_load<R>(l3.dln + tt * D, sub, D, dl[k]);
+                st3[k] = *reinterpret_cast<const float2*>(l3.stats + tt * 2);
+            }
         }
 #pragma unroll
         for (int k = 0; k < kPass; ++k) {
@@ -348,6 +378,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
             if (!live) {
                 row_zero<R>(x[k]);
                 row_zero<R>(g[k]);
+                if constexpr (LN3) row_zero<R>(dl[k]);
             } else if (pos) {
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
@@ -383,6 +414,38 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                         for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
                 }
                 row_normalise<R>(x[k], sub, D, st[k].z, st[k].w, xh2);
+            }
+            if constexpr (LN3) {
+                // the embedding output drop2(LN2(z)) (or drop2(z) without LN2), then g += LN3 backward of dln
+                RowVals<R> xo, xh3, gl;
+                if (w2) {
+                    row_affine<R>(xh2, sub, D, w2, l3.b2, xo);
+                } else {
+                    const bool ex = extra && live;
+                    if (ex) row_load<R>(extra + t * D, sub, D, q[k]);
+#pragma unroll
+                    for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) xo[j][i] = x[k][j][i] + (ex ? q[k][j][i] : 0.f);
+                }
+                if (p2 > 0.f)
+#pragma unroll
+                    for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) xo[j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
+                row_normalise<R>(xo, sub, D, st3[k].x, st3[k].y, xh3);
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc[4][j][i] += dl[k][j][i] * xh3[j][i];
+                        acc[5][j][i] += dl[k][j][i];
+                    }
+                row_ln_bwd<R>(dl[k], xh3, l3.w, st3[k].y, sub, D, gl);
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) g[k][j][i] += gl[j][i];
             }
             if (p2 > 0.f)
 #pragma unroll
@@ -427,7 +490,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
             }
         }
     }
-    if (partials) write_row_partials<R, 4, kWavesPerBlock>(acc, lane, wave, D, partials);
+    if (partials) write_row_partials<R, NACC, kWavesPerBlock>(acc, lane, wave, D, partials);
 }
 
 template <int VPL>
@@ -621,11 +684,12 @@ int with_emb_layout(int64_t D, F&& f, bool lpr16 = ASME_EMB_LPR16) {
     return with_row_layout(D, f);
 }
 
-ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
-                                int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
-                                const float* ln1_b, float ln1_eps, float p1, uint64_t seed1, const float* extra,
-                                const float* ln2_w, const float* ln2_b, float ln2_eps, float p2, uint64_t seed2,
-                                float* out, float* stats, uint8_t* keep_mask, int* err_flag, void* stream) {
+namespace {
+int embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
+                  int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float ln1_eps, float p1,
+                  uint64_t seed1, const float* extra, const float* ln2_w, const float* ln2_b, float ln2_eps, float p2,
+                  uint64_t seed2, float* out, float* stats, uint8_t* keep_mask, int* err_flag, const EmbLn3* l3,
+                  void* stream) {
     ASME_CHECK_ARG(ids && table && out && stats, "asme_embedding_fwd: null pointer");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && seq_len >= 1 && n_tokens >= 0, "asme_embedding_fwd: bad shape");
     ASME_CHECK_ARG(p1 >= 0.f && p1 < 1.f && p2 >= 0.f && p2 < 1.f, "asme_embedding_fwd: dropout p must be in [0,1)");
@@ -635,10 +699,17 @@ ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t se
             if constexpr (R::W == 4) {
                 constexpr int K = ASME_EMB_K;  // tokens per lane group
                 const int64_t rows = (int64_t)kWavesPerBlock * R::RPW * K;
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K>), dim3((unsigned)((n_tokens + rows - 1) / rows)),
-                                   dim3(256), 0, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim,
-                                   pos_table, ln1_w, ln1_b, ln1_eps, p1, extra, ln2_w, ln2_b, ln2_eps, p2,
-                                   emb_seed(seed1, seed2), out, stats, keep_mask, err_flag);
+                const dim3 grid((unsigned)((n_tokens + rows - 1) / rows));
+                if (l3)
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K, true>), grid, dim3(256), 0,
+                                       (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table,
+                                       ln1_w, ln1_b, ln1_eps, p1, extra, ln2_w, ln2_b, ln2_eps, p2,
+                                       emb_seed(seed1, seed2), out, stats, keep_mask, err_flag, *l3);
+                else
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K, false>), grid, dim3(256), 0,
+                                       (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table,
+                                       ln1_w, ln1_b, ln1_eps, p1, extra, ln2_w, ln2_b, ln2_eps, p2,
+                                       emb_seed(seed1, seed2), out, stats, keep_mask, err_flag, EmbLn3{});
             } else {
                 const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
                 hipLaunchKernelGGL(emb_fwd_kernel<R>, dim3((unsigned)((n_tokens + rows - 1) / rows)), dim3(256), 0,
@@ -650,20 +721,46 @@ ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t se
         return -1;
     ASME_LAUNCH_CHECK("asme_embedding_fwd");
 }
+}  // namespace
+
+ASME_API int asme_embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
+                                int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
+                                const float* ln1_b, float ln1_eps, float p1, uint64_t seed1, const float* extra,
+                                const float* ln2_w, const float* ln2_b, float ln2_eps, float p2, uint64_t seed2,
+                                float* out, float* stats, uint8_t* keep_mask, int* err_flag, void* stream) {
+    return embedding_fwd(ids, n_tokens, seq_len, table, vocab, dim, pos_table, ln1_w, ln1_b, ln1_eps, p1, seed1, extra,
+                         ln2_w, ln2_b, ln2_eps, p2, seed2, out, stats, keep_mask, err_flag, nullptr, stream);
+}
+
+// asme_embedding_fwd + the first transformer block's input LayerNorm on the output rows (ln3_out = LN3(out),
+// ln3_stats (T, 2) = mean, rstd); dim % 4 == 0
+ASME_API int asme_embedding_ln_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
+                                   int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
+                                   const float* ln1_b, float ln1_eps, float p1, uint64_t seed1, const float* extra,
+                                   const float* ln2_w, const float* ln2_b, float ln2_eps, float p2, uint64_t seed2,
+                                   const float* ln3_w, const float* ln3_b, float ln3_eps, float* out, float* stats,
+                                   float* ln3_out, float* ln3_stats, uint8_t* keep_mask, int* err_flag,
+                                   void* stream) {
+    ASME_CHECK_ARG(ln3_w && ln3_b && ln3_out && ln3_stats, "asme_embedding_ln_fwd: null pointer");
+    ASME_CHECK_ARG(dim % 4 == 0, "asme_embedding_ln_fwd: dim must be a multiple of 4");
+    const EmbLn3 l3{ln3_w, ln3_b, ln3_eps, ln3_out, ln3_stats, nullptr, nullptr};
+    return embedding_fwd(ids, n_tokens, seq_len, table, vocab, dim, pos_table, ln1_w, ln1_b, ln1_eps, p1, seed1, extra,
+                         ln2_w, ln2_b, ln2_eps, p2, seed2, out, stats, keep_mask, err_flag, &l3, stream);
+}
 
 ASME_API int asme_embedding_bwd_partials_count(void) { return 1024; }
 
-ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
-                                int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
-                                const float* ln1_b, float p1, uint64_t seed1, const float* extra, const float* ln2_w,
-                                float p2, uint64_t seed2, const uint8_t* keep_mask, const float* dout,
-                                const float* stats, float* d_rows, float* d_extra, float* partials,
-                                int64_t n_partials, void* stream) {
+namespace {
+int embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
+                  int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float p1,
+                  uint64_t seed1, const float* extra, const float* ln2_w, float p2, uint64_t seed2,
+                  const uint8_t* keep_mask, const float* dout, const float* stats, float* d_rows, float* d_extra,
+                  float* partials, int64_t n_partials, const EmbLn3* l3, void* stream) {
     ASME_CHECK_ARG(ids && table && dout && stats && d_rows, "asme_embedding_bwd: null pointer");
     ASME_CHECK_ARG(dim >= 1 && dim <= 512, "asme_embedding_bwd: bad shape");
     ASME_CHECK_ARG(!partials || n_partials >= 1, "asme_embedding_bwd: n_partials must be >= 1");
     if (n_tokens == 0) return 0;
-    const size_t lds = partials ? (size_t)kWavesPerBlock * 4 * dim * sizeof(float) : 0;
+    const size_t lds = partials ? (size_t)kWavesPerBlock * (l3 ? 6 : 4) * dim * sizeof(float) : 0;
     if (with_emb_layout(dim, [&](auto layout) {
             using R = decltype(layout);
             const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
@@ -672,10 +769,16 @@ ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t se
             if constexpr (R::W == 4) {
                 constexpr int kPass = 1;  // 2 tokens per pass: 160 VGPRs, 3 waves/SIMD, slower (169 vs 121 us)
                 const int64_t nb4 = partials ? n_partials : (n_tokens + rows - 1) / rows;
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass>), dim3((unsigned)nb4), dim3(256), lds,
-                                   (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w,
-                                   ln1_b, p1, extra, ln2_w, p2, emb_seed(seed1, seed2), keep_mask, dout, stats, d_rows,
-                                   d_extra, partials);
+                if (l3)
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass, true>), dim3((unsigned)nb4), dim3(256),
+                                       lds, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim,
+                                       pos_table, ln1_w, ln1_b, p1, extra, ln2_w, p2, emb_seed(seed1, seed2), keep_mask,
+                                       dout, stats, d_rows, d_extra, partials, *l3);
+                else
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass, false>), dim3((unsigned)nb4),
+                                       dim3(256), lds, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab,
+                                       (int)dim, pos_table, ln1_w, ln1_b, p1, extra, ln2_w, p2, emb_seed(seed1, seed2),
+                                       keep_mask, dout, stats, d_rows, d_extra, partials, EmbLn3{});
             } else {
                 hipLaunchKernelGGL(emb_bwd_kernel<R>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, ids,
                                    n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1, seed1,
@@ -684,6 +787,35 @@ ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t se
         }, ASME_EMB_BWD_LPR16))
         return -1;
     ASME_LAUNCH_CHECK("asme_embedding_bwd");
+}
+}  // namespace
+
+ASME_API int asme_embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
+                                int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
+                                const float* ln1_b, float p1, uint64_t seed1, const float* extra, const float* ln2_w,
+                                float p2, uint64_t seed2, const uint8_t* keep_mask, const float* dout,
+                                const float* stats, float* d_rows, float* d_extra, float* partials,
+                                int64_t n_partials, void* stream) {
+    return embedding_bwd(ids, n_tokens, seq_len, table, vocab, dim, pos_table, ln1_w, ln1_b, p1, seed1, extra, ln2_w,
+                         p2, seed2, keep_mask, dout, stats, d_rows, d_extra, partials, n_partials, nullptr, stream);
+}
+
+// backward of asme_embedding_ln_fwd: dout = gradient of `out` (the residual stream), dln = gradient of ln3_out;
+// partials (n_partials, 6 * dim): LN1 w / b, LN2 w / b, LN3 w / b column partials (LN1 / LN2 rows zero when
+// absent); ln2_b is required with ln2_w (the output is recomputed through LN2's affine)
+ASME_API int asme_embedding_ln_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table,
+                                   int64_t vocab, int64_t dim, const float* pos_table, const float* ln1_w,
+                                   const float* ln1_b, float p1, uint64_t seed1, const float* extra,
+                                   const float* ln2_w, const float* ln2_b, float p2, uint64_t seed2,
+                                   const float* ln3_w, const float* ln3_stats, const uint8_t* keep_mask,
+                                   const float* dout, const float* dln, const float* stats, float* d_rows,
+                                   float* d_extra, float* partials, int64_t n_partials, void* stream) {
+    ASME_CHECK_ARG(ln3_w && ln3_stats && dln && partials, "asme_embedding_ln_bwd: null pointer");
+    ASME_CHECK_ARG(!ln2_w || ln2_b, "asme_embedding_ln_bwd: ln2_b required with ln2_w");
+    ASME_CHECK_ARG(dim % 4 == 0, "asme_embedding_ln_bwd: dim must be a multiple of 4");
+    const EmbLn3 l3{ln3_w, nullptr, 0.f, nullptr, const_cast<float*>(ln3_stats), dln, ln2_b};
+    return embedding_bwd(ids, n_tokens, seq_len, table, vocab, dim, pos_table, ln1_w, ln1_b, p1, seed1, extra, ln2_w,
+                         p2, seed2, keep_mask, dout, stats, d_rows, d_extra, partials, n_partials, &l3, stream);
 }
 
 ASME_API int asme_scatter_add_rows(const float* rows, const int64_t* ids, int64_t n_rows, int64_t dim, float* grad,

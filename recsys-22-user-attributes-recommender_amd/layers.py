@@ -121,7 +121,14 @@ class TransformerEmbedding(nn.Module):
                                  ln2_eps=ln2.eps if ln2 is not None else 1e-5, p2=p2,
                                  table_grad=w._asme_table_grad)
         ln2_t = (ln2.weight, ln2.bias) if ln2 is not None else None
-        return ops.embedding(ids, w, pos, ln1, extra, ln2_t, spec)
+        # the first transformer block's input LayerNorm, when the model feeds this output straight into it
+        # (TransformerEncoderModel sets it): computed by the same kernel, handed over on the output tensor
+        ln3 = self.__dict__.get("_asme_next_norm")
+        if ln3 is None:
+            return ops.embedding(ids, w, pos, ln1, extra, ln2_t, spec)
+        x, ln = ops.embedding(ids, w, pos, ln1, extra, ln2_t, spec, ln3=ln3)
+        x._asme_ln = (ln3, ln)
+        return x
 
     def forward(self, sequence) -> torch.Tensor:
         return self.embed(sequence.sequence)
@@ -263,7 +270,11 @@ class TransformerLayer(nn.Module):
         if len(blocks) == 0:
             return x
         tr = self.training
-        x, ln = ops.layer_norm_pass(x, blocks[0].input_sublayer.norm)
+        pre = getattr(x, "_asme_ln", None)  # LN_in(x) of block 0, computed by the embedding kernel
+        if pre is not None and pre[0] is blocks[0].input_sublayer.norm:
+            ln = pre[1]
+        else:
+            x, ln = ops.layer_norm_pass(x, blocks[0].input_sublayer.norm)
         for i, blk in enumerate(blocks):
             att, ff = blk.attention, blk.feed_forward
             qkv = att.qkv(ln)

@@ -88,6 +88,13 @@ class TransformerEncoderModel(SequenceRecommenderModel):
         rep = Ly.TransformerSequenceRepresentationComponent(transformer_layer, bidirectional=bidirectional)
         super().__init__(embedding_layer, rep, sequence_representation_modifier_layer, projection_layer)
         self.apply(self._init_weights)
+        # the embedding output goes straight into block 0, whose first op is its input LayerNorm: let the embedding
+        # kernel compute it too (ops.embedding ln3; a plain attribute, not a registered submodule)
+        pre = type(embedding_layer) is Ly.PreFusionContextSequenceElementsRepresentationComponent
+        target = embedding_layer.item_embedding_layer if pre else embedding_layer
+        if len(transformer_layer.transformer_blocks) and type(target) is Ly.TransformerEmbedding and (
+                pre or type(embedding_layer) is Ly.TransformerEmbedding):
+            object.__setattr__(target, "_asme_next_norm", transformer_layer.transformer_blocks[0].input_sublayer.norm)
 
     @staticmethod
     def _init_weights(module):

@@ -529,9 +529,93 @@ class _EmbeddingFn(torch.autograd.Function):
                 g[2] if ctx.has[3] else None, g[3] if ctx.has[3] else None, None)
 
 
-def embedding(ids, table, pos=None, ln1=None, extra=None, ln2=None, spec: EmbeddingSpec = None):
+class _EmbeddingLnFn(torch.autograd.Function):
+    """_EmbeddingFn + the first transformer block's input LayerNorm on its output in the same kernel
+    (asme_embedding_ln_fwd / _bwd): returns (x, LN3(x)); x is the block's residual stream, LN3(x) the attention
+    input (transformer_layers.py:251-258), so the separate LayerNorm pass over x and its backward disappear."""
+
+    @staticmethod
+    def forward(ctx, ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, ln3_w, ln3_b, spec: EmbeddingSpec,
+                ln3_eps: float):
+        ids = _i64(ids)
+        T = ids.numel()
+        D = table.shape[1]
+        plan = spec.table_grad.plan if spec.table_grad is not None else None
+        src, src_ids = plan.gather_source(table, ids) if plan is not None else (table, ids)
+        V = src.shape[0]
+        dev = table.device
+        out = torch.empty(T, D, device=dev, dtype=torch.float32)
+        ln = torch.empty(T, D, device=dev, dtype=torch.float32)
+        stats = torch.empty(T, 4, device=dev, dtype=torch.float32)
+        stats3 = torch.empty(T, 2, device=dev, dtype=torch.float32)
+        s1, s2 = new_seed(spec.p1), new_seed(spec.p2)
+        extra_c = None if extra is None else _f32(extra).reshape(T, D)
+        keep = None
+        if spec.p1 > 0 or spec.p2 > 0:
+            keep = torch.empty(T, D // 4, device=dev, dtype=torch.uint8)
+        call("asme_embedding_ln_fwd", ptr(src_ids), T, spec.seq_len, ptr(src), V, D, ptr(pos), ptr(ln1_w), ptr(ln1_b),
+             spec.ln1_eps, spec.p1, s1, ptr(extra_c), ptr(ln2_w), ptr(ln2_b), spec.ln2_eps, spec.p2, s2, ptr(ln3_w),
+             ptr(ln3_b), ln3_eps, ptr(out), ptr(stats), ptr(ln), ptr(stats3), ptr(keep), None, stream())
+        ctx.save_for_backward(ids, src_ids, src, pos, ln1_w, ln1_b, extra_c, ln2_w, ln2_b, ln3_w, stats, stats3, keep)
+        ctx.table_shape = tuple(table.shape)
+        ctx.spec, ctx.seeds = spec, (s1, s2)
+        ctx.has = (pos is not None, ln1_w is not None, extra is not None, ln2_w is not None)
+        shape = (*ids.shape, D)
+        return out.view(shape), ln.view(shape)
+
+    @staticmethod
+    def backward(ctx, dout, dln):
+        ids, src_ids, src, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, ln3_w, stats, stats3, keep = ctx.saved_tensors
+        spec = ctx.spec
+        s1, s2 = ctx.seeds
+        T = ids.numel()
+        V, D = ctx.table_shape
+        dev = src.device
+        dout = _f32(dout).reshape(T, D) if dout is not None else torch.zeros(T, D, device=dev)
+        dln = _f32(dln).reshape(T, D) if dln is not None else torch.zeros(T, D, device=dev)
+        d_rows = torch.empty(T, D, device=dev, dtype=torch.float32)
+        d_extra = torch.empty(T, D, device=dev, dtype=torch.float32) if ctx.has[2] else None
+        part = torch.empty(_EMB_PARTIALS, 6 * D, device=dev, dtype=torch.float32)
+        call("asme_embedding_ln_bwd", ptr(src_ids), T, spec.seq_len, ptr(src), src.shape[0], D, ptr(pos), ptr(ln1_w),
+             ptr(ln1_b), spec.p1, s1, ptr(extra), ptr(ln2_w), ptr(ln2_b), spec.p2, s2, ptr(ln3_w), ptr(stats3),
+             ptr(keep), ptr(dout), ptr(dln), ptr(stats), ptr(d_rows), ptr(d_extra), ptr(part), _EMB_PARTIALS, stream())
+        g_table = None
+        if ctx.needs_input_grad[1]:
+            plan = spec.table_grad.plan if spec.table_grad is not None else None
+            if plan is not None:
+                plan.add_rows(ids, d_rows)
+            else:
+                g_table = dense_table_grad(ids, d_rows, V, D)
+        g_pos = None
+        if ctx.has[0] and ctx.needs_input_grad[2]:
+            L = spec.seq_len
+            B = T // L
+            g_pos = torch.empty_like(pos) if pos.shape[0] == L else torch.zeros_like(pos)
+            nch = max(1, min(32, B))
+            ws = torch.empty(nch, L, D, device=dev, dtype=torch.float32)
+            call("asme_position_grad", ptr(d_rows), B, L, D, ptr(ws), nch, ptr(g_pos), 0, stream())
+        red = _reduce_partials(part, 6 * D)
+        g = [red[i * D:(i + 1) * D] for i in range(6)]
+        g_extra = d_extra.view(*ids.shape, D) if d_extra is not None else None
+        return (None, g_table, g_pos, g[0] if ctx.has[1] else None, g[1] if ctx.has[1] else None, g_extra,
+                g[2] if ctx.has[3] else None, g[3] if ctx.has[3] else None, g[4], g[5], None, None)
+
+
+# the fused next LayerNorm (ln3) is taken when the hidden size allows the 4-wide kernels; 0: A/B switch
+FUSE_EMBEDDING_LN = os.environ.get("ASME_FUSE_EMB_LN", "1") != "0"
+
+
+def embedding(ids, table, pos=None, ln1=None, extra=None, ln2=None, spec: EmbeddingSpec = None, ln3=None):
+    """The fused embedding; `ln3` (an nn.LayerNorm): also return ln3(x) from the same kernel -> (x, ln3(x))."""
     ln1_w, ln1_b = (None, None) if ln1 is None else ln1
     ln2_w, ln2_b = (None, None) if ln2 is None else ln2
+    if ln3 is not None:
+        D = table.shape[1]
+        if FUSE_EMBEDDING_LN and D % 4 == 0 and (ln2_w is None or ln2_b is not None):
+            return _EmbeddingLnFn.apply(ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, ln3.weight, ln3.bias,
+                                        spec, float(ln3.eps))
+        x = _EmbeddingFn.apply(ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, spec)
+        return layer_norm_pass(x, ln3)
     return _EmbeddingFn.apply(ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, spec)
 
 

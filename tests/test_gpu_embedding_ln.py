@@ -1,0 +1,107 @@
+"""The embedding kernel with the first transformer block's input LayerNorm fused (asme_embedding_ln_fwd / _bwd,
+ops.embedding(..., ln3=norm)) against the unfused composition it replaces -- asme_embedding_fwd followed by
+ops.layer_norm_pass -- and against a PyTorch fp32 reference of the whole chain (transformer_layers.py:55-80, 251-258;
+kebert4rec/components.py:54-63).  Same seeds, so the dropout decisions are the same in both kernels."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = {  # name: (pos, ln1, extra, ln2, p1, p2)
+    "bert4rec": (True, True, False, False, 0.2, 0.0),
+    "sasrec": (True, True, False, True, 0.2, 0.2),
+    "kebert4rec_pre": (True, True, True, True, 0.1, 0.3),
+    "no_ln1": (True, False, False, False, 0.0, 0.0),
+}
+
+
+def _ref(ids, table, pos, ln1, extra, ln2, ln3, L):
+    """fp32 reference with p = 0"""
+    F = torch.nn.functional
+    x = table[ids]
+    if pos is not None:
+        x = x + pos[torch.arange(ids.shape[1], device=ids.device) % L]
+    if ln1 is not None:
+        x = F.layer_norm(x, (x.shape[-1],), ln1[0], ln1[1], 1e-5)
+    if extra is not None:
+        x = x + extra
+    if ln2 is not None:
+        x = F.layer_norm(x, (x.shape[-1],), ln2[0], ln2[1], 1e-5)
+    return x, F.layer_norm(x, (x.shape[-1],), ln3.weight, ln3.bias, ln3.eps)
+
+
+@pytest.mark.parametrize("D", [32, 128])
+@pytest.mark.parametrize("case", list(CASES))
+def test_embedding_ln_fused_equals_unfused(asme, dev, case, D):
+    has_pos, has_ln1, has_extra, has_ln2, p1, p2 = CASES[case]
+    torch.manual_seed(3)
+    B, L, V = 6, 37, 501
+    ids = torch.randint(0, V, (B, L), device=dev)
+    ids[0, :5] = 0  # padding rows
+    leaf = lambda *s, scale=1.0: (torch.randn(*s, device=dev) * scale).requires_grad_(True)  # noqa: E731
+    table = leaf(V, D)
+    pos = leaf(L, D) if has_pos else None
+    ln1 = (leaf(D, scale=0.3) + 1.0, leaf(D, scale=0.1)) if has_ln1 else None
+    ln1 = tuple(t.detach().requires_grad_(True) for t in ln1) if ln1 else None
+    ln2 = tuple(t.detach().requires_grad_(True) for t in (leaf(D, scale=0.3) + 1.0, leaf(D, scale=0.1))) \
+        if has_ln2 else None
+    extra = leaf(B, L, D) if has_extra else None
+    ln3 = torch.nn.LayerNorm(D).to(dev)
+    with torch.no_grad():
+        ln3.weight.add_(torch.randn(D, device=dev) * 0.3)
+        ln3.bias.add_(torch.randn(D, device=dev) * 0.1)
+    gx, gl = torch.randn(B, L, D, device=dev), torch.randn(B, L, D, device=dev)
+    leaves = [t for t in (table, pos, *(ln1 or ()), extra, *(ln2 or ()), ln3.weight, ln3.bias) if t is not None]
+
+    def run(fused: bool):
+        spec = asme.ops.EmbeddingSpec(seq_len=L, p1=p1, p2=p2)
+        torch.manual_seed(11)  # same dropout seeds for both forms
+        if fused:
+            x, ln = asme.ops.embedding(ids, table, pos, ln1, extra, ln2, spec, ln3=ln3)
+        else:
+            x = asme.ops.embedding(ids, table, pos, ln1, extra, ln2, spec)
+            x, ln = asme.ops.layer_norm_pass(x, ln3)
+        grads = torch.autograd.grad((x * gx).sum() + (ln * gl).sum(), leaves)
+        return x.detach(), ln.detach(), grads
+
+    xf, lf, gf = run(True)
+    xu, lu, gu = run(False)
+    # (the two kernel instantiations may contract the affine steps differently: ulp-level differences)
+    torch.testing.assert_close(xf, xu, rtol=2e-6, atol=1e-6)
+    torch.testing.assert_close(lf, lu, rtol=1e-5, atol=1e-5)
+    for a, b in zip(gf, gu):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()) + 1e-6)
+    if p1 == 0.0 and p2 == 0.0:
+        xr, lr = _ref(ids, table, pos, ln1, extra, ln2, ln3, L)
+        torch.testing.assert_close(xf, xr.detach(), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(lf, lr.detach(), rtol=1e-4, atol=1e-4)
+        gr = torch.autograd.grad((xr * gx).sum() + (lr * gl).sum(), leaves)
+        for a, b in zip(gf, gr):
+            torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3 * float(b.abs().max()) + 1e-6)
+
+
+def test_models_take_the_fused_embedding_ln(asme, dev):
+    """SASRec / BERT4Rec route block 0's input LayerNorm through the embedding kernel (no separate LayerNorm launch in
+    the forward); UBERT4Rec (user token concatenated after the embedding) keeps the unfused path"""
+    calls = []
+    orig = asme.ops.call
+
+    def spy(name, *a):
+        calls.append(name)
+        return orig(name, *a)
+
+    m = asme.SASRecModel(transformer_hidden_size=32, num_transformer_heads=2, num_transformer_layers=2,
+                         item_vocab_size=100, max_seq_length=12, transformer_dropout=0.1).to(dev)
+    seq = torch.randint(1, 100, (3, 12), device=dev)
+    asme.ops.call = spy
+    try:
+        rep = m.encode(asme.InputSequence(seq, seq.ne(0)))
+    finally:
+        asme.ops.call = orig
+    assert "asme_embedding_ln_fwd" in calls and "asme_layernorm_fwd" not in calls
+    rep.sum().backward()
+    assert m._sequence_embedding_layer.item_embedding_layer.embedding_norm.weight.grad is not None
+    blk0 = m._sequence_representation_layer.transformer_layer.transformer_blocks[0]
+    assert blk0.input_sublayer.norm.weight.grad is not None
+    assert "_asme_next_norm" not in dict(m.named_modules()) and not any(
+        "_asme_next_norm" in k for k in m.state_dict())
