@@ -527,7 +527,9 @@ def main():
                                    "asme_sampled_logits_fwd", "asme_sampled_logits_bwd", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
                                    "asme_ws_linear", "asme_posneg_sample", "asme_table_grad_reduce_apply",
-                                   "asme_dedup_ids", "asme_dedup_ids_segments", "asme_occurrence_csr"])
+                                   "asme_dedup_ids", "asme_dedup_ids_segments", "asme_occurrence_csr",
+                                   "asme_position_grad", "asme_reduce_rows", "asme_sasrec_bce_fwd",
+                                   "asme_sasrec_bce_bwd"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -619,6 +621,14 @@ def main():
         # ordered per-row sums + the lazy Adam step: the three contributions' rows (embedding d_rows, h for the
         # pos and for the neg ids) + their scales, order / slot per occurrence, the staged p / m / v read, the
         # table's p / m / v rows + last_step written, the unique ids read
+        # position-embedding gradient: d_rows read once, 32 chunk partials (L, d) written and read, (L, d) written
+        "asme_position_grad": ("hbm", T * d * 4 + 2 * 32 * L * d * 4 + L * d * 4),
+        # LayerNorm parameter partials summed (mean over the step's launches: the four residual-LN backwards' 1,024 x
+        # 2d and the embedding backward's 2,048 x 6d)
+        "asme_reduce_rows": ("hbm", (4 * 1024 * 2 * d + 2048 * 6 * d) * 4 / 5),
+        # the sampled BCE loss: two logits + the mask read (fwd), + two logit gradients written (bwd)
+        "asme_sasrec_bce_fwd": ("hbm", 2 * T * 4 + T),
+        "asme_sasrec_bce_bwd": ("hbm", 4 * T * 4 + T),
         "asme_table_grad_reduce_apply": ("hbm", 3 * T * d * 4 + 2 * T * 4 + 3 * T * 8 + 6 * U * d * 4 + U * 12),
     }
     # HBM traffic per launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE, gfx950

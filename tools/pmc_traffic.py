@@ -48,6 +48,11 @@ MAP = [
     (r"residual_ln_fwd_kernel", "asme_residual_ln_fwd", True),
     (r"residual_ln_bwd_kernel", "asme_residual_ln_bwd", True),
     (r"ws_gemm_kernel", "asme_ws_linear", True),
+    (r"pos_partial_kernel", "asme_position_grad", True),
+    (r"reduce_rows_kernel", "asme_reduce_rows", True),
+    (r"bce_fwd_kernel", "asme_sasrec_bce_fwd", True),
+    (r"bce_finish_kernel", "asme_sasrec_bce_fwd", False),
+    (r"bce_bwd_kernel", "asme_sasrec_bce_bwd", True),
     # the fused logits + CE head (csrc/logits.hip): the engine's mode names the call; the operand splits that open
     # a call are attributed to the call of the engine launch that follows them (see per_call)
     # (api None: the kernel belongs to the logits call that launched the previous mapped kernel)
