@@ -65,7 +65,7 @@ MAP = [
 ]
 PENDING = r"split_planes_kernel"  # belongs to the next mapped logits kernel's call
 # calls whose launches have different shapes (the bench's work figure is their mean): mean, not median
-MEAN = {"asme_ws_linear", "asme_linear_weight_grad"}
+MEAN = {"asme_ws_linear", "asme_linear_weight_grad", "asme_reduce_rows"}
 
 
 def load(path, counter):
