@@ -570,6 +570,35 @@ __global__ __launch_bounds__(1024) void reduce_rows_kernel(const float* __restri
     if (grp == 0 && c < width) out[c] = accumulate ? out[c] + red[0][col] : red[0][col];
 }
 
+// narrow matrices (the LayerNorm parameter partials: 1,024-2,048 rows x 2d-6d columns): 16 columns per block and 64
+// row-groups, so a 256-column sum runs on 16 workgroups with 16 rows per thread instead of 4 workgroups with 64
+constexpr int kNarCols = 16, kNarGroups = 64;
+__global__ __launch_bounds__(1024) void reduce_rows_narrow_kernel(const float* __restrict__ part, int64_t nrows,
+                                                                  int64_t width, float* __restrict__ out,
+                                                                  int accumulate) {
+    __shared__ float red[kNarGroups][kNarCols];
+    const int col = threadIdx.x % kNarCols, grp = threadIdx.x / kNarCols;
+    const int64_t c = (int64_t)blockIdx.x * kNarCols + col;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (c < width) {
+        int64_t r = grp;
+        for (; r + 3 * kNarGroups < nrows; r += 4 * kNarGroups) {
+            s0 += part[r * width + c];
+            s1 += part[(r + kNarGroups) * width + c];
+            s2 += part[(r + 2 * kNarGroups) * width + c];
+            s3 += part[(r + 3 * kNarGroups) * width + c];
+        }
+        for (; r < nrows; r += kNarGroups) s0 += part[r * width + c];
+    }
+    red[grp][col] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    for (int h = kNarGroups / 2; h > 0; h >>= 1) {
+        if (grp < h) red[grp][col] += red[grp + h][col];
+        __syncthreads();
+    }
+    if (grp == 0 && c < width) out[c] = accumulate ? out[c] + red[0][col] : red[0][col];
+}
+
 template <int VPL>
 __global__ __launch_bounds__(256) void gather_sum_fwd_kernel(const int64_t* __restrict__ ids, int64_t n, int K,
                                                              int skip_zero, const float* __restrict__ table,
@@ -858,8 +887,12 @@ ASME_API int asme_reduce_rows(const float* part, int64_t n_rows, int64_t width, 
                               void* stream) {
     ASME_CHECK_ARG(part && out, "asme_reduce_rows: null pointer");
     if (width == 0) return 0;
-    hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + kRedCols - 1) / kRedCols)), dim3(1024), 0,
-                       (hipStream_t)stream, part, n_rows, width, out, accumulate);
+    if (width <= kNarCols * kNarGroups && n_rows >= 4 * kNarGroups)
+        hipLaunchKernelGGL(reduce_rows_narrow_kernel, dim3((unsigned)((width + kNarCols - 1) / kNarCols)), dim3(1024),
+                           0, (hipStream_t)stream, part, n_rows, width, out, accumulate);
+    else
+        hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + kRedCols - 1) / kRedCols)), dim3(1024), 0,
+                           (hipStream_t)stream, part, n_rows, width, out, accumulate);
     ASME_LAUNCH_CHECK("asme_reduce_rows");
 }
 

@@ -105,3 +105,33 @@ def test_models_take_the_fused_embedding_ln(asme, dev):
     assert blk0.input_sublayer.norm.weight.grad is not None
     assert "_asme_next_norm" not in dict(m.named_modules()) and not any(
         "_asme_next_norm" in k for k in m.state_dict())
+
+
+@pytest.mark.parametrize("B,L,D", [(1024, 200, 128), (37, 13, 32), (5, 7, 6)])
+def test_position_grad_equals_batch_sum(asme, dev, B, L, D):
+    """asme_position_grad (the position embedding's gradient: the token rows summed over the batch per position) vs
+    torch's sum in fp64 (32 batch chunks, then the column sums)"""
+    torch.manual_seed(5)
+    rows = torch.randn(B * L, D, device=dev)
+    nch = max(1, min(32, B))
+    ws = torch.empty(nch, L, D, device=dev)
+    out = torch.empty(L, D, device=dev)
+    asme._lib.call("asme_position_grad", rows.data_ptr(), B, L, D, ws.data_ptr(), nch, out.data_ptr(), 0,
+                   asme._lib.stream())
+    want = rows.double().view(B, L, D).sum(0)
+    torch.testing.assert_close(out.double(), want, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("rows,width", [(1024, 256), (2048, 768), (1024, 1024), (300, 256), (32, 25600), (1, 5)])
+def test_reduce_rows_column_sums(asme, dev, rows, width):
+    """asme_reduce_rows (fixed-order column sums of the per-block partials; narrow matrices on the 16-column kernel)
+    vs fp64, plain and accumulating"""
+    torch.manual_seed(9)
+    part = torch.randn(rows, width, device=dev)
+    out = torch.randn(width, device=dev)
+    base = out.clone()
+    asme._lib.call("asme_reduce_rows", part.data_ptr(), rows, width, out.data_ptr(), 1, asme._lib.stream())
+    want = part.double().sum(0) + base.double()
+    torch.testing.assert_close(out.double(), want, rtol=1e-5, atol=1e-4)
+    asme._lib.call("asme_reduce_rows", part.data_ptr(), rows, width, out.data_ptr(), 0, asme._lib.stream())
+    torch.testing.assert_close(out.double(), part.double().sum(0), rtol=1e-5, atol=1e-4)
