@@ -293,6 +293,30 @@ __global__ __launch_bounds__(1024) void sum_slabs_kernel(const float* __restrict
     }
 }
 
+// Few slabs (the split-T chunks of one weight gradient: 8-64): one thread per column, its rows in flight 8 at a time
+// and added in row order -- no LDS tree, no barrier (the 64-column form above spends its time in the tree and the
+// round trips of 2-4 loads per thread at these row counts)
+__global__ __launch_bounds__(256) void sum_slabs_cols_kernel(const float* __restrict__ part, int64_t nrows,
+                                                             int64_t width_w, float* __restrict__ out_w,
+                                                             int64_t width_b, float* __restrict__ out_b,
+                                                             int accumulate) {
+    const int64_t width = width_w + width_b;
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= width) return;
+    float s = 0.f;
+    int64_t r = 0;
+    for (; r + 8 <= nrows; r += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = part[(r + u) * width + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < nrows; ++r) s += part[r * width + c];
+    float* o = c < width_w ? out_w + c : out_b + (c - width_w);
+    *o = accumulate ? *o + s : s;
+}
+
 struct Plan {
     int64_t nchunks, chunk_rows;
 };
@@ -383,7 +407,11 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
             : launch_weight_grad<1, 1>(grid, s, dy, ld_dy, x, ld_x, n_tokens, N, K, p.chunk_rows, part, bpart);
     if (e != hipSuccess) return hip_status(e, "asme_linear_weight_grad: LDS opt-in");
     const int64_t width_w = out_features * in_features, width_b = db ? out_features : 0;
-    hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width_w + width_b + kRedCols - 1) / kRedCols)), dim3(1024), 0,
-                       s, part, p.nchunks, width_w, dw, width_b, db, accumulate);
+    if (p.nchunks <= 64)
+        hipLaunchKernelGGL(sum_slabs_cols_kernel, dim3((unsigned)((width_w + width_b + 255) / 256)), dim3(256), 0, s,
+                           part, p.nchunks, width_w, dw, width_b, db, accumulate);
+    else
+        hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)((width_w + width_b + kRedCols - 1) / kRedCols)),
+                           dim3(1024), 0, s, part, p.nchunks, width_w, dw, width_b, db, accumulate);
     ASME_LAUNCH_CHECK("asme_linear_weight_grad");
 }

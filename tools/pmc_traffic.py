@@ -22,7 +22,7 @@ MAP = [
     (r"attn_bwd_dq(_res)?_kernel", "asme_attention_bwd", True),
     (r"attn_bwd_dkdv(_res)?_kernel", "asme_attention_bwd", False),
     (r"weight_grad_kernel", "asme_linear_weight_grad", True),
-    (r"sum_slabs_kernel", "asme_linear_weight_grad", False),
+    (r"sum_slabs(_cols)?_kernel", "asme_linear_weight_grad", False),
     (r"emb_fwd4_kernel<.*, true>", "asme_embedding_ln_fwd", True),  # + block 0's input LayerNorm
     (r"emb_bwd4_kernel<.*, true>", "asme_embedding_ln_bwd", True),
     (r"emb_fwd4?_kernel", "asme_embedding_fwd", True),
