@@ -1,5 +1,6 @@
 # fused embedding + block-0 LayerNorm: its tests and the model parity tests, then the headline bench alternating
-# ASME_FUSE_EMB_LN=1 / 0 in one box, then the ws GEMM diagnostic builds (tools/ws_ab.py)
+# ASME_FUSE_EMB_LN=1 / 0 in one box, then (if built: tools/build_variant.sh diagN wsgemm.hip -DASME_WS_DIAG=N) the ws
+# GEMM diagnostic builds (tools/ws_ab.py)
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
@@ -11,5 +12,5 @@ for i in 1 2; do
     python -c "import json; r=json.loads(open('gpurun_out/embln_b$r$i.json').read().strip().splitlines()[-1]); st={x['kernel']: x['avg_ms'] for x in r['rooflines']}; print('fuse=$r', r['value'], r['ms_per_step'], 'emb', st.get('asme_embedding_fwd'), st.get('asme_embedding_bwd'))"
   done
 done
-V=""; for v in 1 2 3 4; do V="$V tools/variants/libasme_mi_diag$v.so"; done
-timeout -k 10 300 python tools/ws_ab.py recsys-22-user-attributes-recommender_amd/libasme_mi.so $V --reps 3
+V=""; for v in 1 2 3 4; do [ -f tools/variants/libasme_mi_diag$v.so ] && V="$V tools/variants/libasme_mi_diag$v.so"; done
+[ -z "$V" ] || timeout -k 10 300 python tools/ws_ab.py recsys-22-user-attributes-recommender_amd/libasme_mi.so $V --reps 3
