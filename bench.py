@@ -129,10 +129,11 @@ def parse():
                     help="gpu (default): every step samples a fresh batch from sessions in HBM with the GPU pos/neg "
                          "sampler (asme_posneg_sample) inside the timed step; resident: two pre-built device batches "
                          "alternating (rows touched one or two steps earlier: less lazy catch-up per step)")
-    ap.add_argument("--legs", default="bert4rec:27000,kebert4rec:13000",
+    ap.add_argument("--legs", default="bert4rec:27000,kebert4rec:13000,sasrec_zipf",
                     help="with the sasrec-neg headline: the other BASELINE workloads run in the same invocation and "
                          "reported under \"workloads\" of the one JSON line (name:items, comma-separated; "
-                         "C3 BERT4Rec |I| = 27,000, C5 KeBERT4Rec |I| = 13,000; 'none' to skip)")
+                         "C3 BERT4Rec |I| = 27,000, C5 KeBERT4Rec |I| = 13,000, sasrec_zipf: the headline step on "
+                         "Zipf(1.07) ids at the headline's --items (SURVEY §8d secondary); 'none' to skip)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -154,26 +155,29 @@ def parse_legs(spec: str):
     out = []
     for part in spec.split(","):
         name, _, items = part.partition(":")
-        if name not in ("bert4rec", "kebert4rec"):
+        if name not in ("bert4rec", "kebert4rec", "sasrec_zipf"):
             raise SystemExit(f"--legs: unknown workload {name!r}")
-        out.append((name, int(items) if items else {"bert4rec": 27000, "kebert4rec": 13000}[name]))
+        out.append((name, int(items) if items else {"bert4rec": 27000, "kebert4rec": 13000, "sasrec_zipf": 0}[name]))
     return out
+
+
+def session_ids(n, V, g, kind):
+    """n item ids in [3, V) for the synthetic sessions: uniform, or Zipf(1.07) over item rank (id 3 the most popular;
+    inverse CDF of the continuous power law, SURVEY §8d secondary)"""
+    if kind == "uniform":
+        return torch.randint(3, V, (n,), device=g.device, generator=g)
+    u = torch.rand(n, device=g.device, generator=g, dtype=torch.float64)
+    a, m = 1.07, V - 3
+    hmax = (m ** (1 - a) - 1) / (1 - a)
+    r = ((u * hmax) * (1 - a) + 1) ** (1 / (1 - a))
+    return r.long().clamp(1, m) + 2
 
 
 def synthetic_batch(B, L, V, seed, dev, kind="uniform"):
     """Full-length sequences (no padding): ids ~ U[3, V) (or Zipf(1.07) over item rank), pos = next id,
     neg ~ U[3, V)."""
     g = torch.Generator(device=dev).manual_seed(seed)
-    if kind == "uniform":
-        full = torch.randint(3, V, (B, L + 1), device=dev, generator=g)
-    else:
-        # Zipf(1.07) by inverse-CDF on a truncated harmonic approximation
-        u = torch.rand(B, L + 1, device=dev, generator=g, dtype=torch.float64)
-        a = 1.07
-        n = V - 3
-        hmax = (n ** (1 - a) - 1) / (1 - a)
-        r = ((u * hmax) * (1 - a) + 1) ** (1 / (1 - a))
-        full = (r.long().clamp(1, n) - 1 + 3)
+    full = session_ids(B * (L + 1), V, g, kind).view(B, L + 1)
     g2 = torch.Generator(device=dev).manual_seed(seed + 1)
     neg = torch.randint(3, V, (B, L), device=dev, generator=g2)
     return {"item": full[:, :L].contiguous(), "positive_samples": full[:, 1:].contiguous(), "negative_samples": neg}
@@ -423,36 +427,14 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
     return result
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and args.backend == "gloo":
-        local = local % torch.cuda.device_count()  # rehearsal: several ranks may share one GPU
-    if world > 1 or args.sharded:
-        torch.cuda.set_device(local)
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29517")
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", str(world))
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
-    dev = torch.device("cuda", local)
-    asme = __graft_entry__.load_package()
+def bench_sasrec(args, asme, dev, world, rank, ids_kind):
+    """The SASRec-neg training step (BASELINE C2 / C4): B sequences per GPU, |I| = args.items, the GPU pos/neg
+    producer inside the timed step; ids_kind "uniform" (the headline) or "zipf" (Zipf(1.07) over item rank, seed
+    1234: SURVEY §8d's secondary, hot keys for the dedup / occurrence CSR / ordered reduce-apply).  Returns the result
+    dict (rank 0 prints it as the headline line, or inside it under "workloads")."""
     V = args.items + 3
     B, L, d = args.batch, args.seq_len, args.dim
-
     torch.manual_seed(rank)
-    if args.workload in ("bert4rec", "kebert4rec"):
-        result = bench_bert4rec(args, asme, dev, world, rank, args.workload, args.items)
-        if rank == 0:
-            print(json.dumps(result), flush=True)
-        if dist.is_initialized():
-            dist.destroy_process_group()
-        return
     sharded = world > 1 or args.sharded
     # N > 1: the item table is row-sharded over the ranks (RCCL all-to-all of ids / rows / row grads,
     # one all_reduce of the replicated dense gradients); N = 1: the whole table on the one GPU
@@ -473,13 +455,13 @@ def main():
         step_fn = lambda b, i: asme.modules.train_step(module, opt, None, b, i)  # noqa: E731
     module.train()
     opt = module.configure_optimizers()
-    batches = [synthetic_batch(B, L, V, 1234 + 7 * (rank * 2 + i), dev, args.ids) for i in range(2)]
+    batches = [synthetic_batch(B, L, V, 1234 + 7 * (rank * 2 + i), dev, ids_kind) for i in range(2)]
     if args.producer == "gpu":
         # sessions of L + 1 items in HBM; each step's batch (x, pos, sampled negatives) is built on the GPU
         # inside the step (asme_posneg_sample), as the reference's DataLoader would produce it
         n_sess = max(4 * B, 8192)
         g = torch.Generator(device=dev).manual_seed(4321 + rank)
-        flat = torch.randint(3, V, (n_sess * (L + 1),), device=dev, generator=g)
+        flat = session_ids(n_sess * (L + 1), V, g, ids_kind)
         store = asme.batches.SessionStore(flat, torch.arange(n_sess + 1, device=dev) * (L + 1))
         sampler = asme.batches.PositiveNegativeSamplerProcessor(tok)
         order = torch.randperm(n_sess, device=dev, generator=g)
@@ -648,16 +630,17 @@ def main():
     roof = rooflines[0] if rooflines else None
 
     result = {
-        "metric": "training sequences/sec at B=1024 L=200 |I|=10M (SASRec-neg, fwd+bwd+Adam)",
+        "metric": ("training sequences/sec at B=1024 L=200 |I|=10M (SASRec-neg, fwd+bwd+Adam)" if ids_kind == "uniform"
+                   else f"training sequences/sec (SASRec-neg, {ids_kind} ids, B={B} L={L} |I|={args.items}, fwd+bwd+Adam)"),
         "value": round(value, 2), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": ("synthetic sessions (uniform ids), a fresh GPU-sampled batch every step, random-init weights"
+        "vs_baseline": None, "dtype": "fp32", "data": (f"synthetic sessions ({ids_kind} ids), a fresh GPU-sampled batch every step, random-init weights"
                                                  if args.producer == "gpu" else
-                                                 "synthetic (uniform ids, two resident batches), random-init weights"),
+                                                 f"synthetic ({ids_kind} ids, two resident batches), random-init weights"),
         "config": {"workload": "sasrec-neg train step", "model": "SASRec", "global_batch": B * world,
                    "batch_per_gpu": B, "seq_len": L, "items": args.items, "dim": d, "heads": args.heads,
                    "layers": args.layers, "dropout": args.dropout, "table_grad": args.table_grad,
-                   "ids": args.ids, "producer": args.producer,
+                   "ids": ids_kind, "producer": args.producer,
                    "parallelism": f"dp{world}+rowshard{world}" if sharded else "single"},
         "roofline": roof,
         "rooflines": rooflines,
@@ -669,6 +652,40 @@ def main():
     asme.ops.SparseTablePlan.release = _orig_release
     del model, module, opt, batches
     torch.cuda.empty_cache()
+    return result
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.backend == "gloo":
+        local = local % torch.cuda.device_count()  # rehearsal: several ranks may share one GPU
+    if world > 1 or args.sharded:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", local)
+    asme = __graft_entry__.load_package()
+    V = args.items + 3
+    B, L, d = args.batch, args.seq_len, args.dim
+
+    torch.manual_seed(rank)
+    if args.workload in ("bert4rec", "kebert4rec"):
+        result = bench_bert4rec(args, asme, dev, world, rank, args.workload, args.items)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
+    result = bench_sasrec(args, asme, dev, world, rank, args.ids)
     # the other BASELINE workloads, measured in the same run (same contract: warm-up, barrier + synchronize around
     # exactly --steps steps, max over ranks) and reported inside this one JSON line
     legs = parse_legs(args.legs)
@@ -676,7 +693,12 @@ def main():
         result["workloads"] = {}
         for leg, items in legs:
             torch.manual_seed(rank)
-            result["workloads"][leg] = bench_bert4rec(args, asme, dev, world, rank, leg, items)
+            if leg == "sasrec_zipf":
+                if args.ids == "zipf":
+                    continue  # the headline already is the Zipf run
+                result["workloads"][leg] = bench_sasrec(args, asme, dev, world, rank, "zipf")
+            else:
+                result["workloads"][leg] = bench_bert4rec(args, asme, dev, world, rank, leg, items)
             torch.cuda.empty_cache()
     if rank == 0 and world == 1 and args.cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, V)

@@ -145,12 +145,21 @@ int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t l
                        const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
                        int causal, float scale, float p_drop, uint64_t seed, const uint8_t* drop_mask, float* workspace,
                        float* dq, int64_t ld_dq, float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream);
-/* Attention kernel selection: 0 = automatic (one workgroup per (batch, head) with the head's operands
- * resident in LDS whenever 2*ceil(L/16)*16*(dk+4)*4 B fits 160 KiB, else the 64-row streaming kernels; the
- * resident backward runs dK/dV first, storing dS, then dQ = dS K), 1 = streaming kernels only, 2 = resident
- * kernels with a dQ pass that recomputes S and dP.  Returns the previous mode.  Process-wide; for tests and A/B
- * timing. */
-int asme_attention_set_mode(int mode);
+/* The same two calls with the kernel family chosen per call (kernel tests and same-process A/B timing; the product
+ * entry points above always run family 0): 0 = automatic (one workgroup per (batch, head) with the head's operands
+ * resident in LDS whenever 2*ceil(L/16)*16*(dk+4)*4 B fits 160 KiB, else the 64-row streaming kernels; the resident
+ * backward runs dK/dV first, storing dS, then dQ = dS K), 1 = streaming kernels only, 2 = resident kernels with a
+ * dQ pass that recomputes S and dP.  No process-wide state. */
+int asme_attention_fwd_kernels(int kernels, const float* q, const float* k, const float* v, int64_t ld_q,
+                               int64_t ld_k, int64_t ld_v, const uint8_t* key_valid, int64_t batch, int64_t heads,
+                               int64_t seq_len, int64_t head_dim, int causal, float scale, float p_drop, uint64_t seed,
+                               float* out, int64_t ld_out, float* lse, uint8_t* drop_mask, void* stream);
+int asme_attention_bwd_kernels(int kernels, const float* q, const float* k, const float* v, int64_t ld_q,
+                               int64_t ld_k, int64_t ld_v, const float* out, int64_t ld_out, const float* dout,
+                               int64_t ld_dout, const float* lse, const uint8_t* key_valid, int64_t batch,
+                               int64_t heads, int64_t seq_len, int64_t head_dim, int causal, float scale, float p_drop,
+                               uint64_t seed, const uint8_t* drop_mask, float* workspace, float* dq, int64_t ld_dq,
+                               float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream);
 /* Size of the drop_mask buffer for asme_attention_fwd/bwd (p_drop > 0). */
 int64_t asme_attention_dropout_mask_bytes(int64_t batch, int64_t heads, int64_t seq_len);
 
@@ -202,8 +211,8 @@ int asme_linear_xent_bwd(const float* H, int64_t ld_h, int64_t n, int64_t dim, c
                          const float* stats, const float* dloss, float* dH, float* dW, float* db, float* workspace,
                          int64_t ws_bytes, void* stream);
 /* Training form of the fused CE head (the logits recomputed once instead of twice): the forward also returns
- * dh_raw (n x dim, row stride ld_dh) = softmax(H W^T + b) W - W[t] per valid row, 0 for ignored rows -- dH before
- * the upstream scale; the backward scales it (dH = dh_raw * dloss[0] / out[1]) and runs the dW / db pass. */
+ * dh_raw (n x dim, contiguous: ld_dh must equal dim) = softmax(H W^T + b) W - W[t] per valid row, 0 for ignored
+ * rows -- dH before the upstream scale; the backward scales it (dH = dh_raw * dloss[0] / out[1]) and runs the dW / db pass. */
 int64_t asme_linear_xent_fwd_dh_workspace(int64_t n, int64_t V, int64_t dim);
 int asme_linear_xent_fwd_dh(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
                             int64_t V, const float* bias, const int64_t* targets, int64_t ignore_index, float* lse,

@@ -40,7 +40,6 @@ SIGNATURES = {
     "asme_layernorm_bwd_add": [p, i64, i64, p, p, p, p, p, p, i64, p],
     "asme_residual_ln_fwd": [p, p, i64, i64, f32, u64, f32, u64, p, p, f32, p, p, p, p],
     "asme_residual_ln_bwd": [p, i64, i64, f32, u64, f32, u64, p, p, p, p, p, p, p, i64, p],
-    "asme_attention_set_mode": [i32],
     "asme_occurrence_csr_workspace": [i64],
     "asme_ws_linear_supported": [i64, i64, i64],
     "asme_ws_linear": [p, i64, i64, p, i64, i32, p, i32, p, p, f32, u64, p, p],
@@ -79,6 +78,10 @@ SIGNATURES = {
     "asme_attention_fwd": [p, p, p, i64, i64, i64, p, i64, i64, i64, i64, i32, f32, f32, u64, p, i64, p, p, p],
     "asme_attention_bwd": [p, p, p, i64, i64, i64, p, i64, p, i64, p, p, i64, i64, i64, i64, i32, f32, f32, u64, p,
                            p, p, i64, p, i64, p, i64, p],
+    "asme_attention_fwd_kernels": [i32, p, p, p, i64, i64, i64, p, i64, i64, i64, i64, i32, f32, f32, u64, p, i64, p,
+                                   p, p],
+    "asme_attention_bwd_kernels": [i32, p, p, p, i64, i64, i64, p, i64, p, i64, p, p, i64, i64, i64, i64, i32, f32,
+                                   f32, u64, p, p, p, i64, p, i64, p, i64, p],
     "asme_sampled_logits_fwd": [p, p, p, p, i64, i64, i64, p, p, p],
     "asme_sampled_logits_bwd": [p, p, p, p, i64, i64, i64, p, p, p, p, p],
     "asme_sasrec_bce_fwd": [p, p, p, i64, p, i64, p, p],

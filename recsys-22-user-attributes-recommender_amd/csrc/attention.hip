@@ -1173,8 +1173,6 @@ inline size_t ds_lds_bytes(int L, int DK) {
     return Lp * (DK + 4) * sizeof(float) + (Lp + 31) / 32 * 4 + 16;
 }
 
-int g_attention_mode = 0;  // 0 auto, 1 streaming kernels only, 2 resident kernels with the recomputing dQ pass
-
 template <class K>
 bool res_prepare(K kernel, size_t lds) {
     if (lds > 160 * 1024) return false;
@@ -1195,11 +1193,17 @@ bool aligned16(const void* p, int64_t ld) { return ((uintptr_t)p & 15) == 0 && (
 
 }  // namespace
 
-ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k,
-                                int64_t ld_v, const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len,
-                                int64_t head_dim, int causal, float scale, float p_drop, uint64_t seed, float* out,
-                                int64_t ld_out, float* lse, uint8_t* drop_mask, void* stream) {
+// kernel families (asme_attention_*_kernels): 0 = automatic (resident kernels whenever the head's operands fit LDS;
+// backward: dK/dV storing dS, then dQ = dS K), 1 = streaming kernels only, 2 = resident kernels with the backward's
+// dQ pass recomputing S and dP (the round-2 path).  1 and 2 exist for the kernel tests and same-process A/B timing;
+// the product entry points asme_attention_fwd / _bwd always take 0.  A per-call argument: no process state.
+ASME_API int asme_attention_fwd_kernels(int kernels, const float* q, const float* k, const float* v, int64_t ld_q,
+                                        int64_t ld_k, int64_t ld_v, const uint8_t* key_valid, int64_t batch,
+                                        int64_t heads, int64_t seq_len, int64_t head_dim, int causal, float scale,
+                                        float p_drop, uint64_t seed, float* out, int64_t ld_out, float* lse,
+                                        uint8_t* drop_mask, void* stream) {
     ASME_CHECK_ARG(q && k && v && out && lse, "asme_attention_fwd: null pointer");
+    ASME_CHECK_ARG(kernels >= 0 && kernels <= 2, "asme_attention_fwd: kernel family must be 0, 1 or 2");
     ASME_CHECK_ARG(seq_len >= 1 && seq_len <= kMaxL, "asme_attention_fwd: seq_len must be in [1, 1024]");
     ASME_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "asme_attention_fwd: dropout p must be in [0,1)");
     ASME_CHECK_ARG(aligned16(out, ld_out) && aligned16(q, ld_q) && aligned16(k, ld_k) && aligned16(v, ld_v),
@@ -1208,7 +1212,7 @@ ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, 
     const dim3 grid((unsigned)((seq_len + kQB - 1) / kQB), (unsigned)(batch * heads));
     const size_t lds = res_lds_bytes((int)seq_len, (int)head_dim, false);
     ASME_DK_DISPATCH(head_dim,
-        if (g_attention_mode != 1 && res_prepare(attn_fwd_res_kernel<DK>, lds))
+        if (kernels != 1 && res_prepare(attn_fwd_res_kernel<DK>, lds))
             hipLaunchKernelGGL(attn_fwd_res_kernel<DK>, dim3((unsigned)(batch * heads)), dim3(kResThreads), lds,
                                (hipStream_t)stream, q, k, v, ld_q, ld_k, ld_v, out, ld_out, lse, key_valid,
                                (int)heads, (int)seq_len, causal, scale, p_drop, seed, drop_mask);
@@ -1219,6 +1223,14 @@ ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, 
     ASME_LAUNCH_CHECK("asme_attention_fwd");
 }
 
+ASME_API int asme_attention_fwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k,
+                                int64_t ld_v, const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len,
+                                int64_t head_dim, int causal, float scale, float p_drop, uint64_t seed, float* out,
+                                int64_t ld_out, float* lse, uint8_t* drop_mask, void* stream) {
+    return asme_attention_fwd_kernels(0, q, k, v, ld_q, ld_k, ld_v, key_valid, batch, heads, seq_len, head_dim, causal,
+                                      scale, p_drop, seed, out, ld_out, lse, drop_mask, stream);
+}
+
 // workspace of asme_attention_bwd: D_i (batch*heads*seq_len floats), then (256-B aligned) the dS image of the
 // resident path ((batch*heads) x Lp x Lp floats, Lp = seq_len rounded up to 16)
 ASME_API int64_t asme_attention_bwd_workspace(int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim) {
@@ -1227,13 +1239,15 @@ ASME_API int64_t asme_attention_bwd_workspace(int64_t batch, int64_t heads, int6
     return ((batch * heads * seq_len * 4 + 255) & ~(int64_t)255) + batch * heads * Lp * Lp * 4;
 }
 
-ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k,
-                                int64_t ld_v, const float* out, int64_t ld_out, const float* dout, int64_t ld_dout,
-                                const float* lse, const uint8_t* key_valid, int64_t batch, int64_t heads,
-                                int64_t seq_len, int64_t head_dim, int causal, float scale, float p_drop,
-                                uint64_t seed, const uint8_t* drop_mask, float* workspace, float* dq, int64_t ld_dq,
-                                float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream) {
+ASME_API int asme_attention_bwd_kernels(int kernels, const float* q, const float* k, const float* v, int64_t ld_q,
+                                        int64_t ld_k, int64_t ld_v, const float* out, int64_t ld_out,
+                                        const float* dout, int64_t ld_dout, const float* lse,
+                                        const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len,
+                                        int64_t head_dim, int causal, float scale, float p_drop, uint64_t seed,
+                                        const uint8_t* drop_mask, float* workspace, float* dq, int64_t ld_dq,
+                                        float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream) {
     ASME_CHECK_ARG(q && k && v && out && dout && lse && workspace && dq && dk && dv, "asme_attention_bwd: null pointer");
+    ASME_CHECK_ARG(kernels >= 0 && kernels <= 2, "asme_attention_bwd: kernel family must be 0, 1 or 2");
     float* dsum_ws = workspace;
     float* ds_ws = workspace + ((batch * heads * seq_len * 4 + 255) & ~(int64_t)255) / 4;
     ASME_CHECK_ARG(seq_len >= 1 && seq_len <= kMaxL, "asme_attention_bwd: seq_len must be in [1, 1024]");
@@ -1250,7 +1264,7 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
     const size_t lds_ds = ds_lds_bytes((int)seq_len, (int)head_dim);
     ASME_DK_DISPATCH(
         head_dim,
-        if (g_attention_mode == 0 && res_prepare(attn_bwd_dkdv_res_kernel<DK, true>, lds_kv) &&
+        if (kernels == 0 && res_prepare(attn_bwd_dkdv_res_kernel<DK, true>, lds_kv) &&
             res_prepare(attn_bwd_dq_ds_kernel<DK>, lds_ds)) {
             // dK/dV first (it stores dS), then dQ = dS K: five products instead of seven
             hipLaunchKernelGGL((attn_bwd_dkdv_res_kernel<DK, true>), rgrid, dim3(kResThreadsKV), lds_kv, s, q, k, v,
@@ -1258,7 +1272,7 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
                                (int)heads, (int)seq_len, causal, scale, p_drop, seed, drop_mask, out, ld_out, ds_ws);
             hipLaunchKernelGGL(attn_bwd_dq_ds_kernel<DK>, rgrid, dim3(kDsThreads), lds_ds, s, k, ld_k, ds_ws, dq, ld_dq,
                                key_valid, (int)heads, (int)seq_len, causal, scale);
-        } else if (g_attention_mode != 1 && res_prepare(attn_bwd_dq_res_kernel<DK>, lds_dq) &&
+        } else if (kernels != 1 && res_prepare(attn_bwd_dq_res_kernel<DK>, lds_dq) &&
                    res_prepare(attn_bwd_dkdv_res_kernel<DK, false>, lds_kv)) {
             hipLaunchKernelGGL(attn_bwd_dq_res_kernel<DK>, rgrid, dim3(kResThreads), lds_dq, s, q, k, v, ld_q, ld_k,
                                ld_v, out, ld_out, dout, ld_dout, lse, dsum_ws, dq, ld_dq, key_valid, (int)heads,
@@ -1278,16 +1292,18 @@ ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, 
     ASME_LAUNCH_CHECK("asme_attention_bwd");
 }
 
+ASME_API int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k,
+                                int64_t ld_v, const float* out, int64_t ld_out, const float* dout, int64_t ld_dout,
+                                const float* lse, const uint8_t* key_valid, int64_t batch, int64_t heads,
+                                int64_t seq_len, int64_t head_dim, int causal, float scale, float p_drop,
+                                uint64_t seed, const uint8_t* drop_mask, float* workspace, float* dq, int64_t ld_dq,
+                                float* dk, int64_t ld_dk, float* dv, int64_t ld_dv, void* stream) {
+    return asme_attention_bwd_kernels(0, q, k, v, ld_q, ld_k, ld_v, out, ld_out, dout, ld_dout, lse, key_valid, batch,
+                                      heads, seq_len, head_dim, causal, scale, p_drop, seed, drop_mask, workspace, dq,
+                                      ld_dq, dk, ld_dk, dv, ld_dv, stream);
+}
+
 // bytes of the drop_mask buffer the forward fills when p_drop > 0 (nibble image + key-major words)
 ASME_API int64_t asme_attention_dropout_mask_bytes(int64_t batch, int64_t heads, int64_t seq_len) {
     return mask_total_bytes(batch * heads, (int)seq_len);
-}
-
-// 0 = automatic (resident kernels whenever the head's operands fit LDS; backward: dK/dV storing dS, then dQ = dS K),
-// 1 = streaming kernels only, 2 = resident kernels with the backward's dQ pass recomputing S and dP (the round-2
-// path, kept for same-process A/B timing).  Returns the previous mode.
-ASME_API int asme_attention_set_mode(int mode) {
-    const int prev = g_attention_mode;
-    g_attention_mode = mode;
-    return prev;
 }

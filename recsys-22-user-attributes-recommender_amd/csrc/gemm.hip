@@ -322,19 +322,18 @@ struct Plan {
 };
 
 // super-tile shape for an N x K gradient: pair two 128-column tiles along whichever side has an even count of them
-// (the FFN's 512 x 128 and 128 x 512), else one tile per workgroup.  ASME_WG_PAIR=0 disables pairing.
+// (the FFN's 512 x 128 and 128 x 512), else one tile per workgroup.  (Unpaired A/B builds: -DASME_WG_PAIR=0.)
+#ifndef ASME_WG_PAIR
+#define ASME_WG_PAIR 1
+#endif
 struct Pairing {
     int tnx, tkx;
 };
 
 Pairing pick_pairing(int64_t N, int64_t K) {
-    static const bool enabled = [] {
-        const char* e = std::getenv("ASME_WG_PAIR");
-        return !(e && e[0] == '0');
-    }();
     const int64_t ntn = (N + kTile - 1) / kTile, ntk = (K + kTile - 1) / kTile;
-    if (enabled && ntn % 2 == 0) return {2, 1};
-    if (enabled && ntk % 2 == 0) return {1, 2};
+    if (ASME_WG_PAIR && ntn % 2 == 0) return {2, 1};
+    if (ASME_WG_PAIR && ntk % 2 == 0) return {1, 2};
     return {1, 1};
 }
 
@@ -360,13 +359,11 @@ Plan make_plan(int64_t T, int64_t N, int64_t K) {
 template <int TNX, int TKX>
 hipError_t launch_weight_grad(dim3 grid, hipStream_t s, const float* dy, int64_t ld_dy, const float* x,
                               int64_t ld_x, int64_t T, int N, int K, int64_t chunk_rows, float* part, float* bpart) {
-    static bool attr = false;  // 96 / 144 KiB of dynamic LDS: opt in once per shape
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)weight_grad_kernel<TNX, TKX>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, WgShape<TNX, TKX>::LDS);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    // 96 / 144 KiB of dynamic LDS: opt in once per shape (a function-local static: thread-safe initialisation)
+    static const hipError_t attr = hipFuncSetAttribute((const void*)weight_grad_kernel<TNX, TKX>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       WgShape<TNX, TKX>::LDS);
+    if (attr != hipSuccess) return attr;
     constexpr int kLds = WgShape<TNX, TKX>::LDS;
     weight_grad_kernel<TNX, TKX><<<grid, dim3(kWgThreads), kLds, s>>>(dy, ld_dy, x, ld_x, T, N, K, chunk_rows, part,
                                                                       bpart);

@@ -234,14 +234,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
 
 // persistent grid: 2 resident workgroups per CU (VGPR-bound), a multiple of 8 for the XCD split
 int64_t linear_grid(int64_t M, int64_t N) {
-    static int n_cu = 0;
-    if (n_cu == 0) {
+    static const int n_cu = [] {  // (thread-safe initialisation)
         int dev = 0;
         hipDeviceProp_t prop;
-        n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+        return (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
                    ? prop.multiProcessorCount
                    : 256;
-    }
+    }();
     const int64_t ntiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
     const int64_t grid = std::min<int64_t>((int64_t)n_cu * 2, (ntiles + 7) / 8 * 8);
     return std::max<int64_t>(8, grid / 8 * 8);

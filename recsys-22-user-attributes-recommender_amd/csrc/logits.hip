@@ -741,13 +741,11 @@ int split(const float* X, int64_t ld, int64_t rows, int d, __bf16* planes, hipSt
 
 template <int MODE, int KB>
 int launch_engine(const LogitsArgs& a, int64_t sblocks, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)logits_engine_kernel<MODE, KB, EngineWaves<MODE>::W>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmem);
-        if (e != hipSuccess) return hip_status(e, "logits: LDS opt-in");
-        attr = true;
-    }
+    // LDS opt-in once per instantiation (a function-local static: thread-safe initialisation)
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void*)logits_engine_kernel<MODE, KB, EngineWaves<MODE>::W>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)kSmem);
+    if (attr != hipSuccess) return hip_status(attr, "logits: LDS opt-in");
     constexpr int W = EngineWaves<MODE>::W;
     hipLaunchKernelGGL((logits_engine_kernel<MODE, KB, W>), dim3((unsigned)(sblocks * a.nchunks)), dim3(W * 64), kSmem,
                        s, a);
@@ -925,17 +923,19 @@ ASME_API int64_t asme_linear_xent_fwd_dh_workspace(int64_t n, int64_t V, int64_t
            align256(p.nchunks * n * dim * 4) + align256(nb * 2 * 4 + 8);
 }
 
-// The training forward: lse (n), out = {mean loss over the valid rows, their count}, and dh_raw (n x dim, row
-// stride ld_dh) = softmax(H W^T + b) W - W[t] per valid row (0 for ignored rows): dH before the upstream scale,
+// The training forward: lse (n), out = {mean loss over the valid rows, their count}, and dh_raw (n x dim,
+// contiguous: ld_dh must equal dim, the layout asme_linear_xent_bwd_dw reads) = softmax(H W^T + b) W - W[t] per valid row (0 for ignored rows): dH before the upstream scale,
 // which asme_linear_xent_bwd_dw applies.  H (n x dim), W (V x dim), dim <= 128.
 ASME_API int asme_linear_xent_fwd_dh(const float* H, int64_t ld_h, int64_t n, int64_t dim, const float* W, int64_t ld_w,
                                      int64_t V, const float* bias, const int64_t* targets, int64_t ignore_index,
                                      float* lse, float* dh_raw, int64_t ld_dh, float* workspace, int64_t ws_bytes,
                                      float* out, void* stream) {
     ASME_CHECK_ARG(H && W && targets && lse && dh_raw && workspace && out, "asme_linear_xent_fwd_dh: null pointer");
-    ASME_CHECK_ARG(dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && ld_w % 4 == 0 && ld_dh % 2 == 0 &&
-                       ld_dh >= dim && aligned16(H) && aligned16(W),
+    ASME_CHECK_ARG(dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && ld_w % 4 == 0 && aligned16(H) &&
+                       aligned16(W),
                    "asme_linear_xent_fwd_dh: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    // dh_raw is consumed by asme_linear_xent_bwd_dw as a contiguous n x dim buffer: no other row stride
+    ASME_CHECK_ARG(ld_dh == dim, "asme_linear_xent_fwd_dh: dh_raw must be contiguous (ld_dh == dim)");
     ASME_CHECK_ARG(n >= 0 && V >= 1 && V < (1LL << 31), "asme_linear_xent_fwd_dh: bad shape");
     ASME_CHECK_ARG(ws_bytes >= asme_linear_xent_fwd_dh_workspace(n, V, dim),
                    "asme_linear_xent_fwd_dh: workspace too small");

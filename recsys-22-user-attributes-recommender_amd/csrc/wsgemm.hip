@@ -343,13 +343,10 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
     const size_t planes = (size_t)NB * K * 6;  // three bf16 planes
     const size_t stage = (size_t)kWaves * 16 * (NB + 4) * 4;
     const size_t lds = planes + (CT >= 4 && planes + stage <= (size_t)kLdsMax ? stage : 0);
-    static bool attr = false;  // opt in above 64 KiB of dynamic LDS once per instantiation
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return hip_status(e, "asme_ws_linear: LDS opt-in");
-        attr = true;
-    }
+    // opt in above 64 KiB of dynamic LDS once per instantiation (a function-local static: thread-safe initialisation)
+    static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return hip_status(attr, "asme_ws_linear: LDS opt-in");
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -41,6 +41,13 @@ def _p(module: nn.Module, training: bool) -> float:
     return float(module.p)
 
 
+def has_forward_hooks(module: nn.Module) -> bool:
+    """forward hooks or pre-hooks on `module`, or global module hooks: such a module must run as a module call"""
+    from torch.nn.modules import module as _m
+    return bool(module._forward_hooks or module._forward_pre_hooks or _m._global_forward_hooks
+                or _m._global_forward_pre_hooks)
+
+
 def key_valid_mask(padding_mask: Optional[torch.Tensor], shape) -> Optional[torch.Tensor]:
     if padding_mask is None:
         return None
@@ -122,9 +129,10 @@ class TransformerEmbedding(nn.Module):
                                  table_grad=w._asme_table_grad)
         ln2_t = (ln2.weight, ln2.bias) if ln2 is not None else None
         # the first transformer block's input LayerNorm, when the model feeds this output straight into it
-        # (TransformerEncoderModel sets it): computed by the same kernel, handed over on the output tensor
+        # (TransformerEncoderModel.fuse_embedding_norm sets it): computed by the same kernel, handed over on the output
+        # tensor.  Not while that norm carries forward hooks: then block 0 calls it as a module (TransformerLayer)
         ln3 = self.__dict__.get("_asme_next_norm")
-        if ln3 is None:
+        if ln3 is None or has_forward_hooks(ln3):
             return ops.embedding(ids, w, pos, ln1, extra, ln2_t, spec)
         x, ln = ops.embedding(ids, w, pos, ln1, extra, ln2_t, spec, ln3=ln3)
         x._asme_ln = (ln3, ln)
@@ -194,10 +202,19 @@ class PreFusionContextSequenceElementsRepresentationComponent(nn.Module):
 
 
 # ------------------------------------------------------------------------------------ transformer
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameters and state_dict keys) whose module call runs the LayerNorm kernel.  The
+    transformer blocks read the parameters directly into their fused kernels; a module call happens only where hooks
+    must see it (block 0's input norm with forward hooks registered, TransformerLayer.forward)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return ops.layer_norm(x, self)
+
+
 class SublayerConnection(nn.Module):
     def __init__(self, size, dropout):
         super().__init__()
-        self.norm = nn.LayerNorm(size)
+        self.norm = LayerNorm(size)
         self.dropout = nn.Dropout(dropout)
 
 
@@ -270,11 +287,14 @@ class TransformerLayer(nn.Module):
         if len(blocks) == 0:
             return x
         tr = self.training
+        norm0 = blocks[0].input_sublayer.norm
         pre = getattr(x, "_asme_ln", None)  # LN_in(x) of block 0, computed by the embedding kernel
-        if pre is not None and pre[0] is blocks[0].input_sublayer.norm:
+        if has_forward_hooks(norm0):
+            ln = norm0(x)  # a module call, so the hooks run (and may replace its input or output)
+        elif pre is not None and pre[0] is norm0:
             ln = pre[1]
-        else:
-            x, ln = ops.layer_norm_pass(x, blocks[0].input_sublayer.norm)
+        else:  # no hand-off (fuse_embedding_norm off, or an op between the embedding and block 0 made x anew)
+            x, ln = ops.layer_norm_pass(x, norm0)
         for i, blk in enumerate(blocks):
             att, ff = blk.attention, blk.feed_forward
             qkv = att.qkv(ln)

@@ -88,13 +88,39 @@ class TransformerEncoderModel(SequenceRecommenderModel):
         rep = Ly.TransformerSequenceRepresentationComponent(transformer_layer, bidirectional=bidirectional)
         super().__init__(embedding_layer, rep, sequence_representation_modifier_layer, projection_layer)
         self.apply(self._init_weights)
-        # the embedding output goes straight into block 0, whose first op is its input LayerNorm: let the embedding
-        # kernel compute it too (ops.embedding ln3; a plain attribute, not a registered submodule)
-        pre = type(embedding_layer) is Ly.PreFusionContextSequenceElementsRepresentationComponent
-        target = embedding_layer.item_embedding_layer if pre else embedding_layer
-        if len(transformer_layer.transformer_blocks) and type(target) is Ly.TransformerEmbedding and (
-                pre or type(embedding_layer) is Ly.TransformerEmbedding):
-            object.__setattr__(target, "_asme_next_norm", transformer_layer.transformer_blocks[0].input_sublayer.norm)
+        self.fuse_embedding_norm = True
+
+    # The embedding output goes straight into block 0, whose first op is its input LayerNorm: with
+    # fuse_embedding_norm (the default) the embedding kernel computes that LayerNorm too (ops.embedding ln3,
+    # asme_embedding_ln_fwd) and hands LN(x) to block 0 on its output tensor.  The embedding holds the norm as a plain
+    # attribute (`_asme_next_norm`, not a registered submodule: state_dict, parameters() and named_modules() are
+    # unchanged).  Fallbacks, same results: any op between the embedding and block 0 makes a new tensor without the
+    # hand-off, and block 0 normalises it itself; forward hooks on block 0's input norm (or global module hooks) make
+    # block 0 call the norm as a module so the hooks run (layers.TransformerLayer.forward).
+    @property
+    def fuse_embedding_norm(self) -> bool:
+        return self._embedding_norm_target() is not None and \
+            "_asme_next_norm" in self._embedding_norm_target().__dict__
+
+    @fuse_embedding_norm.setter
+    def fuse_embedding_norm(self, on: bool):
+        target = self._embedding_norm_target()
+        if target is None:
+            return  # this composition does not feed the embedding straight into block 0 (UBERT4Rec's user column)
+        if on:
+            norm = self._sequence_representation_layer.transformer_layer.transformer_blocks[0].input_sublayer.norm
+            object.__setattr__(target, "_asme_next_norm", norm)
+        else:
+            target.__dict__.pop("_asme_next_norm", None)
+
+    def _embedding_norm_target(self):
+        emb = self._sequence_embedding_layer
+        pre = type(emb) is Ly.PreFusionContextSequenceElementsRepresentationComponent
+        target = emb.item_embedding_layer if pre else emb
+        if len(self._sequence_representation_layer.transformer_layer.transformer_blocks) and \
+                type(target) is Ly.TransformerEmbedding and (pre or type(emb) is Ly.TransformerEmbedding):
+            return target
+        return None
 
     @staticmethod
     def _init_weights(module):

@@ -106,6 +106,9 @@ class _TableGradMixin:
         self.table_grad = mode
         self._slot_map = None
 
+    # the trainer's accumulate_grad_batches (trainer_builder.py:25): > 1 makes an unconsumed table gradient an error
+    accumulate_grad_batches: int = 1
+
     def _plan_table(self, id_sets):
         if self.table_grad != "sparse" or not self.training:
             return
@@ -116,11 +119,13 @@ class _TableGradMixin:
             self._slot_map = torch.full((table.shape[0],), -1, dtype=torch.int32, device=table.device)
         tg = table._asme_table_grad
         if tg.plan is not None and not tg.plan.consumed:
-            if tg.plan.has_gradient():
-                # a backward ran and no optimizer step consumed its rows: gradient accumulation
-                # (accumulate_grad_batches > 1), which the per-step row-sparse plan does not merge
+            if tg.plan.has_gradient() and (tg.plan.accumulate or self.accumulate_grad_batches > 1):
+                # gradient accumulation was asked for (a backward under GradientAllReduce.no_sync, or the trainer's
+                # accumulate_grad_batches > 1): the per-step row-sparse plan does not merge backward passes
                 raise RuntimeError("table_grad='sparse' takes one backward per optimizer step; use table_grad='dense' "
                                    "for gradient accumulation")
+            # otherwise a step that never reached the optimizer (a skipped step): its table gradient is dropped, as
+            # zero_grad drops a dense one
             tg.plan.release()
         tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map)
 
@@ -366,6 +371,12 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         ahead, self._rows_ahead = self._rows_ahead, None
         if ahead is not None and ahead[0] is target:
             rows, row_targets, inverse = ahead[1], ahead[2], ahead[3]
+            if rows.is_cuda:
+                # allocated on the prefetch's side stream, read on this one: keep the caching allocator from
+                # handing their blocks back to the side stream before this stream's reads are done
+                cur = torch.cuda.current_stream(rows.device)
+                for t in (rows, row_targets, inverse):
+                    t.record_stream(cur)
         else:
             rows = torch.nonzero(target.reshape(-1) != pad).squeeze(1)  # (reads the row count on the host)
             row_targets, inverse = target.reshape(-1).index_select(0, rows), None
@@ -381,7 +392,8 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         the stream that produced `batch` (a side stream) once the current step is enqueued, the host waits only
         for that stream's work -- the cloze producer -- never for the main stream's queue, which a nonzero at the
         start of the step drains.  The next training_step must receive the very same target tensor; the caller
-        makes the main stream wait for the side stream before that step."""
+        makes the main stream wait for the side stream before that step (training_step itself records the
+        prefetched tensors on its stream, so the caller need not record_stream them)."""
         target = batch[TARGET_ENTRY_NAME]
         if target.dim() != 2:
             return
@@ -406,6 +418,12 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         (the last-item mask of evaluation, last_item_mask.py:35-44): the masked positions' hidden states against the
         head through asme_catalog_rank, no (n, |V|) predictions.  masked_training_module.py:80-91 + AllItemsSampler
         + NDCG's argsort (metrics/common.py:4-27)."""
+        return self._fused_eval(batch, with_loss=False)[0]
+
+    def _fused_eval(self, batch, with_loss: bool):
+        """(ranks, loss or None) of the masked positions' targets from one encoder pass: the ranks streamed
+        through asme_catalog_rank and, with_loss, the CrossEntropyLoss(ignore_index=pad) of the same hidden states
+        on the fused logits + CE kernels (masked_training_module.py:145-147 logs it) -- no (n, |V|) predictions"""
         self._flush_table()
         sequence = build_model_input(self.model, self.item_tokenizer, batch)
         rows = self._masked_rows(batch)
@@ -413,7 +431,14 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         if rows.numel() != targets.numel():
             raise ValueError("fused masked evaluation needs exactly one masked position per sequence")
         w, b = self.model.head_weight_bias()
-        return ops.catalog_rank(self.model.encode_rows(sequence, rows), w, targets, b)
+        h = self.model.encode_rows(sequence, rows)
+        ranks = ops.catalog_rank(h, w, targets, b)
+        loss = None
+        if with_loss:
+            pad = self.item_tokenizer.pad_token_id
+            loss = (ops.linear_cross_entropy(h, w, b, targets, pad) if ops.linear_xent_ok(h, w, b)
+                    else ops.cross_entropy(ops.logits(h, w, b), targets, pad))
+        return ranks, loss
 
     def _use_fused_eval(self, targets) -> bool:
         if targets.dim() != 1 or self.metrics is None or not hasattr(self.metrics, "update_ranks"):
@@ -426,7 +451,9 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
         input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
         if self._use_fused_eval(targets) and self._masked_rows(batch).numel() == targets.numel():
             with torch.no_grad():
-                self.metrics.update_ranks(self.catalog_ranks(batch))
+                ranks, loss = self._fused_eval(batch, with_loss=True)
+                self.metrics.update_ranks(ranks)
+            self.log(LOG_KEY_TEST_LOSS if is_test else LOG_KEY_VALIDATION_LOSS, loss, prog_bar=True)
             return build_eval_step_return_dict(input_seq, None, targets)
         prediction = self._get_prediction_for_masked_item(batch, batch_idx)
         loss = ops.cross_entropy(prediction, targets, self.item_tokenizer.pad_token_id)

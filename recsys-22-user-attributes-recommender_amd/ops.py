@@ -210,6 +210,7 @@ class SparseTablePlan:
             self._offset[key] = off
             off += k
         self.consumed = False
+        self.accumulate = False  # set when a backward into this plan ran for gradient accumulation (no_sync)
         # (3, capacity, d) param / moments of unique[s] brought up to date, or None: the step's readers take
         # `rows` + `gather_ids(ids)` instead of the table (see LazyTableState.stage)
         self.staged: Optional[torch.Tensor] = None
@@ -230,6 +231,7 @@ class SparseTablePlan:
         return table, ids
 
     _distinct = False
+    accumulate = False
 
     def has(self, ids: torch.Tensor) -> bool:
         return (ids.data_ptr(), tuple(ids.shape)) in (self._offset if self._distinct else self._inverse)
@@ -266,20 +268,23 @@ class SparseTablePlan:
         return self
 
     @classmethod
-    def distinct(cls, table: torch.Tensor, ids: torch.Tensor) -> "SparseTablePlan":
+    def distinct(cls, table: torch.Tensor, ids: torch.Tensor,
+                 slot_map: Optional[torch.Tensor] = None) -> "SparseTablePlan":
         """plan over ids known to be distinct (the row-shard owner's requests at one rank): no dedup, slot s ==
         ids[s]; the rows are staged like any plan's, and a single unscaled gradient contribution (one row per
-        slot) is applied as it is -- no occurrence CSR, no reduction"""
+        slot) is applied as it is -- no occurrence CSR, no reduction.  `slot_map` ((|V|,) int32, -1 at rest): the
+        row -> slot table row_slot_map() fills on demand (the non-lazy row Adam reads it); without one that call
+        raises"""
         self = cls.__new__(cls)
         ids = _i64(ids).reshape(-1)
         n = ids.numel()
         dev = ids.device
         self.vocab, self.dim = table.shape
-        self.slot_map = None
+        self.slot_map = slot_map
         self.unique = ids
         self.count = torch.tensor([n], dtype=torch.int32).to(dev, non_blocking=True)
         self.capacity = n
-        self._slots_mapped = True
+        self._slots_mapped = False  # the map is written only when row_slot_map() asks for it
         self._distinct = True
         self.grad_scale = 1.0
         self._grad_rows = None
@@ -424,6 +429,8 @@ class SparseTablePlan:
     def row_slot_map(self) -> torch.Tensor:
         """the slot map as a row -> slot table (row r's gradient is grad_rows[map[r]], -1: none), rewritten from the
         dedup's first-occurrence entries once (asme_dedup_map_slots)"""
+        if self.slot_map is None:
+            raise RuntimeError("this plan has no row -> slot map (a distinct plan built without slot_map)")
         if not self._slots_mapped:
             call("asme_dedup_map_slots", ptr(self.unique), ptr(self.count), self.capacity, ptr(self.slot_map),
                  stream())
@@ -441,7 +448,8 @@ class SparseTablePlan:
         return self._inverse[key]
 
     def release(self):
-        if self.slot_map is not None:
+        # (a distinct plan's map holds entries only once row_slot_map() wrote them)
+        if self.slot_map is not None and (self._slots_mapped or not self._distinct):
             call("asme_dedup_reset", ptr(self.unique), ptr(self.count), self.capacity, ptr(self.slot_map), stream())
         self.consumed = True
 
@@ -1305,7 +1313,7 @@ class _AttentionFn(torch.autograd.Function):
     key_valid (B, L) uint8; causal selects SASRec's tril mask (sequence_representation.py:34-48)."""
 
     @staticmethod
-    def forward(ctx, qkv, key_valid, heads: int, causal: bool, p_drop: float):
+    def forward(ctx, qkv, key_valid, heads: int, causal: bool, p_drop: float, kernels: int):
         B, L, three_d = qkv.shape
         Dm = three_d // 3
         dk = Dm // heads
@@ -1316,16 +1324,21 @@ class _AttentionFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(dk)
         base = qkv.data_ptr()
         mask = torch.empty(_mask_bytes(B, heads, L), device=qkv.device, dtype=torch.uint8) if p_drop > 0 else None
-        call("asme_attention_fwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(key_valid), B,
-             heads, L, dk, int(causal), scale, p_drop, seed, ptr(out), Dm, ptr(lse), ptr(mask), stream())
+        if kernels == 0:
+            call("asme_attention_fwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(key_valid),
+                 B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(out), Dm, ptr(lse), ptr(mask), stream())
+        else:
+            call("asme_attention_fwd_kernels", kernels, base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d,
+                 ptr(key_valid), B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(out), Dm, ptr(lse), ptr(mask),
+                 stream())
         ctx.save_for_backward(qkv, key_valid, out, lse, mask)
-        ctx.meta = (heads, causal, p_drop, seed, scale)
+        ctx.meta = (heads, causal, p_drop, seed, scale, kernels)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         qkv, key_valid, out, lse, mask = ctx.saved_tensors
-        heads, causal, p_drop, seed, scale = ctx.meta
+        heads, causal, p_drop, seed, scale, kernels = ctx.meta
         B, L, three_d = qkv.shape
         Dm = three_d // 3
         dk = Dm // heads
@@ -1333,14 +1346,20 @@ class _AttentionFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         ws = torch.empty((_attn_bwd_ws_bytes(B, heads, L, dk) + 3) // 4, device=qkv.device, dtype=torch.float32)
         base, gb = qkv.data_ptr(), dqkv.data_ptr()
-        call("asme_attention_bwd", base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(out), Dm,
-             ptr(dout), Dm, ptr(lse), ptr(key_valid), B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(mask),
-             ptr(ws), gb, three_d, gb + 4 * Dm, three_d, gb + 8 * Dm, three_d, stream())
-        return dqkv, None, None, None, None
+        args = (base, base + 4 * Dm, base + 8 * Dm, three_d, three_d, three_d, ptr(out), Dm, ptr(dout), Dm, ptr(lse),
+                ptr(key_valid), B, heads, L, dk, int(causal), scale, p_drop, seed, ptr(mask), ptr(ws), gb, three_d,
+                gb + 4 * Dm, three_d, gb + 8 * Dm, three_d, stream())
+        if kernels == 0:
+            call("asme_attention_bwd", *args)
+        else:
+            call("asme_attention_bwd_kernels", kernels, *args)
+        return dqkv, None, None, None, None, None
 
 
-def attention(qkv, key_valid, heads: int, causal: bool, p_drop: float = 0.0):
-    return _AttentionFn.apply(qkv, key_valid, heads, causal, p_drop)
+def attention(qkv, key_valid, heads: int, causal: bool, p_drop: float = 0.0, kernels: int = 0):
+    """kernels: the kernel family (asme_attention_fwd_kernels): 0 automatic (the product path); 1 streaming only and
+    2 resident with the recomputing dQ pass for the kernel tests and A/B timing"""
+    return _AttentionFn.apply(qkv, key_valid, heads, causal, p_drop, kernels)
 
 
 # ------------------------------------------------------------------------------------ heads / losses

@@ -267,7 +267,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         if train:
             if self.exchange.world == 1:
                 # one rank: the requests are the requester's unique ids -- distinct, no owner dedup / CSR
-                own = ops.SparseTablePlan.distinct(shard, st.recv_local)
+                own = ops.SparseTablePlan.distinct(shard, st.recv_local, self._own_map)
             else:
                 own = ops.SparseTablePlan(shard, [st.recv_local], self._own_map)
                 own.grad_scale = 1.0 / self.exchange.world  # DDP averaging, applied in the ordered row sums

@@ -8,6 +8,7 @@ array is noted next to it (paths relative to /root/reference/src/asme).
 
     python tests/golden/make_golden.py            # all fixtures
     python tests/golden/make_golden.py ml1m       # only the ml-1m-shaped NDCG anchor
+    python tests/golden/make_golden.py ddp        # the DDP (multi-rank) fixtures, W = 2 and 8
 """
 from __future__ import annotations
 
@@ -394,6 +395,128 @@ def gen_narm():
     print("narm", float(loss))
 
 
+def _ddp_round(build, sd, slices, W):
+    """One Lightning-DDP step over W ranks, restated serially (the reference's multi-GPU training,
+    configs/ml-20m/unfiltered/sasrec_config.jsonnet:77-79, bert4rec_config.jsonnet:83-87): every rank starts from
+    the same parameters (DDP's broadcast), runs training_step on ITS slice (its own mean loss), backward; the
+    gradients are averaged over the ranks (DDP's all-reduce / W); every rank takes the same optimizer step.
+    Returns (per-rank losses, averaged gradients, parameters after the step)."""
+    losses, avg = [], None
+    for r in range(W):
+        model, module = build()
+        model.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in sd.items()})
+        loss = module.training_step(slices[r], 0)["loss"]
+        loss.backward()
+        losses.append(float(loss))
+        g = {n: (p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p))
+             for n, p in model.named_parameters()}
+        avg = g if avg is None else {n: avg[n] + g[n] for n in avg}
+    avg = {n: v / W for n, v in avg.items()}
+    model, module = build()
+    model.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in sd.items()})
+    for n, p in model.named_parameters():
+        p.grad = avg[n].clone()
+    opts = module.configure_optimizers()
+    opt = opts if isinstance(opts, torch.optim.Optimizer) else opts[0]
+    opt = opt[0] if isinstance(opt, (list, tuple)) else opt
+    opt.step()
+    return (np.array(losses, np.float32), {n: v.numpy() for n, v in avg.items()},
+            {n: p.detach().numpy().copy() for n, p in model.named_parameters()})
+
+
+# ragged lengths of the 16 DDP sequences: every slice of 2 (W = 8) and of 8 (W = 2) has its own token count, so the
+# per-rank mean losses differ from the global mean
+_DDP_LENGTHS = (50, 43, 37, 31, 25, 50, 12, 8, 50, 3, 17, 29, 44, 6, 1, 38)
+
+
+def gen_ddp_sasrec(worlds=(2, 8), B=16, L=50, d=128, h=2, N=2, NI=300, lengths=_DDP_LENGTHS):
+    """sasrec-neg under DDP (BASELINE C4's semantics; the row-sharded table must reproduce them):
+    SequenceNextItemPredictionTrainingModule + SASRecModel at the production widths (d = 128, h = 2, d_ff = 512),
+    L = 50, ragged sessions; per W: each rank's loss, the rank-averaged gradients, the parameters after one Adam step
+    core/modules/sequence_next_item_prediction_training_module.py:73-115,181-185, core/losses/sasrec/sas_rec_losses.py"""
+    tok = S.make_tokenizer(NI)
+    S.set_context({"item": tok})
+    from asme.core.models.sasrec.sasrec_model import SASRecModel
+    from asme.core.modules.sequence_next_item_prediction_training_module import \
+        SequenceNextItemPredictionTrainingModule
+    V = len(tok)
+
+    def build():
+        model = SASRecModel(transformer_hidden_size=d, num_transformer_heads=h, num_transformer_layers=N,
+                            max_seq_length=L, transformer_dropout=0.0)
+        return model, SequenceNextItemPredictionTrainingModule(model=model, metrics=None)
+
+    torch.manual_seed(20)
+    sd = _sd(build()[0])
+    g = torch.Generator().manual_seed(21)
+    full = _ragged_batch(g, B, L + 1, V, [n + 1 for n in lengths])
+    seq, pos = full[:, :L].clone(), full[:, 1:].clone()
+    for b, n in enumerate(lengths):
+        seq[b, n:] = PAD
+        pos[b, n:] = PAD
+    neg = torch.randint(3, V, (B, L), generator=g)
+    neg[seq == PAD] = PAD
+    out = dict(sd)
+    for W in worlds:
+        per = B // W
+        slices = [{"item": seq[r * per:(r + 1) * per], "positive_samples": pos[r * per:(r + 1) * per],
+                   "negative_samples": neg[r * per:(r + 1) * per]} for r in range(W)]
+        losses, avg, after = _ddp_round(build, sd, slices, W)
+        out[f"w{W}/loss"] = losses
+        out.update({f"w{W}/grad/{n}": v for n, v in avg.items()})
+        out.update({f"w{W}/adam1/{n}": v for n, v in after.items()})
+        print(f"ddp sasrec W={W} losses", losses)
+    out.update(dict(seq=seq.numpy(), pos=pos.numpy(), neg=neg.numpy(), worlds=np.array(worlds),
+                    cfg=np.array([B, L, d, h, N, V]), lr=np.float32(1e-3), betas=np.array([0.99, 0.998], np.float32),
+                    weight_decay=np.float32(1e-3)))
+    np.savez_compressed(os.path.join(HERE, "ddp_sasrec_neg.npz"), **out)
+
+
+def gen_ddp_kebert4rec(worlds=(2, 8), B=16, L=50, d=128, h=2, N=2, NI=300, NG=7, NT=9, K=3, lengths=_DDP_LENGTHS):
+    """KeBERT4Rec (post-fusion genre, pre-fusion tags) under DDP (BASELINE C5): MaskedTrainingModule at the production
+    widths, L = 50, ragged cloze batches (each rank's masked mean over its own masked positions); per W: each rank's
+    loss, the rank-averaged gradients, the parameters after one Adam step
+    core/models/kebert4rec/kebert4rec_model.py:24-89, core/modules/masked_training_module.py:93-111,167-189"""
+    tok = S.make_tokenizer(NI)
+    gtok = S.make_tokenizer(NG, "Genre")
+    ttok = S.make_tokenizer(NT, "Tag")
+    S.set_context({"item": tok, "genre": gtok, "tags": ttok})
+    from asme.core.models.kebert4rec.kebert4rec_model import KeBERT4RecModel
+    from asme.core.modules.masked_training_module import MaskedTrainingModule
+    V = len(tok)
+
+    def build():
+        model = KeBERT4RecModel(transformer_hidden_size=d, num_transformer_heads=h, num_transformer_layers=N,
+                                max_seq_length=L, transformer_dropout=0.0,
+                                prefusion_attributes={"tags": {"embedding_type": "linear_upscale"}},
+                                postfusion_attributes={"genre": {"embedding_type": "content_embedding"}})
+        return model, MaskedTrainingModule(model=model, metrics=None, num_warmup_steps=0)
+
+    torch.manual_seed(22)
+    sd = _sd(build()[0])
+    g = torch.Generator().manual_seed(23)
+    seq, tgt = _cloze_batch(g, B, L, V, list(lengths))
+    genre = torch.randint(3, NG + 3, (B, L), generator=g)
+    tags = torch.randint(3, NT + 3, (B, L, K), generator=g)
+    tags[:, :, 2][torch.rand(B, L, generator=g) < 0.5] = 0
+    genre[seq == PAD] = PAD
+    tags[seq == PAD] = 0
+    out = dict(sd)
+    for W in worlds:
+        per = B // W
+        slices = [{"item": seq[r * per:(r + 1) * per], "item.target": tgt[r * per:(r + 1) * per],
+                   "genre": genre[r * per:(r + 1) * per], "tags": tags[r * per:(r + 1) * per]} for r in range(W)]
+        losses, avg, after = _ddp_round(build, sd, slices, W)
+        out[f"w{W}/loss"] = losses
+        out.update({f"w{W}/grad/{n}": v for n, v in avg.items()})
+        out.update({f"w{W}/adam1/{n}": v for n, v in after.items()})
+        print(f"ddp kebert4rec W={W} losses", losses)
+    out.update(dict(seq=seq.numpy(), target=tgt.numpy(), genre=genre.numpy(), tags=tags.numpy(),
+                    worlds=np.array(worlds), cfg=np.array([B, L, d, h, N, V, len(gtok), len(ttok)]),
+                    lr=np.float32(1e-3), betas=np.array([0.99, 0.998], np.float32)))
+    np.savez_compressed(os.path.join(HERE, "ddp_kebert4rec_post.npz"), **out)
+
+
 def gen_metrics():
     """NDCG/recall/MRR via the reference metric classes (core/metrics/*.py) + AllItemsSampler."""
     from asme.core.metrics.ndcg import NormalizedDiscountedCumulativeGainMetric
@@ -610,6 +733,10 @@ if __name__ == "__main__":
         gen_kebert4rec("pre", lengths=(200, 131, 57, 8), NG=7, NT=9, K=3, **big)
         gen_ubert4rec("seg", lengths=(200, 160, 33, 4), NG=7, NU=6, K=3, **big)
         gen_ubert4rec("upscale", lengths=(200, 97, 21, 3), NG=7, NU=6, K=3, **big)
+    if "ddp" in which:
+        # multi-GPU semantics (BASELINE C4 / C5): Lightning DDP over W = 2 and 8 ranks, restated serially
+        gen_ddp_sasrec()
+        gen_ddp_kebert4rec()
     if "bert4rec_anchor" in which:
         gen_bert4rec_anchor()
     if "metrics" in which:

@@ -101,3 +101,47 @@ def close(a, b, rtol=1e-3, atol=1e-7):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.abs(a - b).max()) <= rtol * float(np.abs(b).max()) + atol
+
+
+ADAM_EPS = 1e-8
+
+
+def elem_excess(got, ref, rtol=1e-3, floor=1e-3):
+    """max over elements of |got - ref| / (rtol * (|ref| + floor * max|ref|)): <= 1 passes (the element-wise criterion
+    of test_gpu_elementwise.py: each element within rtol of its own magnitude; entries more than three decades below
+    the tensor's scale, where fp32 summation order alone decides the low bits, get an absolute floor)"""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    if ref.size == 0:
+        return 0.0
+    scale = np.abs(ref).max()
+    if scale == 0.0:
+        return 0.0 if np.abs(got).max() == 0.0 else float("inf")
+    return float((np.abs(got - ref) / (rtol * (np.abs(ref) + floor * scale))).max())
+
+
+def adam_comparable(got, ref, grad_ref):
+    """Adam's first update is lr * g / (|g| + eps): for 0 < |g| < 10 eps an fp32-rounding difference of the gradient
+    moves the parameter by a visible fraction of lr, which the reference does not determine -- those elements take the
+    reference's value (test_gpu_models._well_conditioned); the key-projection bias (an analytically zero gradient)
+    is skipped by the callers"""
+    g = np.abs(np.asarray(grad_ref))
+    return np.where((g > 0) & (g < 10 * ADAM_EPS), ref, got)
+
+
+def ddp_errors(z, world, rank, loss, grads, params, tables=(), rows=None):
+    """element-wise excess of one rank's DDP step against a make_golden.py `ddp` fixture: its loss (w{W}/loss[rank]),
+    the rank-averaged gradients (w{W}/grad/*; None entries are not checked) and the parameters after the Adam step
+    (w{W}/adam1/*).  Names in `tables` are row shards: compared against rows rank::W of the fixture's table (`rows`:
+    the shard's row count)."""
+    errs = {"loss": abs(loss - float(z[f"w{world}/loss"][rank])) / (1e-4 * abs(float(z[f"w{world}/loss"][rank])))}
+    for n, ref in prefixed(z, f"w{world}/grad").items():
+        if n.endswith("attention.linear_layers.1.bias"):
+            continue  # analytically zero: both sides are rounding noise
+        gref = ref[rank::world] if n in tables else ref
+        if grads.get(n) is not None:
+            errs["grad/" + n] = elem_excess(grads[n], gref)
+        want = z[f"w{world}/adam1/{n}"]
+        want = want[rank::world] if n in tables else want
+        errs["adam1/" + n] = elem_excess(adam_comparable(params[n], want, gref), want)
+    return errs

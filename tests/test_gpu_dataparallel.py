@@ -2,9 +2,12 @@
 
 Reference: Lightning DDP (configs/ml-20m/unfiltered/bert4rec_config.jsonnet:83-87): each rank's loss is the
 masked mean over ITS slice, gradients are averaged over ranks, then every rank takes the same Adam step.
-Each worker checks the averaged gradients (every parameter, the row-sparse item table included) and the
-parameters after one dataparallel.train_step against the same computation done serially in that process:
-the module run on each slice separately, the gradients averaged, one FusedAdam step."""
+test_dataparallel_matches_reference_ddp: each rank's loss, the averaged gradients (every parameter, the row-sparse
+item table included) and the parameters after the Adam step against the REFERENCE's DDP step (make_golden.py `ddp`:
+the reference MaskedTrainingModule run on every rank's slice, gradients averaged, one Adam step; d = 128, L = 50,
+ragged cloze batches, W = 2 and 8), element-wise at 1e-3.
+test_dataparallel_kebert4rec_matches_serial_ddp: the same step against the HIP path run serially in that process
+(the module on each slice separately, the gradients averaged, one FusedAdam step), at 1e-5."""
 import os
 import socket
 import sys
@@ -106,6 +109,66 @@ def _worker(rank, world, port, name, q):
         raise
     finally:
         dist.destroy_process_group()
+
+
+def _ref_worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import __graft_entry__
+    from helpers import build_model, ddp_errors, load, state_dict
+    asme = __graft_entry__.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    try:
+        z = load("ddp_kebert4rec_post")
+        model = build_model(asme, "kebert4rec_post", z)
+        model.load_state_dict(state_dict(z))
+        model.to(dev)
+        tok = asme.tokenization.Tokenizer(int(z["cfg"][5]) - 3)
+        module = asme.MaskedTrainingModule(model=model, item_tokenizer=tok, metrics=None, num_warmup_steps=0)
+        red = asme.dataparallel.GradientAllReduce(module, bucket_bytes=256 << 10)
+        opt, _ = asme.modules.split_optimizers(module.configure_optimizers())
+        B = z["seq"].shape[0]
+        per = B // world
+        mine = {k: torch.from_numpy(z[s][rank * per:(rank + 1) * per]).to(dev)
+                for k, s in (("item", "seq"), ("item.target", "target"), ("genre", "genre"), ("tags", "tags"))}
+        loss = module.training_step(mine, 0)["loss"]
+        asme.modules.backward(loss)
+        red.finish()  # every gradient averaged over the ranks, the row-sparse table's as a dense (|V|, d) gradient
+        named = dict(model.named_parameters())
+        grads = {n: p.grad.detach().cpu().numpy() for n, p in named.items()}
+        opt.step()
+        opt.flush()
+        params = {n: p.detach().cpu().numpy() for n, p in named.items()}
+        q.put((rank, ddp_errors(z, world, rank, float(loss), grads, params)))
+    except Exception as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_dataparallel_matches_reference_ddp(world):
+    """BASELINE C5's semantics pinned to the reference: KeBERT4Rec data parallel on W ranks == the reference module's
+    DDP step (tests/golden/ddp_kebert4rec_post.npz), element-wise"""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ref_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, errs in res.items():
+        assert isinstance(errs, dict), f"rank {rank}: {errs}"
+        bad = {k: e for k, e in errs.items() if not e <= 1.0}
+        assert not bad, (rank, bad)
+    assert all(p.exitcode == 0 for p in procs)
 
 
 @pytest.mark.parametrize("name", ["kebert4rec_pre", "kebert4rec_post_d128"])

@@ -107,6 +107,33 @@ def test_models_take_the_fused_embedding_ln(asme, dev):
         "_asme_next_norm" in k for k in m.state_dict())
 
 
+@pytest.mark.parametrize("mode", ["hook", "flag_off"])
+def test_block0_norm_fallbacks_match_the_fused_path(asme, dev, mode):
+    """A forward hook on block 0's input norm runs (the norm becomes a module call on the LayerNorm kernel), and
+    fuse_embedding_norm = False drops the hand-off; both give the fused path's output and gradients"""
+    torch.manual_seed(3)
+    res = []
+    for variant in ("fused", mode):
+        torch.manual_seed(0)
+        m = asme.SASRecModel(transformer_hidden_size=32, num_transformer_heads=2, num_transformer_layers=2,
+                             item_vocab_size=100, max_seq_length=12, transformer_dropout=0.0).to(dev)
+        norm = m._sequence_representation_layer.transformer_layer.transformer_blocks[0].input_sublayer.norm
+        fired = []
+        if variant == "hook":
+            norm.register_forward_hook(lambda mod, inp, out: fired.append(out.shape))
+        elif variant == "flag_off":
+            m.fuse_embedding_norm = False
+        seq = torch.randint(1, 100, (3, 12), generator=torch.Generator().manual_seed(1)).to(dev)
+        rep = m.encode(asme.InputSequence(seq, seq.ne(0)))
+        rep.square().sum().backward()
+        assert len(fired) == (1 if variant == "hook" else 0)
+        res.append((rep.detach(), {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}))
+    torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-5)
+    assert set(res[0][1]) == set(res[1][1])
+    for n, g in res[0][1].items():
+        torch.testing.assert_close(res[1][1][n], g, rtol=1e-4, atol=1e-4 * float(g.abs().max()) + 1e-7)
+
+
 @pytest.mark.parametrize("B,L,D", [(1024, 200, 128), (37, 13, 32), (5, 7, 6)])
 def test_position_grad_equals_batch_sum(asme, dev, B, L, D):
     """asme_position_grad (the position embedding's gradient: the token rows summed over the batch per position) vs

@@ -29,10 +29,9 @@ def _attn_ref(q, k, v, valid, causal):
 
 
 @pytest.fixture(params=[0, 1, 2], ids=["auto", "streaming", "recompute"])
-def attn_mode(request, asme):
-    prev = asme._lib.load().asme_attention_set_mode(request.param)
-    yield request.param
-    asme._lib.load().asme_attention_set_mode(prev)
+def attn_mode(request):
+    """the attention kernel family, passed per call (asme_attention_fwd_kernels / _bwd_kernels)"""
+    return request.param
 
 
 @pytest.mark.parametrize("dk", [16, 32, 64, 128])
@@ -53,7 +52,7 @@ def test_attention_fwd_bwd(asme, dev, dk, causal, L, attn_mode):
     ref.backward(g)
     # HIP
     xd = qkv.to(dev).requires_grad_(True)
-    out = asme.ops.attention(xd, valid.to(dev), H, causal, 0.0)
+    out = asme.ops.attention(xd, valid.to(dev), H, causal, 0.0, kernels=attn_mode)
     out.backward(g.to(dev))
     assert _rel(out, ref) < 1e-4
     assert _rel(xd.grad, x.grad) < 1e-3
@@ -87,16 +86,16 @@ def test_attention_dropout_mask_matches_regeneration(asme, dev, causal, attn_mod
     mask = torch.empty(asme.ops._mask_bytes(B, H, L), device=dev, dtype=torch.uint8)
     call, ptr, st = asme._lib.call, asme._lib.ptr, asme._lib.stream
     b, scale, seed = qkv.data_ptr(), dk ** -0.5, 1234567
-    call("asme_attention_fwd", b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(valid), B, H, L, dk, int(causal),
-         scale, 0.25, seed, ptr(out), D, ptr(stats), ptr(mask), st())
+    call("asme_attention_fwd_kernels", attn_mode, b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(valid), B, H, L,
+         dk, int(causal), scale, 0.25, seed, ptr(out), D, ptr(stats), ptr(mask), st())
     grads = []
     for m in (mask, None):
         g = torch.zeros_like(qkv)
         ws = torch.empty(asme.ops._attn_bwd_ws_bytes(B, H, L, dk) // 4 + 1, device=dev)
         gb = g.data_ptr()
-        call("asme_attention_bwd", b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(out), D, ptr(dout), D,
-             ptr(stats), ptr(valid), B, H, L, dk, int(causal), scale, 0.25, seed, ptr(m), ptr(ws), gb, 3 * D,
-             gb + 4 * D, 3 * D, gb + 8 * D, 3 * D, st())
+        call("asme_attention_bwd_kernels", attn_mode, b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(out), D,
+             ptr(dout), D, ptr(stats), ptr(valid), B, H, L, dk, int(causal), scale, 0.25, seed, ptr(m), ptr(ws), gb,
+             3 * D, gb + 4 * D, 3 * D, gb + 8 * D, 3 * D, st())
         grads.append(g)
     torch.cuda.synchronize()
     assert torch.equal(grads[0], grads[1])
@@ -110,15 +109,12 @@ def test_attention_resident_matches_streaming_with_dropout(asme, dev, causal):
     qkv = torch.randn(B, L, 3 * H * dk, device=dev)
     valid = (torch.arange(L).unsqueeze(0) < torch.tensor([200, 150, 1, 0]).unsqueeze(1)).to(torch.uint8).to(dev)
     g = torch.randn(B, L, H * dk, device=dev)
-    lib = asme._lib.load()
     res = []
     for mode in (0, 1, 2):
-        prev = lib.asme_attention_set_mode(mode)
         x = qkv.clone().requires_grad_(True)
         torch.manual_seed(11)
-        out = asme.ops.attention(x, valid, H, causal, 0.2)
+        out = asme.ops.attention(x, valid, H, causal, 0.2, kernels=mode)
         out.backward(g)
-        lib.asme_attention_set_mode(prev)
         res.append((out.detach(), x.grad))
     for other in res[1:]:
         assert _rel(res[0][0], other[0]) < 1e-5
@@ -565,9 +561,11 @@ def test_sasrec_sparse_lazy_matches_dense_training(asme, dev):
         assert _rel(results[1][k], results[0][k]) < 1e-5, k
 
 
-def test_sharded_module_single_rank_matches_unsharded(asme, dev):
+@pytest.mark.parametrize("lazy_table", [True, False])
+def test_sharded_module_single_rank_matches_unsharded(asme, dev, lazy_table):
     """The row-sharded training path (dedup -> all_to_all routing -> owner catch-up/gather -> compact
-    table -> grad push -> lazy Adam on the shard) on a 1-rank RCCL group equals plain training."""
+    table -> grad push -> lazy Adam on the shard) on a 1-rank RCCL group equals plain training.  lazy_table=False:
+    the owner's distinct-id plan hands the non-lazy row Adam (asme_adam_rows_step) its row -> slot map."""
     import os
     import torch.distributed as dist
     from helpers import build_model, load, state_dict
@@ -576,9 +574,12 @@ def test_sharded_module_single_rank_matches_unsharded(asme, dev):
     batch = {k: torch.from_numpy(z[s]).to(dev) for k, s in
              (("item", "seq"), ("positive_samples", "pos"), ("negative_samples", "neg"))}
     tok = asme.tokenization.Tokenizer(V - 3)
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29533")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
     try:
         out = []
         for sharded in (False, True):
@@ -588,7 +589,9 @@ def test_sharded_module_single_rank_matches_unsharded(asme, dev):
             if sharded:
                 module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(
                     model=model, item_tokenizer=tok, metrics=None, vocab=V)
-                opt = module.configure_optimizers()
+                opt = asme.optim.FusedAdam(module.parameters(), lr=module.learning_rate,
+                                           betas=(module.beta_1, module.beta_2), weight_decay=module.weight_decay,
+                                           lazy_table=lazy_table)
                 for i in range(3):
                     asme.sharded.train_step(module, opt, batch, i)
             else:

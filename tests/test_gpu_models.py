@@ -239,11 +239,19 @@ def test_bert4rec_anchor_ndcg(asme, dev, fused_eval):
     container = asme.metrics.RankingMetricsContainer([ndcg])
     module = asme.MaskedTrainingModule(model=model, item_tokenizer=tok, metrics=container, fused_eval=fused_eval)
     module.eval()
+    logged = {}
+    module.log = lambda key, value, **kw: logged.setdefault(key, []).append(float(value))
     seqs = torch.from_numpy(z["eval_seq"].astype(np.int64))
     targets = torch.from_numpy(z["targets"])
     with torch.no_grad():
         for i in range(0, n_users, 512):
-            out = module.validation_step({"item": seqs[i:i + 512].to(dev), "item.target": targets[i:i + 512].to(dev)}, 0)
+            b = {"item": seqs[i:i + 512].to(dev), "item.target": targets[i:i + 512].to(dev)}
+            out = module.validation_step(b, 0)
             assert (out["predictions"] is None) == fused_eval
+            # val_loss is logged on both paths (masked_training_module.py:145-147): CE of the masked predictions
+            want = torch.nn.functional.cross_entropy(module.predict_step(b, 0).double().cpu(), b["item.target"].cpu(),
+                                                     ignore_index=0)
+            assert abs(logged["val_loss"][-1] - float(want)) <= 1e-4 * abs(float(want)), (logged["val_loss"][-1], want)
+    assert len(logged["val_loss"]) == (n_users + 511) // 512
     got = float(ndcg.compute())
     assert abs(got - float(z["ndcg10"])) <= 1e-4, (got, float(z["ndcg10"]))

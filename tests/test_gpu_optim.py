@@ -136,3 +136,25 @@ def test_staged_rows_match_in_place_catch_up(asme, dev, monkeypatch):
     for a, b in ((out[0], out[4]), (out[1], out[5]), (out[2], out[4]), (out[3], out[5])):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+def test_skipped_optimizer_step_drops_the_table_gradient(asme, dev):
+    """a backward whose optimizer step is skipped (a GradScaler inf/NaN skip, a trainer skipping the step) drops the
+    row-sparse table gradient, as zero_grad drops a dense one: the next step equals a run without the skipped
+    backward.  Gradient accumulation (accumulate_grad_batches > 1) raises instead of merging silently."""
+    out = []
+    for skip in (False, True):
+        model, module, batch = _sasrec(asme, dev, "sparse")
+        opt = module.configure_optimizers()
+        if skip:
+            module.training_step(batch, 0)["loss"].backward()   # no optimizer step follows
+            opt.zero_grad()
+        asme.modules.train_step(module, opt, None, batch, 0)
+        out.append(_params(model))
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
+    model, module, batch = _sasrec(asme, dev, "sparse")
+    module.accumulate_grad_batches = 2
+    module.training_step(batch, 0)["loss"].backward()
+    with pytest.raises(RuntimeError, match="gradient accumulation"):
+        module.training_step(batch, 1)

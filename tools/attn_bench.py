@@ -23,11 +23,10 @@ def main():
     ap.add_argument("--heads", type=int, default=2)
     ap.add_argument("--dk", type=int, default=64)
     ap.add_argument("--bidir", action="store_true")
-    ap.add_argument("--modes", default="0,1", help="asme_attention_set_mode values to alternate: 0 auto (resident "
+    ap.add_argument("--modes", default="0,1", help="attention kernel families to alternate (ops.attention kernels=): 0 auto (resident "
                                                    "kernels where the head fits LDS), 1 streaming")
     a = ap.parse_args()
     asme = __graft_entry__.load_package()
-    lib = asme._lib.load()
     dev = torch.device("cuda", 0)
     B, L, H, dk = a.batch, a.seq, a.heads, a.dk
     D = H * dk
@@ -42,10 +41,9 @@ def main():
     res = {m: ([], []) for m in modes}
     for rep in range(a.reps):
         for mode in modes:
-            lib.asme_attention_set_mode(mode)
             for it in range(a.iters + 2):
                 ev[0].record()
-                out = asme.ops.attention(qkv, valid, H, causal, a.dropout)
+                out = asme.ops.attention(qkv, valid, H, causal, a.dropout, kernels=mode)
                 ev[1].record()
                 out.backward(g)
                 ev[2].record()
@@ -54,7 +52,6 @@ def main():
                     res[mode][0].append(ev[0].elapsed_time(ev[1]))
                     res[mode][1].append(ev[1].elapsed_time(ev[2]))
                 qkv.grad = None
-    lib.asme_attention_set_mode(0)
     unit = 2.0 * B * H * dk * (L * (L + 1) / 2 if causal else L * L)  # one causal-aware matmul pass
     for mode in modes:
         tf, tb = sorted(res[mode][0]), sorted(res[mode][1])
