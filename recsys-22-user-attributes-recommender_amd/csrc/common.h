@@ -221,4 +221,16 @@ __device__ __forceinline__ floatx4 mfma_bf3(const Bf3& a, const Bf3& b, floatx4 
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, acc, 0, 0, 0);
 }
 
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// acc += a . b over one 16-k step of v_mfma_f32_32x32x16_bf16, the six bf16x6 terms smallest first
+__device__ __forceinline__ floatx16 mfma32_bf3(const Bf3& a, const Bf3& b, floatx16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
+}
+
 }  // namespace asme

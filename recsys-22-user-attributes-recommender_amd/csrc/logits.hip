@@ -176,18 +176,6 @@ struct TileMeta {
     }
 };
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-// acc += a . b over one 16-k step of v_mfma_f32_32x32x16_bf16, the six bf16x6 terms smallest first
-__device__ __forceinline__ floatx16 mfma32_bf3(const Bf3& a, const Bf3& b, floatx16 acc) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
-}
-
 // 32x32x16 fragment maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) supplies A[row r][k 8h..8h+7]
 // and B[k 8h..8h+7][col r]; accumulator register i holds C[row (i & 3) + 8 (i >> 2) + 4h][col r].
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }

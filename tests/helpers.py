@@ -120,13 +120,19 @@ def elem_excess(got, ref, rtol=1e-3, floor=1e-3):
     return float((np.abs(got - ref) / (rtol * (np.abs(ref) + floor * scale))).max())
 
 
-def adam_comparable(got, ref, grad_ref):
-    """Adam's first update is lr * g / (|g| + eps): for 0 < |g| < 10 eps an fp32-rounding difference of the gradient
-    moves the parameter by a visible fraction of lr, which the reference does not determine -- those elements take the
-    reference's value (test_gpu_models._well_conditioned); the key-projection bias (an analytically zero gradient)
-    is skipped by the callers"""
-    g = np.abs(np.asarray(grad_ref))
-    return np.where((g > 0) & (g < 10 * ADAM_EPS), ref, got)
+def adam_excess(got, want, g, lr, rtol=1e-3, floor=1e-3):
+    """element-wise excess of a parameter after Adam's first step, lr * g / (|g| + eps) with g the total gradient
+    (weight decay included): the parameter's own element-wise bound plus what the gradient's element-wise bound
+    (rtol * (|g| + floor * max|g|), the one the gradients are held to) moves the update by -- its derivative
+    lr * eps / (|g| + eps)^2 is large only for |g| within a few decades of eps, where fp32 summation order alone
+    decides the gradient's low bits"""
+    got, want, g = (np.asarray(x, np.float64) for x in (got, want, g))
+    if want.size == 0:
+        return 0.0
+    ag = np.abs(g)
+    tol = rtol * (np.abs(want) + floor * np.abs(want).max()) + \
+        lr * ADAM_EPS / (ag + ADAM_EPS) ** 2 * rtol * (ag + floor * ag.max())
+    return float((np.abs(got - want) / tol).max())
 
 
 def ddp_errors(z, world, rank, loss, grads, params, tables=(), rows=None):
@@ -142,6 +148,9 @@ def ddp_errors(z, world, rank, loss, grads, params, tables=(), rows=None):
         if grads.get(n) is not None:
             errs["grad/" + n] = elem_excess(grads[n], gref)
         want = z[f"w{world}/adam1/{n}"]
-        want = want[rank::world] if n in tables else want
-        errs["adam1/" + n] = elem_excess(adam_comparable(params[n], want, gref), want)
+        p0 = z["sd/" + n]
+        if n in tables:
+            want, p0 = want[rank::world], p0[rank::world]
+        wd = float(z["weight_decay"]) if "weight_decay" in z.files else 0.0
+        errs["adam1/" + n] = adam_excess(params[n], want, gref + wd * p0, float(z["lr"]))
     return errs

@@ -141,7 +141,7 @@ def _ref_worker(rank, world, port, q):
         opt.step()
         opt.flush()
         params = {n: p.detach().cpu().numpy() for n, p in named.items()}
-        q.put((rank, ddp_errors(z, world, rank, float(loss), grads, params)))
+        q.put((rank, ddp_errors(z, world, rank, float(loss.detach()), grads, params)))
     except Exception as e:
         q.put((rank, repr(e)))
         raise

@@ -179,7 +179,7 @@ def _ddp_worker(rank, world, port, q):
         opt.flush()
         params = {n: p.detach().cpu().numpy() for n, p in named.items()}
         table_names = {n for n, p in named.items() if p is table}
-        q.put((rank, ddp_errors(z, world, rank, float(loss), grads, params, table_names)))
+        q.put((rank, ddp_errors(z, world, rank, float(loss.detach()), grads, params, table_names)))
     except Exception as e:
         q.put((rank, repr(e)))
         raise

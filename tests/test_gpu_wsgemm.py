@@ -18,7 +18,7 @@ def _call(asme, x, w, N, trans, bias=None, epi=0, pre_out=None, pre_in=None, p=0
 
 
 @pytest.mark.parametrize("M", [1, 17, 1000, 4099, 65536 + 48])
-@pytest.mark.parametrize("K,N", [(128, 128), (128, 384), (128, 512), (512, 128), (384, 128), (256, 64)])
+@pytest.mark.parametrize("K,N", [(128, 128), (128, 256), (128, 384), (128, 512), (512, 128), (384, 128), (256, 64)])
 def test_ws_linear_matches_fp64(asme, dev, M, K, N):
     torch.manual_seed(M + K + N)
     assert asme._lib.load().asme_ws_linear_supported(M, K, N) == 1
