@@ -42,6 +42,10 @@
 #ifndef ASME_LOGITS_PIPE
 #define ASME_LOGITS_PIPE 0
 #endif
+#ifndef ASME_LOGITS_DIAG
+#define ASME_LOGITS_DIAG 0  // diagnostic builds of the fdh pass: 1 no gradient product, 2 no score product, 3 no exp,
+                            // 4 no next-tile DMA (the current tile re-used)
+#endif
 
 using namespace asme;
 
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
         const int cur = it & 1;
         const bool more = r0 + kTS < s_end;
         if (more) {  // the next tile flies into the other buffer during this tile's MFMAs
-            dma_tile<W>(a.strm, a.strm_pad, r0 + kTS, bufs + (cur ^ 1) * kTile);
+            if (ASME_LOGITS_DIAG != 4 || MODE != M_FDH) dma_tile<W>(a.strm, a.strm_pad, r0 + kTS, bufs + (cur ^ 1) * kTile);
             if (threadIdx.x < kTS) tm.load(MODE, a, r0 + kTS + threadIdx.x);
         }
         const char* buf = bufs + cur * kTile;
@@ -305,7 +309,13 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
                 for (int ft = 0; ft < NFT; ++ft) y[ft] = mfma32_bf3(grad_a(sub, s2, ft), P[s2], y[ft]);
         };
         if constexpr (MODE == M_FDH) {
+#if ASME_LOGITS_DIAG == 2
+            floatx16 xs[2];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) xs[0][i] = xs[1][i] = tf[i] * (float)(i + 1);
+#else
             floatx16 xs[2] = {score(0), score(1)};
+#endif
             float tmax = -INFINITY;
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) {
@@ -345,7 +355,11 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
             for (int sub = 0; sub < 2; ++sub) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
+#if ASME_LOGITS_DIAG == 3
+                    xs[sub][i] = xs[sub][i] - base;
+#else
                     xs[sub][i] = __expf(xs[sub][i] - base);
+#endif
                     run_sum += xs[sub][i];
                 }
                 Bf3 P[2];
@@ -355,7 +369,11 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
                         make_float4(xs[sub][8 * s2], xs[sub][8 * s2 + 1], xs[sub][8 * s2 + 2], xs[sub][8 * s2 + 3]),
                         make_float4(xs[sub][8 * s2 + 4], xs[sub][8 * s2 + 5], xs[sub][8 * s2 + 6],
                                     xs[sub][8 * s2 + 7]));
+#if ASME_LOGITS_DIAG == 1
+                asm volatile("" ::"v"(P[0].h), "v"(P[0].m), "v"(P[0].l), "v"(P[1].h), "v"(P[1].m), "v"(P[1].l));
+#else
                 grad(sub, P);
+#endif
             }
         } else if constexpr (MODE == M_DH || MODE == M_DW) {
 #if ASME_LOGITS_PIPE
