@@ -103,8 +103,14 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     // row-major staging of the finished tile (per wave, 16 rows x NB, 16-B row pad) so each store instruction
     // writes whole rows (16 lanes x 16 B = 256 B of one row at NB = 64) instead of 16 rows x 64 B (measured:
     // N = 384 / 512 launches 12-23 % faster); not where the W planes leave no room for it
-    constexpr int NB4 = NB / 4, SROW = NB + 4;
+    // CT = 8 (128-feature blocks, K = 128: the W planes take 96 KiB): the staging rows are not padded but their
+    // 16-B chunks XOR-swizzled by the row (the 160 KiB hold planes + staging exactly), conflict-free both ways
+    constexpr bool kSwz = CT == 8;
+    constexpr int NB4 = NB / 4, SROW = kSwz ? NB : NB + 4;
     constexpr bool kStage = CT >= 4 && NB * K * 6 + kWaves * 16 * SROW * 4 <= kLdsMax;  // (CT = 2: no gain)
+    // W fragments in flight: one k32 block ahead for every feature tile (CT <= 6), or a ring of four tiles ahead
+    // (CT = 8: 48 instead of 96 registers; still 24 MFMAs between a fragment's read and its use)
+    constexpr int WR = CT <= 6 ? CT : 4;
     extern __shared__ __attribute__((aligned(16))) uint4 lds16[];
     const int nblk = N / NB;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
@@ -154,11 +160,15 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const __amdgpu_buffer_rsrc_t pr = EPI == WS_ACCUM ? yr
                                     : rsrc(EPI == WS_GELU_DROP ? (const void*)ep.pre_out : (const void*)ep.pre_in,
                                            EPI == WS_STORE ? 0 : M * N * 4);
-    float4 breg[CT];
+    // the bias: added where the staged tile is read back when every read of a lane falls on the same float4 of
+    // the feature block (64 % NB4 == 0: one register set instead of CT), else to the accumulators at the tile's end
+    constexpr bool kBiasEpi = kStage && 64 % NB4 == 0;
+    float4 breg[kBiasEpi ? 1 : CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-        breg[ct] = ep.bias ? *reinterpret_cast<const float4*>(ep.bias + n0 + ct * 16 + 4 * g)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ct = 0; ct < (kBiasEpi ? 1 : CT); ++ct)
+        breg[ct] = !ep.bias ? make_float4(0.f, 0.f, 0.f, 0.f)
+                 : kBiasEpi ? *reinterpret_cast<const float4*>(ep.bias + n0 + 4 * ((threadIdx.x & 63) % NB4))
+                            : *reinterpret_cast<const float4*>(ep.bias + n0 + ct * 16 + 4 * g);
     const float keep_k = ep.p > 0.f ? 1.f / (1.f - ep.p) : 1.f;
     const uint32_t thr = gelu_thresh(ep.p);
     uint32_t pend = 0;  // GELU-dropout bits of the odd feature tile of the current pair
@@ -180,6 +190,9 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         const int idx = 64 * ct + (threadIdx.x & 63), row = idx / NB4, c4 = idx % NB4;
         return r0 + row < M ? (uint32_t)(((r0 + row) * N + n0 + 4 * c4) * 4) : kDrop;
     };
+    auto stg_at = [&](int row, int c4) -> float* {  // float4 chunk c4 of staging row `row` (row < 16)
+        return stg + row * SROW + 4 * (kSwz ? (c4 ^ row) : c4);
+    };
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) stash[ct] = pre[ct] = make_float4(0.f, 0.f, 0.f, 0.f);
     // W operand of feature tile ct, k32 block kb: row ct*16 + c16, k 8g..8g+7 of the three planes
@@ -191,15 +204,16 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         w.l = __builtin_bit_cast(bf16x8, lds16[2 * PL + sl]);
         return w;
     };
-    Bf3 wc[CT];
+    Bf3 wc[WR];  // wc[ct % WR] holds tile ct's fragment of the current block when its MFMAs run
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) wc[ct] = wload(ct, 0);
+    for (int ct = 0; ct < WR; ++ct) wc[ct] = wload(ct, 0);
     Bf3 xs = split_bf3(ring[0], ring[1]);
     // the stashed tile's epilogue for one 16-feature tile
     auto epilogue = [&](int ct) {
         if constexpr (kStage) {
             const int idx = 64 * ct + (threadIdx.x & 63);
-            const float4 v = *reinterpret_cast<const float4*>(stg + (idx / NB4) * SROW + 4 * (idx % NB4));
+            float4 v = *reinterpret_cast<const float4*>(stg_at(idx / NB4, idx % NB4));
+            if constexpr (kBiasEpi) v = make_float4(v.x + breg[0].x, v.y + breg[0].y, v.z + breg[0].z, v.w + breg[0].w);
             const uint32_t off = staged_off(ct, srow0);
             if constexpr (EPI == WS_STORE) {
                 bstore(v, yr, off, nt_out);
@@ -282,12 +296,13 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
 #if ASME_WS_DIAG != 1
-                acc[ct] = mfma_bf3(wc[ct], xs, acc[ct]);
+                acc[ct] = mfma_bf3(wc[ct % WR], xs, acc[ct]);
 #else
-                acc[ct][0] += (float)xs.h[0] + (float)wc[ct].h[0];
+                acc[ct][0] += (float)xs.h[0] + (float)wc[ct % WR].h[0];
 #endif
 #if ASME_WS_DIAG != 3
-                wc[ct] = wload(ct, kbn);
+                // the fragment WR tiles on: tile ct + WR of this block, or (past the last tile) of the next block
+                wc[ct % WR] = ct + WR < CT ? wload(ct + WR, kb) : wload(ct + WR - CT, kbn);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -317,16 +332,17 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             srow0 = (t0 + j * wcount) * 16;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
-                *reinterpret_cast<float4*>(stg + c16 * SROW + ct * 16 + 4 * g) =
-                    make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
-                                acc[ct][3] + breg[ct].w);
+                *reinterpret_cast<float4*>(stg_at(c16, ct * 4 + g)) =
+                    kBiasEpi ? make_float4(acc[ct][0], acc[ct][1], acc[ct][2], acc[ct][3])
+                             : make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
+                                           acc[ct][3] + breg[ct].w);
                 if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM) pre[ct] = bload(pr, staged_off(ct, srow0));
             }
         } else {
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
-                stash[ct] = make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
-                                        acc[ct][3] + breg[ct].w);
+                stash[ct] = make_float4(acc[ct][0] + breg[kBiasEpi ? 0 : ct].x, acc[ct][1] + breg[kBiasEpi ? 0 : ct].y,
+                                        acc[ct][2] + breg[kBiasEpi ? 0 : ct].z, acc[ct][3] + breg[kBiasEpi ? 0 : ct].w);
                 if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM) pre[ct] = bload(pr, soff + ct * 64);
             }
         }
@@ -341,7 +357,7 @@ template <int K, int CT, bool TRANS, int EPI>
 int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
     constexpr int NB = 16 * CT;
     const size_t planes = (size_t)NB * K * 6;  // three bf16 planes
-    const size_t stage = (size_t)kWaves * 16 * (NB + 4) * 4;
+    const size_t stage = (size_t)kWaves * 16 * (CT == 8 ? NB : NB + 4) * 4;  // (the kernel's SROW)
     const size_t lds = planes + (CT >= 4 && planes + stage <= (size_t)kLdsMax ? stage : 0);
     // opt in above 64 KiB of dynamic LDS once per instantiation (a function-local static: thread-safe initialisation)
     static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI>,
@@ -358,8 +374,14 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
 // features per workgroup: 64; 96 when N / 64 does not divide the 32 workgroups of an XCD (N = 384, K = 128:
 // wider tiles at larger K run out of registers); 32 when a 64-feature block of the three bf16 planes would
 // not fit the LDS (K = 512); else 64 with the XCD's leftover workgroups idle
+#ifndef ASME_WS_CT8
+#define ASME_WS_CT8 1
+#endif
 int pick_ct(int N, int K) {
     const bool fit4 = 64 * K * 6 <= kLdsMax;
+    // K = 128 with whole 128-feature blocks that split an XCD's 32 workgroups: each X tile is split once per 128
+    // features instead of once per 64 (the split's VALU does not overlap the MFMAs, §4)
+    if (ASME_WS_CT8 && K == 128 && N % 128 == 0 && 32 % (N / 128) == 0) return 8;
     if (N % 64 == 0 && 32 % (N / 64) == 0 && fit4) return 4;
     if (K == 128 && N % 96 == 0 && 32 % (N / 96) == 0) return 6;
     if (N % 32 == 0 && 32 % (N / 32) == 0 && 32 * K * 6 <= kLdsMax) return 2;
@@ -373,6 +395,11 @@ int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float*
         if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
     if constexpr (K == 128)
         if (ct == 6) return launch_ws<K, 6, TRANS, EPI>(X, M, W, N, Y, ep, s);
+    // (the activation-factor epilogue keeps 64-feature blocks: its CT factor registers would spill at CT = 8)
+    if constexpr (K == 128 && EPI != WS_GELU_BWD)
+        if (ct == 8) return launch_ws<K, 8, TRANS, EPI>(X, M, W, N, Y, ep, s);
+    if constexpr (K == 128 && EPI == WS_GELU_BWD)
+        if (ct == 8) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
     return launch_ws<K, 2, TRANS, EPI>(X, M, W, N, Y, ep, s);
 }
 
