@@ -157,10 +157,15 @@ __device__ __forceinline__ void load_row_slice(const float* __restrict__ rowp, b
     }
 }
 
-// acc[sub] += Tile[sub*16 + c16][slice g] . f  (16 x 16 result per sub-tile, rows of the tile on C/D rows)
-template <int DK, int NS = kNS>
+struct NoFill {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+// acc[sub] += Tile[sub*16 + c16][slice g] . f  (16 x 16 result per sub-tile, rows of the tile on C/D rows).
+// fill(s4) runs after step s4's MFMAs are issued, in the same scheduling region: independent vector work of the
+// caller that issues in the shadow of this wave's MFMAs.
+template <int DK, int NS = kNS, class F = NoFill>
 __device__ __forceinline__ void rows_times_slice(const float* __restrict__ tile, int g, int c16,
-                                                 const float (&f)[DK / 4], floatx4 (&acc)[NS]) {
+                                                 const float (&f)[DK / 4], floatx4 (&acc)[NS], F&& fill = F{}) {
     constexpr int S = DK + 4, DQ = DK / 4;
     // the b128 row reads of step s4+1 are issued before step s4's MFMAs (LDS latency off the MFMA stream)
     float4 ab[2][NS];
@@ -185,6 +190,7 @@ __device__ __forceinline__ void rows_times_slice(const float* __restrict__ tile,
         for (int sub = 0; sub < NS; ++sub) acc[sub] = mfma16(a[sub].z, f[4 * s4 + 2], acc[sub]);
 #pragma unroll
         for (int sub = 0; sub < NS; ++sub) acc[sub] = mfma16(a[sub].w, f[4 * s4 + 3], acc[sub]);
+        fill(s4);
     }
 }
 
@@ -991,14 +997,61 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
             const int kstride = mask_key_stride(L);
             const int q_start = (causal && any_valid) ? kb : 0;  // earlier queries see none of these keys
             const int nsub = (Lp - q_start) / 16;
-            auto chunk = [&](auto ns_tag, int qb) {
+            // P and dS of 16-query sub-tile `sub` of the chunk at qb (this lane: queries qb + 16 sub + 4g .. +3,
+            // key kj) from its scores st / dP' dpt and key-major dropout word mw; dS is stored for the dQ pass
+            // (ph_tag: dropout decisions recomputed by Philox -- no stored mask -- a branch; the pipelined chunks read
+            // the stored mask through selects only)
+            const float keepk = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+            const uint32_t mw_or = (p_drop > 0.f && drop_mask) ? 0u : 0xFFFFFFFFu;  // no dropout: every key kept
+            auto soft_sub = [&](auto ph_tag, int qb, int sub, const floatx4& stv, const floatx4& dpv, uint32_t mwv_,
+                                float (&pd)[4], float (&ds)[4]) {
+                constexpr bool PH = decltype(ph_tag)::value;
+                const int q4 = qb + sub * 16 + 4 * g;  // this lane's 4 query rows q4 .. q4+3
+                const float4 mx4 = *reinterpret_cast<const float4*>(mx_s + q4);
+                const float4 il4 = *reinterpret_cast<const float4*>(il_s + q4);
+                const float4 ds4 = *reinterpret_cast<const float4*>(dsum_s + q4);
+                const uint32_t mw = mwv_ >> (4 * g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    // branch-free (selects): the pipelined loop keeps this work in the MFMA steps' scheduling regions
+                    // (padding query rows read zero statistics: finite values, then discarded)
+                    const int qq = q4 + r;
+                    const bool ok = qq < L && key_ok;
+                    const bool masked = key_masked_pad || (causal && kj > qq);
+                    // explicitly rounded operations: the Philox and the stored-mask forms of this code (different
+                    // surroundings) must not contract differently -- their results are compared bit for bit
+                    const float sv_ = masked ? kMaskedScore : __fmul_rn(stv[r], scale);
+                    const float pr = __fmul_rn(__expf(__fsub_rn(sv_, pick(mx4, r))), pick(il4, r));
+                    float f;
+                    if (PH) {
+                        f = 1.f;
+                        if (p_drop > 0.f) {
+                            f = drop_mask ? ((mw >> r) & 1u ? keepk : 0.f)
+                                          : pick(attn_keep4(seed, (uint64_t)bh * L + qq, kj & ~3, p_drop), kj & 3);
+                        }
+                    } else {
+                        f = ((mw | mw_or) >> r) & 1u ? keepk : 0.f;
+                    }
+                    pd[r] = ok ? __fmul_rn(pr, f) : 0.f;
+                    ds[r] = (ok && !masked) ? __fmul_rn(pr, __fmaf_rn(dpv[r], f, -pick(ds4, r))) : 0.f;
+                }
+                if (DS) {  // dS[query q4 + r][key kj]: 16 lanes of a group store 64 contiguous bytes per row
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) ds_head[(int64_t)(q4 + r) * Lp + kj] = ds[r];
+                }
+            };
+            // the chunk's key-major dropout words, requested before its MFMAs
+            auto load_mw = [&](auto ns_tag, int qb, uint32_t* mwv) {
                 constexpr int NS = decltype(ns_tag)::value;
-                floatx4 st[NS], dpt[NS];
-                // the chunk's key-major dropout words are requested before its MFMAs
-                uint32_t mwv[NS];
 #pragma unroll
                 for (int sub = 0; sub < NS; ++sub)
                     mwv[sub] = (p_drop > 0.f && drop_mask) ? keyw_key[((qb >> 4) + sub) * kstride] : 0u;
+            };
+            auto chunk = [&](auto ns_tag, int qb) {
+                constexpr int NS = decltype(ns_tag)::value;
+                floatx4 st[NS], dpt[NS];
+                uint32_t mwv[NS];
+                load_mw(ns_tag, qb, mwv);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int sub = 0; sub < NS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1006,42 +1059,70 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
                 rows_times_slice<DK, NS>(Ds + qb * S, g, c16, vf, dpt);
                 float pd[NS][4], ds[NS][4];
 #pragma unroll
-                for (int sub = 0; sub < NS; ++sub) {
-                    const int q4 = qb + sub * 16 + 4 * g;  // this lane's 4 query rows q4 .. q4+3
-                    const float4 mx4 = *reinterpret_cast<const float4*>(mx_s + q4);
-                    const float4 il4 = *reinterpret_cast<const float4*>(il_s + q4);
-                    const float4 ds4 = *reinterpret_cast<const float4*>(dsum_s + q4);
-                    const uint32_t mw = mwv[sub] >> (4 * g);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int qq = q4 + r;
-                        float pv = 0.f, dsv = 0.f;
-                        if (qq < L && key_ok) {
-                            const bool masked = key_masked_pad || (causal && kj > qq);
-                            const float sv_ = masked ? kMaskedScore : st[sub][r] * scale;
-                            const float pr = __expf(sv_ - pick(mx4, r)) * pick(il4, r);
-                            float f = 1.f;
-                            if (p_drop > 0.f) {
-                                f = drop_mask ? ((mw >> r) & 1u ? 1.f / (1.f - p_drop) : 0.f)
-                                              : pick(attn_keep4(seed, (uint64_t)bh * L + qq, kj & ~3, p_drop), kj & 3);
-                            }
-                            pv = pr * f;
-                            dsv = masked ? 0.f : pr * (dpt[sub][r] * f - pick(ds4, r));
-                        }
-                        pd[sub][r] = pv;
-                        ds[sub][r] = dsv;
-                    }
-                    if (DS) {  // dS[query q4 + r][key kj]: 16 lanes of a group store 64 contiguous bytes per row
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) ds_head[(int64_t)(q4 + r) * Lp + kj] = ds[sub][r];
-                    }
-                }
+                for (int sub = 0; sub < NS; ++sub)
+                    soft_sub(std::true_type{}, qb, sub, st[sub], dpt[sub], mwv[sub], pd[sub], ds[sub]);
                 cols_times_weights<DK, NS>(Ds + qb * S, g, c16, pd, dvt);  // dV^T += dO^T P
                 cols_times_weights<DK, NS>(Qs + qb * S, g, c16, ds, dkt);  // dK^T += Q^T dS
             };
-            int c0 = 0;
-            for (; c0 + kNS <= nsub; c0 += kNS) chunk(std::integral_constant<int, kNS>{}, q_start + c0 * 16);
-            for (; c0 < nsub; ++c0) chunk(std::integral_constant<int, 1>{}, q_start + c0 * 16);
+            // Full 64-query chunks as a two-stage pipeline within the wave: the score products of chunk c + 1 are
+            // issued with chunk c's softmax-gradient vector work spread between their steps (it issues in the
+            // MFMAs' shadow instead of between chunk c's two MFMA phases), then chunk c's dV / dK products.
+            // (dk = 128: the second chunk's scores do not fit the 256 registers of two waves per SIMD: unpipelined)
+            // (also unpipelined: dropout without the forward's stored decisions, Philox recomputed per element)
+            const bool pipe = DK <= 64 && !(p_drop > 0.f && !drop_mask);
+            const int nfull = pipe ? nsub / kNS : 0;
+            constexpr int T = 2 * (DQ / 4);  // score-product steps per chunk (Q, then dO)
+            if (!pipe) {
+                int c0 = 0;
+                for (; c0 + kNS <= nsub; c0 += kNS) chunk(std::integral_constant<int, kNS>{}, q_start + c0 * 16);
+                for (; c0 < nsub; ++c0) chunk(std::integral_constant<int, 1>{}, q_start + c0 * 16);
+            }
+            if (pipe && nfull > 0) {
+                floatx4 st[kNS], dpt[kNS];
+                uint32_t mwv[kNS];
+                load_mw(std::integral_constant<int, kNS>{}, q_start, mwv);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int sub = 0; sub < kNS; ++sub) st[sub] = dpt[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
+                rows_times_slice<DK, kNS>(Qs + q_start * S, g, c16, kf, st);
+                rows_times_slice<DK, kNS>(Ds + q_start * S, g, c16, vf, dpt);
+                for (int c = 0; c < nfull; ++c) {
+                    const int qb = q_start + c * kKT;
+                    float pd[kNS][4], ds[kNS][4];
+                    if (c + 1 < nfull) {
+                        floatx4 stn[kNS], dptn[kNS];
+                        uint32_t mwn[kNS];
+                        load_mw(std::integral_constant<int, kNS>{}, qb + kKT, mwn);
+#pragma unroll
+                        for (int sub = 0; sub < kNS; ++sub) stn[sub] = dptn[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
+                        auto fill = [&](int t) {
+#pragma unroll
+                            for (int sub = t * kNS / T; sub < (t + 1) * kNS / T; ++sub)
+                                soft_sub(std::false_type{}, qb, sub, st[sub], dpt[sub], mwv[sub], pd[sub], ds[sub]);
+                        };
+                        rows_times_slice<DK, kNS>(Qs + (qb + kKT) * S, g, c16, kf, stn, [&](int s4) { fill(s4); });
+                        rows_times_slice<DK, kNS>(Ds + (qb + kKT) * S, g, c16, vf, dptn,
+                                                  [&](int s4) { fill(DQ / 4 + s4); });
+                        __builtin_amdgcn_sched_barrier(0);
+                        cols_times_weights<DK, kNS>(Ds + qb * S, g, c16, pd, dvt);  // dV^T += dO^T P
+                        cols_times_weights<DK, kNS>(Qs + qb * S, g, c16, ds, dkt);  // dK^T += Q^T dS
+#pragma unroll
+                        for (int sub = 0; sub < kNS; ++sub) {
+                            st[sub] = stn[sub];
+                            dpt[sub] = dptn[sub];
+                            mwv[sub] = mwn[sub];
+                        }
+                    } else {
+#pragma unroll
+                        for (int sub = 0; sub < kNS; ++sub)
+                            soft_sub(std::false_type{}, qb, sub, st[sub], dpt[sub], mwv[sub], pd[sub], ds[sub]);
+                        cols_times_weights<DK, kNS>(Ds + qb * S, g, c16, pd, dvt);
+                        cols_times_weights<DK, kNS>(Qs + qb * S, g, c16, ds, dkt);
+                    }
+                }
+            }
+            if (pipe)
+                for (int c0 = nfull * kNS; c0 < nsub; ++c0) chunk(std::integral_constant<int, 1>{}, q_start + c0 * 16);
         }
         if (key_ok) {
             float* krow = dk + (tok0 + kj) * lddk + h * DK;

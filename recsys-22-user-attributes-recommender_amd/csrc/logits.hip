@@ -520,6 +520,407 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------ gradient passes
+// The gradient passes (dH, dW, fdh) as a two-stage software pipeline over the streamed tiles, three LDS buffers
+// (144 KiB + metadata; one workgroup of 4 waves per CU):
+//   iteration t:  DMA of tile t + 2 (issued first, waited for at the end of the iteration)
+//                 [A] score product of tile t + 1 (16 steps of 6 MFMAs, row reads one step ahead)
+//                     || P of tile t: exp, one-hot, the exact three-way bf16 split (a value pair per step)
+//                 [B] gradient product of tile t (16 steps of 6 MFMAs, transposed reads one step ahead)
+//                     || tile t + 1's scores prepared: + bias / - lse, one-hot bits, running max (a pair per step)
+// Each step is its own scheduling region (sched_barrier) in which a dependent chain of six MFMAs takes the step's
+// vector work and next step's reads into its shadow (at one wave per SIMD up to ~5 single-issue instructions per
+// 32x32x16 MFMA hide, MI355X_MICROARCH.md).  The engine above ran the softmax VALU between the products and read
+// its LDS operands just before use.
+// The tile DMA is issued by inline assembly: with the compiler's LDS-DMA builtin in flight, every
+// ds_read_b64_tr_b16 is preceded by s_waitcnt vmcnt(0) (the compiler cannot tell the buffers apart), which put the
+// next tile's fetch on the critical path once per tile.  Completion is explicit: s_waitcnt vmcnt(0) in every
+// issuing wave, then the workgroup barrier, before a buffer is read.  Products, sums and their order are those of
+// the engine: results are bit-identical to it.
+constexpr int kGradW = 4;
+constexpr size_t kSmemGrad = 3 * kTile + 3 * kTS * 8;
+
+// The tile's 12 wave-instructions of this wave in one asm block: wave-instruction i = plane / image-row group
+// w = wave + 4 i lands at LDS byte w * 1 KiB of the buffer (plane w / 16 at 16 KiB, rows 4 (w % 16) at 1 KiB), so
+// M0 starts at buf + 1 KiB * wave and steps by 4 KiB; it is saved and restored around the block.
+static_assert(kTile / 1024 / kGradW == 12 && kPlaneTile == 16 * 1024, "dma_tile_asm: 12 x 1 KiB per wave");
+__device__ __forceinline__ void dma_tile_asm(const __bf16* __restrict__ planes, int64_t pad, int64_t row0, char* buf) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)buf + 1024u * (uint32_t)wave;
+    const __bf16* src[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const int w = wave + kGradW * i;
+        const int p = w / (kTS / 4), R = 4 * (w % (kTS / 4));
+        const int row = R + (lane >> 4);
+        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));  // swz(): slot lane & 15 holds chunk ch
+        src[i] = planes + (int64_t)p * pad * kDP + (row0 + row) * kDP + ch * 8;
+    }
+    uint32_t saved;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %13\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %2, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %3, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %4, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %5, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %6, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %7, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %8, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %9, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %10, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %11, off\n\ts_add_u32 m0, m0, 4096\n\t"
+        "global_load_lds_dwordx4 %12, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "v"(src[0]), "v"(src[1]), "v"(src[2]), "v"(src[3]), "v"(src[4]), "v"(src[5]), "v"(src[6]), "v"(src[7]),
+          "v"(src[8]), "v"(src[9]), "v"(src[10]), "v"(src[11]), "s"(__builtin_amdgcn_readfirstlane(base))
+        : "memory", "scc");
+}
+
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+struct Bf3u {  // a Bf3 viewed as packed bf16 pairs
+    u32x4v h, m, l;
+};
+// the exact three-way split (split_bf3) of one value pair into bf16 pair k of each plane
+__device__ __forceinline__ void split_pair(float a, float b, Bf3u& P, int k) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 h = {(__bf16)a, (__bf16)b};
+    const float ra = a - (float)h[0], rb = b - (float)h[1];
+    const bf16x2 m = {(__bf16)ra, (__bf16)rb};
+    const bf16x2 l = {(__bf16)(ra - (float)m[0]), (__bf16)(rb - (float)m[1])};
+    P.h[k] = __builtin_bit_cast(uint32_t, h);
+    P.m[k] = __builtin_bit_cast(uint32_t, m);
+    P.l[k] = __builtin_bit_cast(uint32_t, l);
+}
+__device__ __forceinline__ Bf3 as_bf3(const Bf3u& u) {
+    Bf3 b;
+    b.h = __builtin_bit_cast(bf16x8, u.h);
+    b.m = __builtin_bit_cast(bf16x8, u.m);
+    b.l = __builtin_bit_cast(bf16x8, u.l);
+    return b;
+}
+
+#ifndef ASME_LOGITS_SCHED
+#define ASME_LOGITS_SCHED 0  // per-step sched_group_barrier pattern (MFMA, read, vector work)
+#endif
+// the step boundary: the next step's operand reads (issued above it) are not sunk below it (a compiler-level
+// memory fence), and this step's MFMAs do not rise above it (their operand passes through the fence)
+__device__ __forceinline__ void step_fence(Bf3& A) {
+    asm volatile("" ::: "memory");
+    asm volatile("" : "+v"(A.h), "+v"(A.m), "+v"(A.l));
+}
+// one MFMA, then up to R LDS reads and V vector instructions, six times: the step's schedule
+template <int R, int V>
+__device__ __forceinline__ void step_pattern() {
+#if ASME_LOGITS_SCHED
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (R > 0) __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+    }
+#endif
+}
+
+template <int MODE, int KB>
+__global__ __launch_bounds__(kGradW * 64) void logits_grad_kernel(LogitsArgs a) {
+    constexpr int W = kGradW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* bufs = smem;                                                  // 3 x kTile
+    float* mf = reinterpret_cast<float*>(smem + 3 * kTile);            // 3 x kTS
+    int* mt = reinterpret_cast<int*>(smem + 3 * kTile + 3 * kTS * 4);  // 3 x kTS
+    constexpr int KS = 2 * KB;   // 16-k steps of the score product (per 32-row sub-tile)
+    constexpr int NFT = KB;      // 32-feature tiles of the gradient product
+    constexpr int NA = 2 * KS;   // stage-A steps (sub-tile, k step)
+    constexpr int NB = 4 * NFT;  // stage-B steps (sub-tile, 16-row half, feature tile)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r32 = lane & 31;
+    const int chunk_id = (int)(blockIdx.x % (unsigned)a.nchunks);
+    const int64_t sblock = blockIdx.x / (unsigned)a.nchunks;
+    const int64_t srow = sblock * (32 * W) + wave * 32 + r32;  // this lane's stationary row (MFMA column)
+    const int64_t s_begin = (int64_t)chunk_id * a.chunk;
+    const int64_t s_end = std::min(a.strm_pad, s_begin + a.chunk);  // tiles past n_strm read zero planes
+    const int ntiles = (int)((s_end - s_begin) / kTS);
+
+    // stationary fragments, loaded straight into AGPRs (the MFMAs read their B operand there): the 256
+    // architectural VGPRs are left to the scores, P, the prefetched operands and the addresses
+    Bf3 st[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const __bf16* o = a.stat + srow * kDP + 16 * ks + 8 * h;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(st[ks].h) : "v"(o) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(st[ks].m) : "v"(o + a.stat_pad * kDP) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(st[ks].l) : "v"(o + 2 * a.stat_pad * kDP) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float s_lse = 0.f, s_bias = 0.f;
+    int s_tgt = -1;
+    if (MODE == M_DH || MODE == M_FDH) {
+        const int64_t tg = srow < a.n_stat ? a.targets[srow] : -1;
+        const bool ok = srow < a.n_stat && valid_target(tg, a.ignore, a.V);
+        s_tgt = ok ? (int)tg : -1;
+        if (MODE == M_DH) s_lse = ok ? a.lse[srow] : INFINITY;  // ignored / padding queries: P = 0
+    } else {
+        s_bias = srow < a.n_stat ? (a.bias ? a.bias[srow] : 0.f) : -INFINITY;
+        s_tgt = (int)srow;  // compare the streamed query's target against this item
+    }
+    float run_max = -INFINITY, run_sum = 0.f, t_logit = 0.f, base = 0.f;
+    bool have_t = false;
+    floatx16 y[NFT];
+#pragma unroll
+    for (int f = 0; f < NFT; ++f)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) y[f][i] = 0.f;
+    float db = 0.f;
+
+    auto score_a = [&](const char* buf, int sub, int ks) {
+        const int off = swz(32 * sub + r32, 2 * ks + h);
+        Bf3 A;
+        A.h = lds_b128(buf, off);
+        A.m = lds_b128(buf + kPlaneTile, off);
+        A.l = lds_b128(buf + 2 * kPlaneTile, off);
+        return A;
+    };
+    auto grad_a = [&](const char* buf, int sub, int s2, int ft) {
+        const int fh = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+        const int rlo = 32 * sub + 16 * s2 + 4 * h + q, rhi = rlo + 8;
+        const int ch = 4 * ft + 2 * fh + (p4 >> 1);
+        const int olo = swz(rlo, ch) + 8 * (p4 & 1), ohi = swz(rhi, ch) + 8 * (p4 & 1);
+        Bf3 A;
+        A.h = cat8(lds_tr(buf, olo), lds_tr(buf, ohi));
+        A.m = cat8(lds_tr(buf + kPlaneTile, olo), lds_tr(buf + kPlaneTile, ohi));
+        A.l = cat8(lds_tr(buf + 2 * kPlaneTile, olo), lds_tr(buf + 2 * kPlaneTile, ohi));
+        return A;
+    };
+
+    TileMeta tm;
+    auto stage = [&](int slot, int64_t r0) {  // tile at streamed row r0 into buffer slot: metadata load + DMA
+        if (threadIdx.x < kTS) tm.load(MODE, a, r0 + threadIdx.x);
+        dma_tile_asm(a.strm, a.strm_pad, r0, bufs + slot * kTile);
+    };
+    auto stage_meta = [&](int slot) {
+        if (threadIdx.x < kTS) {
+            mf[slot * kTS + threadIdx.x] = tm.f;
+            mt[slot * kTS + threadIdx.x] = tm.t;
+        }
+    };
+
+    // scores of the current tile (xs) and of the next (xn); value v = 16 sub + i is streamed row
+    // 32 sub + acc_row(i, h); oh / ohn: the one-hot bits (dH, dW)
+    floatx16 xs[2], xn[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) xs[0][i] = xs[1][i] = xn[0][i] = xn[1][i] = 0.f;
+    uint32_t oh = 0u, ohn = 0u;
+    float tmax = -INFINITY;
+    // prepare value pair p (values 2p, 2p + 1) of the scores x of the tile at streamed row r0 from the pair's
+    // metadata (read one step ahead of its use: a read just before its use would wait for the step's prefetched
+    // transposed reads too)
+    struct PairMeta {
+        float2 f;
+        int2 t;
+    };
+    auto load_meta = [&](int slot, int p) {
+        const int lr = 32 * (p >> 3) + acc_row(2 * (p & 7), h);  // rows lr, lr + 1
+        PairMeta m;
+        m.f = *reinterpret_cast<const float2*>(mf + slot * kTS + lr);
+        if (MODE == M_DW) m.t = *reinterpret_cast<const int2*>(mt + slot * kTS + lr);
+        return m;
+    };
+    auto prep_pair = [&](floatx16 (&x)[2], uint32_t& bits, const PairMeta& m, int64_t r0, int p) {
+        const int sub = p >> 3, i0 = 2 * (p & 7);
+        const int lr = 32 * sub + acc_row(i0, h);
+        if constexpr (MODE == M_FDH) {
+            x[sub][i0] += m.f.x;
+            x[sub][i0 + 1] += m.f.y;
+            tmax = fmaxf(tmax, fmaxf(x[sub][i0], x[sub][i0 + 1]));
+        } else if constexpr (MODE == M_DH) {
+            x[sub][i0] = x[sub][i0] + m.f.x - s_lse;
+            x[sub][i0 + 1] = x[sub][i0 + 1] + m.f.y - s_lse;
+            bits |= ((int64_t)s_tgt == r0 + lr ? 1u : 0u) << (2 * p);
+            bits |= ((int64_t)s_tgt == r0 + lr + 1 ? 1u : 0u) << (2 * p + 1);
+        } else {
+            x[sub][i0] = x[sub][i0] + s_bias - m.f.x;
+            x[sub][i0 + 1] = x[sub][i0 + 1] + s_bias - m.f.y;
+            bits |= (m.t.x == s_tgt ? 1u : 0u) << (2 * p);
+            bits |= (m.t.y == s_tgt ? 1u : 0u) << (2 * p + 1);
+        }
+    };
+    // fdh, after a tile's scores are prepared: the target logit, the running max (lazy rescale: the reference max
+    // moves only when a tile's max passes it by more than 8, so P = exp(s - ref) <= e^8), the exp base
+    auto fdh_post = [&](const floatx16 (&x)[2], int64_t r0) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            const int rel = s_tgt - (int)(r0 + 32 * sub);  // target in this sub-tile and lane half?
+            if ((unsigned)rel < 32u && ((rel >> 2) & 1) == h) {
+                const int ri = (rel & 3) + 4 * (rel >> 3);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (i == ri) t_logit = x[sub][i];
+                have_t = true;
+            }
+        }
+        const float tm2 = fmaxf(tmax, __shfl_xor(tmax, 32, 64));  // one running max per query over both halves
+        tmax = -INFINITY;
+        if (__ballot(!(tm2 <= run_max + 8.f)) != 0ull) {
+            const float nm = fmaxf(run_max, tm2);
+            const float alpha = run_max == -INFINITY ? 0.f : __expf(run_max - nm);
+#pragma unroll
+            for (int f = 0; f < NFT; ++f)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) y[f][i] *= alpha;
+            run_sum *= alpha;
+            run_max = nm;
+        }
+        base = run_max == -INFINITY ? 0.f : run_max;  // nothing finite yet: P = 0, no NaN
+    };
+    // P value pair p of the current tile into the split B fragments
+    Bf3u P[2][2];
+    auto p_pair = [&](int p) {
+        const int sub = p >> 3, i0 = 2 * (p & 7), s2 = i0 >> 3, k = (i0 & 7) >> 1;
+        float v0 = xs[sub][i0], v1 = xs[sub][i0 + 1];
+        if constexpr (MODE == M_FDH) {
+            v0 = __expf(v0 - base);
+            v1 = __expf(v1 - base);
+            run_sum += v0;
+            run_sum += v1;
+        } else {
+            v0 = __expf(v0) - (float)((oh >> (2 * p)) & 1u);
+            v1 = __expf(v1) - (float)((oh >> (2 * p + 1)) & 1u);
+            if (MODE == M_DW) {
+                db += v0;
+                db += v1;
+            }
+        }
+        split_pair(v0, v1, P[sub][s2], k);
+    };
+
+    if (ntiles > 0) {
+        stage(0, s_begin);
+        stage_meta(0);
+        if (ntiles > 1) {
+            stage(1, s_begin + kTS);
+            stage_meta(1);
+        }
+        wait_dma();
+        __syncthreads();
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) xs[sub] = mfma32_bf3(score_a(bufs, sub, ks), st[ks], xs[sub]);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) prep_pair(xs, oh, load_meta(0, p), s_begin, p);
+        if constexpr (MODE == M_FDH) fdh_post(xs, s_begin);
+    }
+    int cur = 0;
+    for (int it = 0; it < ntiles; ++it) {
+        const int nxt = cur == 2 ? 0 : cur + 1, nn = nxt == 2 ? 0 : nxt + 1;
+        const bool has_next = it + 1 < ntiles, has_nn = it + 2 < ntiles;
+        const int64_t r0 = s_begin + (int64_t)it * kTS;
+        if (has_nn) stage(nn, r0 + 2 * kTS);
+        const char* buf = bufs + cur * kTile;
+        __builtin_amdgcn_sched_barrier(0);
+        // stage A
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xn[0][i] = xn[1][i] = 0.f;
+        ohn = 0u;
+        if (has_next) {
+            const char* nbuf = bufs + nxt * kTile;
+            Bf3 A = score_a(nbuf, 0, 0);
+#pragma unroll
+            for (int s = 0; s < NA; ++s) {
+                const int sub = s / KS, ks = s % KS;
+                Bf3 An = A;
+                if (s + 1 < NA) An = score_a(nbuf, (s + 1) / KS, (s + 1) % KS);
+                step_fence(A);
+                xn[sub] = mfma32_bf3(A, st[ks], xn[sub]);
+#pragma unroll
+                for (int p = s * 16 / NA; p < (s + 1) * 16 / NA; ++p) p_pair(p);
+                step_pattern<1, 4>();
+                A = An;
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < 16; ++p) p_pair(p);
+        }
+        // stage B
+        {
+            Bf3 A = grad_a(buf, 0, 0, 0);
+            const int64_t r1 = r0 + kTS;
+            constexpr int MP = (16 + NB - 1) / NB;  // most pairs per step
+            PairMeta cm[MP], nm[MP];
+#pragma unroll
+            for (int p = 0; p < 16 / NB; ++p) cm[p] = load_meta(nxt, p);
+#pragma unroll
+            for (int s = 0; s < NB; ++s) {
+                const int sub = s / (2 * NFT), s2 = (s / NFT) % 2, ft = s % NFT;
+                const int plo = s * 16 / NB, phi = (s + 1) * 16 / NB, nhi = (s + 2) * 16 / NB;
+#pragma unroll
+                for (int p = phi; p < nhi && s + 1 < NB; ++p) nm[p - phi] = load_meta(nxt, p);
+                Bf3 An = A;
+                if (s + 1 < NB) An = grad_a(buf, (s + 1) / (2 * NFT), ((s + 1) / NFT) % 2, (s + 1) % NFT);
+                step_fence(A);
+                y[ft] = mfma32_bf3(A, as_bf3(P[sub][s2]), y[ft]);
+                // (on the last tile this prepares stale values that are never used: no branch in the chain)
+#pragma unroll
+                for (int p = plo; p < phi; ++p) prep_pair(xn, ohn, cm[p - plo], r1, p);
+#pragma unroll
+                for (int p = 0; p < MP; ++p) cm[p] = nm[p];
+                step_pattern<1, 3>();
+                A = An;
+            }
+        }
+        if constexpr (MODE == M_FDH) {
+            if (has_next) fdh_post(xn, r0 + kTS);
+        }
+        xs[0] = xn[0];
+        xs[1] = xn[1];
+        oh = ohn;
+        if (has_nn) stage_meta(nn);
+        wait_dma();
+        __syncthreads();
+        cur = nxt;
+    }
+
+    if (MODE == M_FDH) {
+        run_sum += __shfl_xor(run_sum, 32, 64);  // (the halves share the running max)
+        if (srow < a.n_stat) {
+            if (h == 0) {
+                a.part[((int64_t)chunk_id * a.n_stat + srow) * 2] = run_max;
+                a.part[((int64_t)chunk_id * a.n_stat + srow) * 2 + 1] = run_sum;
+            }
+            if (have_t) a.part2[srow] = t_logit;
+            float* dst = a.upart + ((int64_t)chunk_id * a.n_stat + srow) * a.d;
+#pragma unroll
+            for (int ft = 0; ft < NFT; ++ft)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int f = 32 * ft + 8 * u + 4 * h;
+                    if (f < a.d)
+                        *reinterpret_cast<float4*>(dst + f) =
+                            make_float4(y[ft][4 * u], y[ft][4 * u + 1], y[ft][4 * u + 2], y[ft][4 * u + 3]);
+                }
+        }
+        return;
+    }
+    const float scale = a.dloss[0] / a.stats[1];
+    if (srow < a.n_stat) {
+        float* dst = a.part + ((a.nchunks > 1 ? (int64_t)chunk_id * a.n_stat : 0) + srow) * a.d;
+#pragma unroll
+        for (int ft = 0; ft < NFT; ++ft)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int f = 32 * ft + 8 * u + 4 * h;
+                if (f < a.d)
+                    *reinterpret_cast<float4*>(dst + f) =
+                        make_float4(y[ft][4 * u] * scale, y[ft][4 * u + 1] * scale, y[ft][4 * u + 2] * scale,
+                                    y[ft][4 * u + 3] * scale);
+            }
+    }
+    if (MODE == M_DW && a.part2) {
+        db += __shfl_xor(db, 32, 64);
+        if (h == 0 && srow < a.n_stat) a.part2[(a.nchunks > 1 ? (int64_t)chunk_id * a.n_stat : 0) + srow] = db * scale;
+    }
+}
+
 // one block: lse[q] = merge of the chunks; out[0] = mean over valid rows of lse - s_t (NaN if none), out[1] = count
 // The forward's finish, in two launches (one 1,024-thread block had merged every row's chunk partials alone:
 // 0.19 ms per C3 step for 37k rows x 53 chunks): lce_rows_kernel merges each row's partials into its lse and sums
@@ -745,8 +1146,23 @@ int split(const float* X, int64_t ld, int64_t rows, int d, __bf16* planes, hipSt
     return hip_status(hipGetLastError(), "logits: split");
 }
 
+#ifndef ASME_LOGITS_XTILE
+#define ASME_LOGITS_XTILE 1  // gradient passes on logits_grad_kernel (0: the single-stage engine, for A/B)
+#endif
+template <int MODE>
+constexpr bool kGradKernel = ASME_LOGITS_XTILE && ASME_LOGITS_DIAG == 0 && (MODE == M_DH || MODE == M_DW || MODE == M_FDH);
+
 template <int MODE, int KB>
 int launch_engine(const LogitsArgs& a, int64_t sblocks, hipStream_t s) {
+    if constexpr (kGradKernel<MODE>) {
+        static const hipError_t attr = hipFuncSetAttribute((const void*)logits_grad_kernel<MODE, KB>,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemGrad);
+        if (attr != hipSuccess) return hip_status(attr, "logits: LDS opt-in");
+        static_assert(EngineWaves<MODE>::W == kGradW, "the plan's stationary blocks are kGradW waves");
+        hipLaunchKernelGGL((logits_grad_kernel<MODE, KB>), dim3((unsigned)(sblocks * a.nchunks)), dim3(kGradW * 64),
+                           kSmemGrad, s, a);
+        return hip_status(hipGetLastError(), "logits: gradient pass");
+    }
     // LDS opt-in once per instantiation (a function-local static: thread-safe initialisation)
     static const hipError_t attr = hipFuncSetAttribute(
         (const void*)logits_engine_kernel<MODE, KB, EngineWaves<MODE>::W>, hipFuncAttributeMaxDynamicSharedMemorySize,
