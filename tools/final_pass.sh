@@ -8,7 +8,7 @@ tail -1 $OUT/bench.json | python -c "import json,sys; r=json.loads(sys.stdin.rea
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "ws_gemm|weight_grad|attn|sum_slabs" \
     -d $OUT/mfma -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --cpu-baseline 0 --legs none \
     --kernel-events off > $OUT/mfma.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "logits_engine|fdh_finish|scale_rows|lce_" \
+timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "logits_engine|logits_grad|fdh_finish|scale_rows|lce_" \
     -d $OUT/mfma_b4r -o run --output-format csv -- python bench.py --workload bert4rec --items 27000 --steps 2 --warmup 1 \
     --cpu-baseline 0 --legs none --kernel-events off > $OUT/mfma_b4r.log 2>&1 || exit $?
 python tools/pmc_mfma.py $(find $OUT/mfma -name "*counter_collection.csv") $OUT/mfma_busy.json 1024 200 10000000 128 2

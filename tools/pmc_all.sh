@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 TAG=${TAG:-r3}
 export TMPDIR=/tmp
-RX='asme|attn|emb_|lazy|adam|residual|gelu|ln_|weight_grad|sum_slabs|ws_gemm|sampled|posneg|claim|dedup|csr_|chained|grad_chunk|grad_span|logits_engine|lce_|fdh|scale_rows|split_planes|sum_parts|bce|cloze|reduce_rows|pos_partial'
+RX='asme|attn|emb_|lazy|adam|residual|gelu|ln_|weight_grad|sum_slabs|ws_gemm|sampled|posneg|claim|dedup|csr_|chained|grad_chunk|grad_span|logits_engine|logits_grad|lce_|fdh|scale_rows|split_planes|sum_parts|bce|cloze|reduce_rows|pos_partial'
 for W in ${WORKLOADS:-sasrec-neg bert4rec kebert4rec}; do
   case $W in
     sasrec-neg) ARGS="--workload sasrec-neg";;

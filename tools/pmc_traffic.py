@@ -56,11 +56,12 @@ MAP = [
     # the fused logits + CE head (csrc/logits.hip): the engine's mode names the call; the operand splits that open
     # a call are attributed to the call of the engine launch that follows them (see per_call)
     # (api None: the kernel belongs to the logits call that launched the previous mapped kernel)
+    # (the gradient passes run on logits_grad16_kernel / logits_grad_kernel: same mode numbers)
     (r"logits_engine_kernel<0", "asme_linear_xent_fwd", True),
-    (r"logits_engine_kernel<4", "asme_linear_xent_fwd_dh", True),
-    (r"logits_engine_kernel<1", "asme_linear_xent_bwd", True),
+    (r"logits_(engine|grad16|grad)_kernel<4", "asme_linear_xent_fwd_dh", True),
+    (r"logits_(engine|grad16|grad)_kernel<1", "asme_linear_xent_bwd", True),
     (r"scale_rows_kernel", "asme_linear_xent_bwd_dw", True),
-    (r"logits_engine_kernel<2", None, False),
+    (r"logits_(engine|grad16|grad)_kernel<2", None, False),
     (r"(lce_rows|lce_finish|fdh_finish|sum_parts)_kernel", None, False),
 ]
 PENDING = r"split_planes_kernel"  # belongs to the next mapped logits kernel's call
