@@ -578,11 +578,10 @@ inline int64_t huge_blocks(int64_t n) { return (n + kHugeOcc - 1) / kHugeOcc; }
 __device__ __forceinline__ void csr_huge_count(const int64_t* __restrict__ inverse, int64_t n, int64_t cap,
                                                const int32_t* __restrict__ hidx, const int32_t* __restrict__ huge,
                                                const int32_t* __restrict__ hbeg, int32_t* __restrict__ cntm,
-                                               int64_t nblk_h, int32_t* __restrict__ ticket, int blk) {
+                                               int64_t nblk_h, int blk) {
     const int nh = min(*huge, kHugeFast);
     if (nh == 0) return;
     __shared__ int32_t c[kHugeFast];
-    __shared__ int last;
     if (threadIdx.x < kHugeFast) c[threadIdx.x] = 0;
     __syncthreads();
     const int64_t b0 = (int64_t)blk * kHugeOcc;
@@ -592,30 +591,31 @@ __device__ __forceinline__ void csr_huge_count(const int64_t* __restrict__ inver
         if (j >= 0 && j < kHugeFast) atomicAdd(&c[j], 1);  // (counts only: order does not matter here)
     }
     __syncthreads();
-    if ((int)threadIdx.x < nh) publish_i32(cntm + (int64_t)threadIdx.x * nblk_h + blk, c[threadIdx.x]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // (7) by the last block to finish (a ticket, no waiting): per huge key, base[j][b] = hbeg[j] + its counts over
-    // blocks < b, in place -- one wave per key, 64 blocks per wave-scan step
-    __syncthreads();
-    if (threadIdx.x == 0) last = last_arrival(ticket, nblk_h);
-    __syncthreads();
-    if (!last) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int j = wave; j < nh; j += 4) {
-        int32_t* row = cntm + (int64_t)j * nblk_h;
-        int32_t carry = hbeg[j];
-        for (int64_t c0 = 0; c0 < nblk_h; c0 += 64) {
-            const int64_t b = c0 + lane;
-            const int32_t v = b < nblk_h ? coherent_i32(row + b) : 0;
-            int32_t x = v;
+    if ((int)threadIdx.x < nh) cntm[(int64_t)threadIdx.x * nblk_h + blk] = c[threadIdx.x];
+}
+
+// (7) per huge key j (one wave each, its own launch): base[j][b] = hbeg[j] + its counts over the blocks < b, in place.
+// (This scan had run in the last block of (6) to finish, one wave per key over every key: ~160 keys of a Zipf(1.07)
+// batch at |I| = 10M, each a chain of dependent device-coherent loads; the occurrence CSR of the Zipf bench leg
+// 0.45 -> 0.39 ms per call with this launch, same box.)
+__global__ __launch_bounds__(64) void csr_huge_scan_kernel(const int32_t* __restrict__ huge,
+                                                           const int32_t* __restrict__ hbeg, int32_t* __restrict__ cntm,
+                                                           int64_t nblk_h) {
+    const int j = blockIdx.x, lane = threadIdx.x;
+    if (j >= min(*huge, kHugeFast)) return;
+    int32_t* row = cntm + (int64_t)j * nblk_h;
+    int32_t carry = hbeg[j];
+    for (int64_t c0 = 0; c0 < nblk_h; c0 += 64) {
+        const int64_t b = c0 + lane;
+        const int32_t v = b < nblk_h ? row[b] : 0;
+        int32_t x = v;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            if (b < nblk_h) row[b] = carry + x - v;
-            carry += __shfl(x, 63, 64);
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
+        if (b < nblk_h) row[b] = carry + x - v;
+        carry += __shfl(x, 63, 64);
     }
 }
 
@@ -628,12 +628,11 @@ __global__ __launch_bounds__(256) void csr_long_huge_kernel(const int64_t* __res
                                                             const int32_t* __restrict__ hidx,
                                                             const int32_t* __restrict__ huge,
                                                             const int32_t* __restrict__ hbeg,
-                                                            int32_t* __restrict__ cntm, int64_t nblk_h,
-                                                            int32_t* __restrict__ ticket) {
+                                                            int32_t* __restrict__ cntm, int64_t nblk_h) {
     if (blockIdx.x < kLongBlocks)
         csr_long(seg_off, n, cap, longs, order, tmp, blockIdx.x, kLongBlocks);
     else
-        csr_huge_count(inverse, n, cap, hidx, huge, hbeg, cntm, nblk_h, ticket, blockIdx.x - kLongBlocks);
+        csr_huge_count(inverse, n, cap, hidx, huge, hbeg, cntm, nblk_h, blockIdx.x - kLongBlocks);
 }
 
 __global__ __launch_bounds__(256) void csr_huge_place_kernel(const int64_t* __restrict__ inverse, int64_t n,
@@ -976,7 +975,6 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     int32_t* huge = (int32_t*)(ws + csr_up((size_t)(n + 1) * 4));
     int32_t* hbeg = huge + 1;
     int32_t* hend = hbeg + nh;
-    int32_t* ticket = hend + nh;  // (zeroed with the counts)
     unsigned long long* scan_state = (unsigned long long*)((char*)huge + csr_up((size_t)(2 + 2 * nh) * 4));
     int32_t* longs = (int32_t*)((char*)scan_state + csr_up((size_t)(1 + scan_tiles(cap + 1)) * 8));
     int32_t* tmp = (int32_t*)((char*)longs + csr_up((size_t)(n + 2) * 4));
@@ -997,10 +995,12 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     // long ranges ranked and (a huge range is possible) huge keys counted in one launch, then the stable placement
     const int64_t hblocks = n > kLongSeg ? nblk_h : 0;
     hipLaunchKernelGGL(csr_long_huge_kernel, dim3((unsigned)(kLongBlocks + hblocks)), dim3(256), 0, s, inverse, seg_off,
-                       n, cap, longs, order, tmp, hidx, huge, hbeg, cntm, nblk_h, ticket);
-    if (n > kLongSeg)
+                       n, cap, longs, order, tmp, hidx, huge, hbeg, cntm, nblk_h);
+    if (n > kLongSeg) {
+        hipLaunchKernelGGL(csr_huge_scan_kernel, dim3(kHugeFast), dim3(64), 0, s, huge, hbeg, cntm, nblk_h);
         hipLaunchKernelGGL(csr_huge_place_kernel, dim3((unsigned)nblk_h), dim3(256), 0, s, inverse, n, cap, hidx, huge,
                            cntm, nblk_h, order);
+    }
     ASME_LAUNCH_CHECK("asme_occurrence_csr");
 }
 
