@@ -21,7 +21,16 @@ namespace {
 // atomic on ONE address -- 0.34 ms per kernel for the 37k MASK occurrences of a KeBERT4Rec batch, against ~10 us
 // for uniform ids.  Each 256-thread block first combines its occurrences per key in an LDS hash table (512 slots,
 // linear probing, at most 256 keys: every insert terminates) and then issues one global atomic per distinct key.
-constexpr int kHashSlots = 512;
+// kOcc occurrences per thread (4: 1,024 per block, 2,048 slots): a key on every block -- the head of a Zipf(1.07)
+// id distribution at |I| = 10M, ~160 keys on > 256 occurrences of a 614k-occurrence batch -- costs a quarter of
+// the same-address atomics (they serialise at the L2: the claim took 0.17-0.24 ms per call on Zipf ids).
+#ifndef ASME_HASH_OCC
+#define ASME_HASH_OCC 4
+#endif
+constexpr int kOcc = ASME_HASH_OCC;
+constexpr int kHashSlots = 512 * kOcc;
+constexpr int kHashBits = kOcc == 1 ? 9 : kOcc == 2 ? 10 : kOcc == 4 ? 11 : 12;
+static_assert((1 << kHashBits) == kHashSlots, "hash slots: a power of two");
 struct BlockHash {
     int32_t key[kHashSlots];
     int32_t val[kHashSlots];
@@ -35,7 +44,7 @@ __device__ __forceinline__ void hash_init(BlockHash& t, int32_t v0) {
     __syncthreads();
 }
 __device__ __forceinline__ int hash_insert(BlockHash& t, int32_t key) {  // key >= 0
-    uint32_t h = ((uint32_t)key * 2654435761u) >> 23;  // 9 bits
+    uint32_t h = ((uint32_t)key * 2654435761u) >> (32 - kHashBits);
     for (;;) {
         const int32_t prev = atomicCAS(&t.key[h], -1, key);
         if (prev == -1 || prev == key) return (int)h;
@@ -83,9 +92,12 @@ __global__ __launch_bounds__(256) void claim_kernel(IdSegs S, int64_t n, int64_t
                                                     int32_t* __restrict__ ticket) {
     __shared__ BlockHash t;
     hash_init(t, INT32_MAX);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t id = i < n ? seg_id(S, i) : -1;
-    if (id >= 0 && id < V) atomicMin(&t.val[hash_insert(t, (int32_t)id)], (int32_t)i);
+#pragma unroll
+    for (int q = 0; q < kOcc; ++q) {
+        const int64_t i = ((int64_t)blockIdx.x * kOcc + q) * blockDim.x + threadIdx.x;
+        const int64_t id = i < n ? seg_id(S, i) : -1;
+        if (id >= 0 && id < V) atomicMin(&t.val[hash_insert(t, (int32_t)id)], (int32_t)i);
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0;
     __syncthreads();
     for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x)
@@ -196,6 +208,7 @@ __global__ void owner_hist_kernel(const int64_t* __restrict__ ids, const int32_t
 }
 
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+inline unsigned nblk_occ(int64_t n) { return (unsigned)((n + 256 * kOcc - 1) / (256 * kOcc)); }  // hashed kernels
 
 // ---- stable bucketing of the requester's unique ids by owner (counting sort over W <= 64 buckets):
 // block b of kBk ids -> bcount[w * nb + b]; one block scans (w-major) into offsets; the scatter pass ranks
@@ -347,7 +360,7 @@ ASME_API int asme_dedup_ids_segments(int nseg, const int64_t* const* seg_ids, co
     int32_t* lpre = (int32_t*)ws;
     int32_t* bcnt = (int32_t*)(ws + ws_up((size_t)n * 4));
     int32_t* ticket = bcnt + nb;
-    hipLaunchKernelGGL(claim_kernel, dim3(nblk(n)), dim3(256), 0, s, S, n, vocab, map, ticket);
+    hipLaunchKernelGGL(claim_kernel, dim3(nblk_occ(n)), dim3(256), 0, s, S, n, vocab, map, ticket);
     hipLaunchKernelGGL(dedup_rank_kernel, dim3((unsigned)nb), dim3(256), 0, s, S, n, vocab, map, lpre, bcnt, ticket,
                        count);
     hipLaunchKernelGGL(dedup_slot_kernel, dim3(nblk(n)), dim3(256), 0, s, S, n, vocab, map, lpre, bcnt, unique,
@@ -460,8 +473,11 @@ __global__ __launch_bounds__(256) void csr_count_kernel(const int64_t* __restric
                                                         int32_t* __restrict__ cnt) {
     __shared__ BlockHash t;
     hash_init(t, 0);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&t.val[hash_insert(t, occ_key(inverse, i, cap))], 1);
+#pragma unroll
+    for (int q = 0; q < kOcc; ++q) {
+        const int64_t i = ((int64_t)blockIdx.x * kOcc + q) * blockDim.x + threadIdx.x;
+        if (i < n) atomicAdd(&t.val[hash_insert(t, occ_key(inverse, i, cap))], 1);
+    }
     __syncthreads();
     for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x)
         if (t.key[j] >= 0) atomicAdd(cnt + t.key[j], t.val[j]);
@@ -475,22 +491,31 @@ __global__ __launch_bounds__(256) void csr_scatter_kernel(const int64_t* __restr
                                                           int32_t* __restrict__ sorted_slot) {
     __shared__ BlockHash t;
     hash_init(t, 0);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int32_t k = 0;
-    int h = 0, r = 0;
-    if (i < n) {
-        k = occ_key(inverse, i, cap);
-        h = hash_insert(t, k);
-        r = atomicAdd(&t.val[h], 1);
+    int32_t k[kOcc];
+    int h[kOcc], r[kOcc];
+#pragma unroll
+    for (int q = 0; q < kOcc; ++q) {
+        const int64_t i = ((int64_t)blockIdx.x * kOcc + q) * blockDim.x + threadIdx.x;
+        k[q] = 0;
+        h[q] = r[q] = 0;
+        if (i < n) {
+            k[q] = occ_key(inverse, i, cap);
+            h[q] = hash_insert(t, k[q]);
+            r[q] = atomicAdd(&t.val[h[q]], 1);
+        }
     }
     __syncthreads();
     for (int j = threadIdx.x; j < kHashSlots; j += blockDim.x)
         if (t.key[j] >= 0) t.aux[j] = atomicSub(cnt + t.key[j], t.val[j]) - t.val[j];
     __syncthreads();
-    if (i >= n) return;
-    const int32_t pos = seg_off[k] + t.aux[h] + r;
-    order[pos] = (int32_t)i;
-    sorted_slot[pos] = k;
+#pragma unroll
+    for (int q = 0; q < kOcc; ++q) {
+        const int64_t i = ((int64_t)blockIdx.x * kOcc + q) * blockDim.x + threadIdx.x;
+        if (i >= n) break;
+        const int32_t pos = seg_off[k[q]] + t.aux[h[q]] + r[q];
+        order[pos] = (int32_t)i;
+        sorted_slot[pos] = k[q];
+    }
 }
 
 // one thread per key: ranges of 2..kShortSeg sorted in registers (an odd-even transposition network over a padded
@@ -985,10 +1010,10 @@ ASME_API int asme_occurrence_csr(const int64_t* inverse, int64_t n, int64_t cap,
     // together (contiguous)
     if (hipMemsetAsync(cnt, 0, (char*)longs - ws + 4, s) != hipSuccess)
         return hip_status(hipGetLastError(), "asme_occurrence_csr: zero");
-    hipLaunchKernelGGL(csr_count_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, cnt);
+    hipLaunchKernelGGL(csr_count_kernel, dim3(nblk_occ(n)), dim3(256), 0, s, inverse, n, cap, cnt);
     hipLaunchKernelGGL(chained_scan_kernel, dim3((unsigned)scan_tiles(cap + 1)), dim3(256), 0, s, cnt, cap + 1, seg_off,
                        scan_state);
-    hipLaunchKernelGGL(csr_scatter_kernel, dim3(nblk(n)), dim3(256), 0, s, inverse, n, cap, seg_off, cnt, order,
+    hipLaunchKernelGGL(csr_scatter_kernel, dim3(nblk_occ(n)), dim3(256), 0, s, inverse, n, cap, seg_off, cnt, order,
                        sorted_slot);
     hipLaunchKernelGGL(csr_order_kernel, dim3(nblk(cap + 1)), dim3(256), 0, s, seg_off, n, cap, order, longs, huge,
                        hbeg, hend, hidx);
