@@ -11,6 +11,7 @@
 // Layout: table (V, D) fp32 row-major; tokens t = b*L + s; activations (T, D) fp32.
 // One 64-lane wave owns one token row; lane l holds elements l + 64*j (coalesced 256-B segments).
 #include "rows.h"
+#include <type_traits>
 #include <algorithm>
 
 using namespace asme;
@@ -330,7 +331,10 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 // LN3: `dout` is the gradient of the embedding output through the residual stream, l3.dln that of the fused
 // LayerNorm's output; the output row is recomputed (LN1 / dropout / LN2 affine / dropout, from the stored statistics
 // and keep bits) for the LN3 backward, whose parameter gradients are accumulators 4 and 5 of the partials.
-template <class R, int kPass, bool LN3>  // kPass: tokens per lane group per grid-stride pass
+// LN2: the second LayerNorm (pre-fusion attributes) is present -- a template flag, so without it (SASRec, BERT4Rec)
+// its accumulators and normalised row cost no registers: 200 -> 155 VGPRs at D = 128 with LN3, a third wave per SIMD
+// (in-step 0.150-0.154 -> 0.139-0.140 ms per call, same box; forcing a fourth wave spills: 0.315 ms)
+template <class R, int kPass, bool LN3, bool LN2>  // kPass: tokens per lane group per grid-stride pass
 __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1,
@@ -405,7 +409,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                 for (int j = 0; j < R::NV; ++j)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
-            if (w2) {
+            if (LN2) {
                 if (extra && live) {
                     row_load<R>(extra + t * D, sub, D, q[k]);
 #pragma unroll
@@ -418,7 +422,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
             if constexpr (LN3) {
                 // the embedding output drop2(LN2(z)) (or drop2(z) without LN2), then g += LN3 backward of dln
                 RowVals<R> xo, xh3, gl;
-                if (w2) {
+                if (LN2) {
                     row_affine<R>(xh2, sub, D, w2, l3.b2, xo);
                 } else {
                     const bool ex = extra && live;
@@ -453,7 +457,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
 #pragma unroll
                     for (int i = 0; i < 4; ++i) g[k][j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
             RowVals<R> gz;
-            if (w2) {
+            if (LN2) {
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
 #pragma unroll
@@ -798,16 +802,20 @@ int embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const f
             if constexpr (R::W == 4) {
                 constexpr int kPass = 1;  // 2 tokens per pass: 160 VGPRs, 3 waves/SIMD, slower (169 vs 121 us)
                 const int64_t nb4 = partials ? n_partials : (n_tokens + rows - 1) / rows;
-                if (l3)
-                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass, true>), dim3((unsigned)nb4), dim3(256),
-                                       lds, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim,
-                                       pos_table, ln1_w, ln1_b, p1, extra, ln2_w, p2, emb_seed(seed1, seed2), keep_mask,
-                                       dout, stats, d_rows, d_extra, partials, *l3);
-                else
-                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass, false>), dim3((unsigned)nb4),
+                auto launch = [&](auto ln3_tag, auto ln2_tag) {
+                    constexpr bool LN3 = decltype(ln3_tag)::value, LN2 = decltype(ln2_tag)::value;
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass, LN3, LN2>), dim3((unsigned)nb4),
                                        dim3(256), lds, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab,
                                        (int)dim, pos_table, ln1_w, ln1_b, p1, extra, ln2_w, p2, emb_seed(seed1, seed2),
-                                       keep_mask, dout, stats, d_rows, d_extra, partials, EmbLn3{});
+                                       keep_mask, dout, stats, d_rows, d_extra, partials, l3 ? *l3 : EmbLn3{});
+                };
+                if (l3) {
+                    if (ln2_w) launch(std::true_type{}, std::true_type{});
+                    else launch(std::true_type{}, std::false_type{});
+                } else {
+                    if (ln2_w) launch(std::false_type{}, std::true_type{});
+                    else launch(std::false_type{}, std::false_type{});
+                }
             } else {
                 hipLaunchKernelGGL(emb_bwd_kernel<R>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, ids,
                                    n_tokens, seq_len, table, vocab, (int)dim, pos_table, ln1_w, ln1_b, p1, seed1,
