@@ -209,7 +209,7 @@ struct EmbLn3 {
     const float* b2;   // backward: LN2's bias (the embedding output is recomputed through LN2's affine)
 };
 
-template <class R, int kEmbK, bool LN3>  // kEmbK: tokens per lane group
+template <class R, int kEmbK, bool LN3, bool LN2 = true>  // kEmbK: tokens per lane group; LN2: as the backward's
 __global__ __launch_bounds__(256) void emb_fwd4_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float eps1, float p1,
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
         row_load<R>(w1, sub, D, w1v);
         row_load<R>(b1, sub, D, b1v);
     }
-    if (w2) {
+    if (LN2 && w2) {
         row_load<R>(w2, sub, D, w2v);
         row_load<R>(b2, sub, D, b2v);
     }
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
             for (int j = 0; j < R::NV; ++j)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
-        if (w2) {
+        if (LN2 && w2) {
             row_ln_stats<R>(x[k], sub, D, eps2, m2, r2);
             row_normalise<R>(x[k], sub, D, m2, r2, tmp);
 #pragma unroll
@@ -733,16 +733,20 @@ int embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const f
                 constexpr int K = ASME_EMB_K;  // tokens per lane group
                 const int64_t rows = (int64_t)kWavesPerBlock * R::RPW * K;
                 const dim3 grid((unsigned)((n_tokens + rows - 1) / rows));
-                if (l3)
-                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K, true>), grid, dim3(256), 0,
+                auto launch = [&](auto ln3_tag, auto ln2_tag) {
+                    constexpr bool LN3 = decltype(ln3_tag)::value, LN2 = decltype(ln2_tag)::value;
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K, LN3, LN2>), grid, dim3(256), 0,
                                        (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table,
                                        ln1_w, ln1_b, ln1_eps, p1, extra, ln2_w, ln2_b, ln2_eps, p2,
-                                       emb_seed(seed1, seed2), out, stats, keep_mask, err_flag, *l3);
-                else
-                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_fwd4_kernel<R, K, false>), grid, dim3(256), 0,
-                                       (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab, (int)dim, pos_table,
-                                       ln1_w, ln1_b, ln1_eps, p1, extra, ln2_w, ln2_b, ln2_eps, p2,
-                                       emb_seed(seed1, seed2), out, stats, keep_mask, err_flag, EmbLn3{});
+                                       emb_seed(seed1, seed2), out, stats, keep_mask, err_flag, l3 ? *l3 : EmbLn3{});
+                };
+                if (l3) {
+                    if (ln2_w) launch(std::true_type{}, std::true_type{});
+                    else launch(std::true_type{}, std::false_type{});
+                } else {
+                    if (ln2_w) launch(std::false_type{}, std::true_type{});
+                    else launch(std::false_type{}, std::false_type{});
+                }
             } else {
                 const int64_t rows = (int64_t)kWavesPerBlock * R::RPW;
                 hipLaunchKernelGGL(emb_fwd_kernel<R>, dim3((unsigned)((n_tokens + rows - 1) / rows)), dim3(256), 0,

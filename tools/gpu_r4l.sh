@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -q -p no:cacheprovider --timeout 200 --timeout-method thread tests/test_gpu_embedding_ln.py tests/test_gpu_kernels.py -k "emb or Emb or gather" > gpurun_out/r4l_t.log 2>&1
 rc=$?; tail -2 gpurun_out/r4l_t.log; [ $rc -eq 0 ] || exit $rc
 NEW=recsys-22-user-attributes-recommender_amd/libasme_mi.so
-for i in 1 2; do for lib in $NEW tools/variants/libasme_mi_embold.so tools/variants/libasme_mi_embwpe4.so; do
+for i in 1 2 3; do for lib in $NEW tools/variants/libasme_mi_embc.so; do
   ASME_MI_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --legs none > gpurun_out/lab.json 2> gpurun_out/lab.err || exit 1
   python - "$lib" <<'PY'
 import json, sys
