@@ -445,6 +445,64 @@ def test_occurrence_csr_equals_stable_sort(asme, dev, n, cap):
     assert torch.equal(off.cpu()[:U + 1], want_off[:U + 1])
 
 
+def _zipf_ids(n, V, seed, a=1.07):
+    """n ids in [0, V) with Zipf(a) over rank (id 0 the most popular): the bench's Zipf leg (bench.session_ids)"""
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand(n, generator=g, dtype=torch.float64)
+    hmax = (V ** (1 - a) - 1) / (1 - a)
+    r = ((u * hmax) * (1 - a) + 1) ** (1 / (1 - a))
+    return (r.long() - 1).clamp(0, V - 1)
+
+
+def test_dedup_and_csr_zipf_head(asme, dev):
+    """The Zipf(1.07) secondary's id distribution at |I| = 10M (~160 keys on > 256 occurrences, a hot head on every
+    1,024-occurrence hash block): asme_dedup_ids_segments == numpy first-occurrence unique / inverse, and
+    asme_occurrence_csr over that inverse == a stable sort by slot, exactly."""
+    L = asme._lib
+    V, sizes = 10_000_000, (204800, 204800, 204800)
+    segs = [_zipf_ids(k, V, 71 + i) for i, k in enumerate(sizes)]
+    flat = torch.cat(segs).numpy()
+    _, first = np.unique(flat, return_index=True)
+    uniq_ref = flat[np.sort(first)]
+    slot_of = np.full(V, -1, dtype=np.int64)
+    slot_of[uniq_ref] = np.arange(uniq_ref.size)
+    inv_ref = slot_of[flat]
+    n = flat.size
+    dsegs = [x.to(dev) for x in segs]
+    m = torch.full((V,), -1, dtype=torch.int32, device=dev)
+    ws_bytes = int(L.load().asme_dedup_workspace_bytes(n))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    uniq = torch.empty(n, dtype=torch.int64, device=dev)
+    inv = torch.empty(n, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    k = len(dsegs)
+    L.call("asme_dedup_ids_segments", k, (ctypes.c_void_p * k)(*[x.data_ptr() for x in dsegs]),
+           (ctypes.c_int64 * k)(*[x.numel() for x in dsegs]), V, L.ptr(m), L.ptr(ws), ws_bytes, L.ptr(uniq),
+           L.ptr(inv), L.ptr(cnt), L.stream())
+    c = int(cnt.item())
+    assert c == uniq_ref.size
+    assert np.array_equal(uniq[:c].cpu().numpy(), uniq_ref)
+    assert np.array_equal(inv.cpu().numpy(), inv_ref)
+    # the occurrence CSR of that inverse (every occurrence has a slot)
+    key = torch.from_numpy(inv_ref)
+    assert int((torch.bincount(key) > 256).sum()) > 100  # the huge-range path is exercised
+    want_order = torch.sort(key, stable=True).indices.to(torch.int32)
+    want_slot = key[want_order.long()].to(torch.int32)
+    counts = torch.bincount(key, minlength=c + 1)
+    want_off = (torch.cumsum(counts, 0) - counts).to(torch.int32)
+    nb = int(L.load().asme_occurrence_csr_workspace(n))
+    ws2 = torch.empty(nb, dtype=torch.uint8, device=dev)
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    slot = torch.empty(n, dtype=torch.int32, device=dev)
+    off = torch.empty(c + 1, dtype=torch.int32, device=dev)
+    L.call("asme_occurrence_csr", L.ptr(inv), n, c, L.ptr(ws2), nb, L.ptr(order), L.ptr(slot), L.ptr(off), L.stream())
+    assert torch.equal(order.cpu(), want_order)
+    assert torch.equal(slot.cpu(), want_slot)
+    assert torch.equal(off.cpu(), want_off)
+    L.call("asme_dedup_reset", L.ptr(uniq), L.ptr(cnt), n, L.ptr(m), L.stream())
+    assert int((m != -1).sum()) == 0
+
+
 @pytest.mark.parametrize("V,D", [(2000, 64), (2003, 128), (1601, 256)])
 def test_lazy_adam_bit_exact_vs_dense(asme, dev, V, D):
     """Exact catch-up: lazily replayed zero-gradient steps == the dense row update every step, bitwise.  D = 128 / 256
