@@ -245,7 +245,9 @@ int asme_adam_rows_step(float* param, float* exp_avg, float* exp_avg_sq, int64_t
 
 /* Lazy dense Adam ("exact catch-up"): bit-identical to asme_adam_rows_step every step, but a row with a
  * zero gradient is only rewritten when it is next read.  last_step (rows int32) = step each row is up to
- * date with; hist (hist_rows, 8) float = per-step constants written by asme_lazy_adam_record_step; every
+ * date with; hist (hist_rows, 8) float = per-step constants written by asme_lazy_adam_record_step (allocate it
+ * zero-filled and write it only through that call: row 0 is no step, it holds the first step of the current run of
+ * identical beta1 / beta2 / eps / weight_decay, which lets the replay keep those in registers); every
  * step named (step / upto) must be < hist_rows, else the call fails with ASME_ERR_ARG. */
 int asme_lazy_adam_record_step(float* hist, int64_t hist_rows, int64_t step, float lr, float beta1, float beta2,
                                float eps, float weight_decay, void* stream);

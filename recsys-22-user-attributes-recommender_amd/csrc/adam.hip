@@ -191,8 +191,74 @@ namespace {
 
 static_assert(sizeof(AdamHyper) == 8 * sizeof(float), "hist row = 8 floats");
 
+// hist row 0 is never a step (steps start at 1); its first word holds, as an int32, the first step of the current
+// run of steps with identical (b1, b2, 1-b1, 1-b2, eps, wd): hist[t] for t in [const_from, latest recorded step] differ
+// at most in neg_step_size / inv_bc2_sqrt.  A replay that starts at or after it reads those two per step and keeps
+// the rest in registers (replay_const).  Each step is compared with the row recorded before it (bitwise); a step whose
+// predecessor was never recorded (step 1, a resumed run) opens a new run -- rows never replay a step at or before
+// the step the lazy state was started at, so the chain only has to hold over steps recorded in order.
+__device__ __forceinline__ bool same_consts(const AdamHyper& a, const AdamHyper& b) {
+    return __float_as_uint(a.b1) == __float_as_uint(b.b1) && __float_as_uint(a.b2) == __float_as_uint(b.b2) &&
+           __float_as_uint(a.one_minus_b1) == __float_as_uint(b.one_minus_b1) &&
+           __float_as_uint(a.one_minus_b2) == __float_as_uint(b.one_minus_b2) &&
+           __float_as_uint(a.eps) == __float_as_uint(b.eps) && __float_as_uint(a.wd) == __float_as_uint(b.wd);
+}
 __global__ void record_step_kernel(float* __restrict__ hist, int64_t step, AdamHyper hp) {
-    if (threadIdx.x == 0) reinterpret_cast<AdamHyper*>(hist)[step] = hp;
+    if (threadIdx.x == 0) {
+        AdamHyper* h = reinterpret_cast<AdamHyper*>(hist);
+        int32_t* const_from = reinterpret_cast<int32_t*>(hist);
+        const bool same = step > 1 && same_consts(h[step - 1], hp);
+        const int32_t cf = *const_from;
+        *const_from = same ? min(cf, (int32_t)step) : (int32_t)step;
+        h[step] = hp;
+    }
+}
+
+// The zero-gradient replay of steps t0+1..upto on a wave's element pairs.  When the whole range lies in the current
+// run of constant (b1, b2, eps, wd) (hist row 0, above), only the two step-dependent constants are read per step, the
+// next step's pair one iteration ahead (scalar loads off the recurrence), and the weight-decay branch is taken once;
+// otherwise every step's full constants are read as before.  Same adam_elem2 / adam_decay2 operations: same bits.
+#ifndef ASME_REPLAY_CONST
+#define ASME_REPLAY_CONST 1
+#endif
+template <int NP>
+__device__ __forceinline__ void replay_steps(float2v (&P)[NP], float2v (&M)[NP], float2v (&Vv)[NP],
+                                             const AdamHyper* __restrict__ hist, int32_t t0, int32_t upto,
+                                             int32_t const_from) {
+    if (ASME_REPLAY_CONST && t0 + 1 >= const_from) {
+        if (t0 >= upto) return;
+        AdamHyper hp = hist[upto];
+        const float2* __restrict__ lr = reinterpret_cast<const float2*>(hist) + 3;  // (neg_step_size, inv_bc2_sqrt)
+        float2 nx = lr[4 * (t0 + 1)];
+        if (hp.wd != 0.f) {
+            for (int32_t t = t0 + 1; t <= upto; ++t) {
+                hp.neg_step_size = nx.x;
+                hp.inv_bc2_sqrt = nx.y;
+                nx = lr[4 * min(t + 1, upto)];
+#pragma unroll
+                for (int j = 0; j < NP; ++j) adam_elem2(P[j], float2v{0.f, 0.f}, M[j], Vv[j], hp);
+            }
+        } else {
+            for (int32_t t = t0 + 1; t <= upto; ++t) {
+                hp.neg_step_size = nx.x;
+                hp.inv_bc2_sqrt = nx.y;
+                nx = lr[4 * min(t + 1, upto)];
+#pragma unroll
+                for (int j = 0; j < NP; ++j) adam_decay2(P[j], M[j], Vv[j], hp);
+            }
+        }
+        return;
+    }
+    for (int32_t t = t0 + 1; t <= upto; ++t) {
+        const AdamHyper hp = hist[t];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            if (hp.wd != 0.f)
+                adam_elem2(P[j], float2v{0.f, 0.f}, M[j], Vv[j], hp);
+            else
+                adam_decay2(P[j], M[j], Vv[j], hp);
+        }
+    }
 }
 
 template <int VPL>
@@ -408,6 +474,7 @@ __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restric
     const uint64_t live = __ballot(lane < nr && (STAGE || my_t < upto));
     if (live == 0) return;  // wave-uniform
     const int nl = __popcll(live);
+    const int32_t const_from = *reinterpret_cast<const int32_t*>(hist);
     int ln[RPW];  // lane (slot - base) of the i-th live slot; past the last one: the last one again (never stored)
     {
         uint64_t mm = live;
@@ -447,16 +514,7 @@ __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restric
         const int sl = i % PF;
         const int32_t t0 = __builtin_amdgcn_readlane(my_t, ln[i]);
         if (i < nl) {
-            for (int32_t t = t0 + 1; t <= upto; ++t) {
-                const AdamHyper hp = hist[t];
-#pragma unroll
-                for (int j = 0; j < NP; ++j) {
-                    if (hp.wd != 0.f)
-                        adam_elem2(P[sl][j], float2v{0.f, 0.f}, M[sl][j], Vv[sl][j], hp);
-                    else
-                        adam_decay2(P[sl][j], M[sl][j], Vv[sl][j], hp);
-                }
-            }
+            replay_steps<NP>(P[sl], M[sl], Vv[sl], hist, t0, upto, const_from);
             const int64_t orow = STAGE ? base + ln[i] : row_of(i);
             float* op = STAGE ? sp : p;
             float* om = STAGE ? sm : m;

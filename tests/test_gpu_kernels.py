@@ -503,12 +503,15 @@ def test_dedup_and_csr_zipf_head(asme, dev):
     assert int((m != -1).sum()) == 0
 
 
-@pytest.mark.parametrize("V,D", [(2000, 64), (2003, 128), (1601, 256)])
-def test_lazy_adam_bit_exact_vs_dense(asme, dev, V, D):
+@pytest.mark.parametrize("V,D,sched", [(2000, 64, False), (2003, 128, False), (1601, 256, False), (2003, 128, True),
+                                        (1601, 256, True)])
+def test_lazy_adam_bit_exact_vs_dense(asme, dev, V, D, sched):
     """Exact catch-up: lazily replayed zero-gradient steps == the dense row update every step, bitwise.  D = 128 / 256
-    stage and flush through the pipelined replay (lazy_pipe_kernel: 16 slots per wave, a ragged last wave here)."""
+    stage and flush through the pipelined replay (lazy_pipe_kernel: 16 slots per wave, a ragged last wave here).
+    sched: the learning rate changes every step and betas / weight decay change mid-run, so replays cross a change of
+    the constants (the per-step path) and start after one (the constants-in-registers path, adam.hip replay_steps)."""
     torch.manual_seed(6)
-    T, steps = 300, 7
+    T, steps = 300, 10 if sched else 7
     assert V // 5 >= T  # the narrow steps draw T distinct ids below V // 5
     base = torch.randn(V, D, device=dev)
     p_lazy = torch.nn.Parameter(base.clone())
@@ -521,6 +524,14 @@ def test_lazy_adam_bit_exact_vs_dense(asme, dev, V, D):
     map_e = torch.full((V,), -1, dtype=torch.int32, device=dev)
     gen = torch.Generator(device=dev).manual_seed(0)
     for step in range(steps):
+        if sched:
+            for opt in (o_lazy, o_eager):
+                g = opt.param_groups[0]
+                g["lr"] = 3e-3 * (1.0 + 0.1 * step)
+                if step == 3:
+                    g["betas"] = (0.9, 0.999)
+                if step == 6:
+                    g["weight_decay"] = 0.0
         hi = V if step % 2 == 0 else V // 5  # alternate wide / narrow id ranges: long and short gaps
         # distinct ids: the compact-row scatter uses fp32 atomics, whose order (not the Adam update) varies
         ids = torch.randperm(hi, device=dev, generator=gen)[:T]
