@@ -498,6 +498,10 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind):
 
     for i in range(args.warmup):
         run(i, i)
+    # the warm-up steps' own deferred zero-gradient table updates are applied before the timer starts, so the timed
+    # region holds exactly K steps of optimizer work: the steps' staged rows plus the end-of-run flush of every row's
+    # remaining timed steps (otherwise the timed region also replayed W steps of warm-up updates for every row)
+    opt.flush()
     torch.cuda.synchronize()
 
     # per-kernel device time of the dominant kernel (HIP events on the launching stream)
