@@ -209,6 +209,9 @@ struct EmbLn3 {
     const float* b2;   // backward: LN2's bias (the embedding output is recomputed through LN2's affine)
 };
 
+#ifndef ASME_EMB_FWD_HOIST
+#define ASME_EMB_FWD_HOIST 1
+#endif
 template <class R, int kEmbK, bool LN3, bool LN2 = true>  // kEmbK: tokens per lane group; LN2: as the backward's
 __global__ __launch_bounds__(256) void emb_fwd4_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
@@ -230,6 +233,23 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
         }
         id[k] = v;
     }
+#if ASME_EMB_FWD_HOIST
+    // LN3's w / b staged in LDS with the id loads in flight, instead of a global round trip (which also waits for the
+    // output row stores: vmcnt counts stores) between the first token's stores and its LN3 affine
+    __shared__ __attribute__((aligned(16))) float prm3[2][512];
+    if constexpr (LN3) {
+        for (int e = threadIdx.x; e < D; e += blockDim.x) {
+            prm3[0][e] = l3.w[e];
+            prm3[1][e] = l3.b[e];
+        }
+        __syncthreads();
+    }
+    const float* w3p = prm3[0];
+    const float* b3p = prm3[1];
+#else
+    const float* w3p = l3.w;
+    const float* b3p = l3.b;
+#endif
     RowVals<R> x[kEmbK], q[kEmbK];
 #pragma unroll
     for (int k = 0; k < kEmbK; ++k) row_load<R>(table + id[k] * D, sub, D, x[k]);
@@ -313,7 +333,7 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
             float m3, r3;
             row_ln_stats<R>(x[k], sub, D, l3.eps, m3, r3);
             row_normalise<R>(x[k], sub, D, m3, r3, tmp);
-            row_affine<R>(tmp, sub, D, l3.w, l3.b, x[k]);
+            row_affine<R>(tmp, sub, D, w3p, b3p, x[k]);
             row_store<R>(l3.out + t * D, sub, D, x[k]);
             if (sub == 0) *reinterpret_cast<float2*>(l3.stats + t * 2) = make_float2(m3, r3);
         }
@@ -322,6 +342,9 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 
 #ifndef ASME_EMB_BWD_WPE
 #define ASME_EMB_BWD_WPE 0
+#endif
+#ifndef ASME_EMB_BWD_HOIST
+#define ASME_EMB_BWD_HOIST 1
 #endif
 #if ASME_EMB_BWD_WPE
 #define ASME_EMB_BWD_ATTR __attribute__((amdgpu_waves_per_eu(ASME_EMB_BWD_WPE, 8)))
@@ -350,11 +373,33 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
     const bool drop = p1 > 0.f || p2 > 0.f;
     const uint32_t th1 = emb_thresh(p1), th2 = emb_thresh(p2);
     const float k1 = 1.f / (1.f - p1), k2 = 1.f / (1.f - p2);
+#if ASME_EMB_BWD_HOIST
+    // LN1's w / b and LN3's w staged once per workgroup: each pass reads them from LDS instead of three dependent
+    // global (cache-hit) round trips after its row loads
+    __shared__ __attribute__((aligned(16))) float prm[3][512];
+    for (int e = threadIdx.x; e < D; e += blockDim.x) {
+        if (w1) {
+            prm[0][e] = w1[e];
+            prm[1][e] = b1[e];
+        }
+        if constexpr (LN3) prm[2][e] = l3.w[e];
+    }
+    __syncthreads();
+    const float* w1p = prm[0];
+    const float* b1p = prm[1];
+    const float* w3p = prm[2];
+#else
+    const float* w1p = w1;
+    const float* b1p = b1;
+    const float* w3p = l3.w;
+#endif
+    const bool keep_in = keep && drop;
     for (int64_t tb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * R::RPW * kPass + lane / R::LPR;
          tb - lane / R::LPR < T; tb += (int64_t)gridDim.x * kWavesPerBlock * R::RPW * kPass) {
         int64_t id[kPass];
         float4 st[kPass];
         float2 st3[kPass];
+        uint32_t kb[kPass][R::NV];
         RowVals<R> x[kPass], g[kPass], q[kPass], dl[kPass];
 #pragma unroll
         for (int k = 0; k < kPass; ++k) {
@@ -373,6 +418,12 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
             if constexpr (LN3) {
                 row_load<R>(l3.dln + tt * D, sub, D, dl[k]);
                 st3[k] = *reinterpret_cast<const float2*>(l3.stats + tt * 2);
+            }
+            // the stored keep bits ride with the row loads (one round trip per pass, not one per byte)
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j) {
+                const int c = R::col(sub, j);
+                kb[k][j] = keep_in ? (uint32_t)keep[((uint64_t)tt * D + (c < D ? c : 0)) >> 2] : 0xFFu;
             }
         }
 #pragma unroll
@@ -395,14 +446,13 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                 const int c = R::col(sub, j);
                 bits[j] = 0xFFu;
                 if (drop && live && c < D)
-                    bits[j] = keep ? (uint32_t)keep[((uint64_t)t * D + c) >> 2]
-                                   : emb_keep_bits(seed, ((uint64_t)t * D + c) >> 2, th1, th2);
+                    bits[j] = keep ? kb[k][j] : emb_keep_bits(seed, ((uint64_t)t * D + c) >> 2, th1, th2);
             }
             // recompute z = drop1(LN1(x)) + extra
             RowVals<R> xh1, xh2;
             if (w1) {
                 row_normalise<R>(x[k], sub, D, st[k].x, st[k].y, xh1);
-                row_affine<R>(xh1, sub, D, w1, b1, x[k]);
+                row_affine<R>(xh1, sub, D, w1p, b1p, x[k]);
             }
             if (p1 > 0.f)
 #pragma unroll
@@ -445,7 +495,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                         acc[4][j][i] += dl[k][j][i] * xh3[j][i];
                         acc[5][j][i] += dl[k][j][i];
                     }
-                row_ln_bwd<R>(dl[k], xh3, l3.w, st3[k].y, sub, D, gl);
+                row_ln_bwd<R>(dl[k], xh3, w3p, st3[k].y, sub, D, gl);
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
 #pragma unroll
@@ -487,7 +537,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                         acc[1][j][i] += gz[j][i];
                     }
                 RowVals<R> gx;
-                row_ln_bwd<R>(gz, xh1, w1, st[k].y, sub, D, gx);
+                row_ln_bwd<R>(gz, xh1, w1p, st[k].y, sub, D, gx);
                 if (live) row_store<R>(d_rows + t * D, sub, D, gx);
             } else if (live) {
                 row_store<R>(d_rows + t * D, sub, D, gz);
