@@ -340,8 +340,10 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
     }
 }
 
+// three waves per SIMD: SASRec's variant (LN2 + LN3) needs 170 VGPRs with its LN parameters in LDS; held to 168 it
+// spills one 8-byte loop-invariant (12 B of scratch, one reload per pass) and runs 0.103-0.109 vs 0.110-0.118 ms
 #ifndef ASME_EMB_BWD_WPE
-#define ASME_EMB_BWD_WPE 0
+#define ASME_EMB_BWD_WPE 3
 #endif
 #ifndef ASME_EMB_BWD_HOIST
 #define ASME_EMB_BWD_HOIST 1
@@ -376,22 +378,30 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
 #if ASME_EMB_BWD_HOIST
     // LN1's w / b and LN3's w staged once per workgroup: each pass reads them from LDS instead of three dependent
     // global (cache-hit) round trips after its row loads
-    __shared__ __attribute__((aligned(16))) float prm[3][512];
+    __shared__ __attribute__((aligned(16))) float prm[5][512];
     for (int e = threadIdx.x; e < D; e += blockDim.x) {
         if (w1) {
             prm[0][e] = w1[e];
             prm[1][e] = b1[e];
         }
         if constexpr (LN3) prm[2][e] = l3.w[e];
+        if constexpr (LN2) {
+            prm[3][e] = w2[e];
+            if constexpr (LN3) prm[4][e] = l3.b2[e];
+        }
     }
     __syncthreads();
     const float* w1p = prm[0];
     const float* b1p = prm[1];
     const float* w3p = prm[2];
+    const float* w2p = prm[3];
+    const float* b2p = prm[4];
 #else
     const float* w1p = w1;
     const float* b1p = b1;
     const float* w3p = l3.w;
+    const float* w2p = w2;
+    const float* b2p = l3.b2;
 #endif
     const bool keep_in = keep && drop;
     for (int64_t tb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * R::RPW * kPass + lane / R::LPR;
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                 // the embedding output drop2(LN2(z)) (or drop2(z) without LN2), then g += LN3 backward of dln
                 RowVals<R> xo, xh3, gl;
                 if (LN2) {
-                    row_affine<R>(xh2, sub, D, w2, l3.b2, xo);
+                    row_affine<R>(xh2, sub, D, w2p, b2p, xo);
                 } else {
                     const bool ex = extra && live;
                     if (ex) row_load<R>(extra + t * D, sub, D, q[k]);
@@ -515,7 +525,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                         acc[2][j][i] += g[k][j][i] * xh2[j][i];
                         acc[3][j][i] += g[k][j][i];
                     }
-                row_ln_bwd<R>(g[k], xh2, w2, st[k].w, sub, D, gz);
+                row_ln_bwd<R>(g[k], xh2, w2p, st[k].w, sub, D, gz);
             } else {
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
