@@ -224,14 +224,9 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
     const int64_t t0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * R::RPW * kEmbK + lane / R::LPR;
     int64_t id[kEmbK];
 #pragma unroll
-    for (int k = 0; k < kEmbK; ++k) {
+    for (int k = 0; k < kEmbK; ++k) {  // every id requested before the first is checked (one wait, not kEmbK)
         const int64_t t = t0 + (int64_t)k * R::RPW;
-        int64_t v = t < T ? ids[t] : 0;
-        if (v < 0 || v >= V) {
-            if (sub == 0 && t < T && err) atomicOr(err, 1);
-            v = 0;
-        }
-        id[k] = v;
+        id[k] = t < T ? ids[t] : 0;
     }
 #if ASME_EMB_FWD_HOIST
     // LN3's w / b staged in LDS with the id loads in flight, instead of a global round trip (which also waits for the
@@ -250,6 +245,14 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
     const float* w3p = l3.w;
     const float* b3p = l3.b;
 #endif
+#pragma unroll
+    for (int k = 0; k < kEmbK; ++k) {
+        const int64_t t = t0 + (int64_t)k * R::RPW;
+        if (id[k] < 0 || id[k] >= V) {
+            if (sub == 0 && t < T && err) atomicOr(err, 1);
+            id[k] = 0;
+        }
+    }
     RowVals<R> x[kEmbK], q[kEmbK];
 #pragma unroll
     for (int k = 0; k < kEmbK; ++k) row_load<R>(table + id[k] * D, sub, D, x[k]);
