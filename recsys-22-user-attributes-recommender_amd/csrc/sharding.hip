@@ -892,14 +892,24 @@ __global__ __launch_bounds__(256) void grad_chunk_kernel(const int32_t* __restri
         for (int j0 = 0; j0 < cnt; j0 += 8) {
             int32_t sl[8];
             float4 v[8];
+            float sc[8];
+            bool ok[8];
+            // eight gathers before the dependent adds: unconditional global loads (an occurrence without a source row
+            // reads the chunk's own head row instead, discarded below), scaled only once all eight are in flight --
+            // a load inside the `ok` branch, scaled right after, was a flat load waited on before the next was issued
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {  // eight gathers before the dependent adds
+            for (int q = 0; q < 8; ++q) {
                 const int j = j0 + q;
                 sl[q] = j < cnt ? s_slot[g][j] : -1;
                 const float* src = j < cnt ? s_src[g][j] : nullptr;
-                v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (sl[q] >= 0 && src) v[q] = scale4(*reinterpret_cast<const float4*>(src + c0), s_sc[g][j]);
+                sc[q] = j < cnt ? s_sc[g][j] : 0.f;
+                ok[q] = sl[q] >= 0 && src;
+                const float* a = ok[q] ? src + c0 : head + c0;
+                const floatx4 x = *(const __attribute__((address_space(1))) floatx4*)a;
+                v[q] = make_float4(x[0], x[1], x[2], x[3]);
             }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = ok[q] ? scale4(v[q], sc[q]) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 if (sl[q] < 0) break;
