@@ -105,6 +105,76 @@ def roofline_entries(kstats, work, traffic, busy=None):
     return out
 
 
+# the north_star's named kernel targets (BASELINE.json): >= 70 % of the HBM roofline on the embedding gather,
+# >= 50 % MFMA on the logits GEMM -- surfaced by name in the compact line
+TARGET_KERNELS = ("asme_embedding_ln_fwd", "asme_embedding_ln_bwd", "asme_linear_xent_fwd_dh",
+                  "asme_linear_xent_bwd_dw", "asme_catalog_rank")
+ROOF_KEYS = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "avg_ms", "launches")
+
+
+def slim_roofline(r):
+    if not r:
+        return r
+    out = {k: r[k] for k in ROOF_KEYS if k in r}
+    for k in ("mfma_busy", "mfma_frac"):
+        if k in r:
+            out[k] = r[k]
+    return out
+
+
+def compact(result, top=3):
+    """The one stdout line: the contract keys, the dominant kernel's roofline, the CPU baseline, the top-`top`
+    rooflines and the named target kernels of every workload -- short enough that the driver's stdout tail holds
+    all of it (the full record goes to --full-json)."""
+    out = {k: v for k, v in result.items() if k not in ("rooflines", "workloads", "eval", "cpu_baseline")}
+    out["roofline"] = slim_roofline(result.get("roofline"))
+    rl = result.get("rooflines") or []
+    out["rooflines_top"] = [slim_roofline(r) for r in rl[:top]]
+    targets = {r["kernel"]: r["frac"] for r in rl if r["kernel"] in TARGET_KERNELS}
+    cb = result.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+        if "single_thread" in cb:
+            out["cpu_baseline"]["single_thread"] = cb["single_thread"]["value"]
+    else:
+        out["cpu_baseline"] = None
+    if result.get("eval"):
+        e = result["eval"]
+        out["eval"] = {k: e[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "ndcg@10") if k in e}
+        out["eval"]["roofline"] = slim_roofline(e.get("roofline"))
+        targets.update({r["kernel"]: r["frac"] for r in e.get("rooflines", []) if r["kernel"] in TARGET_KERNELS})
+    wl = {}
+    for name, w in (result.get("workloads") or {}).items():
+        c = {k: w[k] for k in ("value", "unit", "ms_per_step", "n_gpus") if k in w}
+        c["parallelism"] = w.get("config", {}).get("parallelism")
+        cbw = w.get("cpu_baseline")
+        c["cpu_baseline"] = ({k: cbw[k] for k in ("value", "cores", "kind", "batch", "s_per_step") if k in cbw}
+                             if cbw else None)
+        wrl = w.get("rooflines") or []
+        c["rooflines_top"] = [{k: r[k] for k in ("kernel", "bound", "frac", "achieved", "unit", "avg_ms") if k in r}
+                              for r in wrl[:top]]
+        tw = {r["kernel"]: r["frac"] for r in wrl if r["kernel"] in TARGET_KERNELS}
+        if tw:
+            c["target_kernels"] = tw
+        wl[name] = c
+    if wl:
+        out["workloads"] = wl
+    out["target_kernels"] = targets
+    return out
+
+
+def emit(result, args):
+    """rank 0: the full record to --full-json, the compact line to stdout"""
+    if args.full_json:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(args.full_json)), exist_ok=True)
+            with open(args.full_json, "w") as f:
+                json.dump(result, f, indent=1)
+        except OSError as e:
+            print(f"bench.py: could not write {args.full_json}: {e}", file=sys.stderr, flush=True)
+    print(json.dumps(compact(result)), flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,6 +204,12 @@ def parse():
                          "reported under \"workloads\" of the one JSON line (name:items, comma-separated; "
                          "C3 BERT4Rec |I| = 27,000, C5 KeBERT4Rec |I| = 13,000, sasrec_zipf: the headline step on "
                          "Zipf(1.07) ids at the headline's --items (SURVEY §8d secondary); 'none' to skip)")
+    ap.add_argument("--eval-steps", type=int, default=3,
+                    help="timed full-catalogue evaluation steps of the trained headline model (0: no eval leg)")
+    ap.add_argument("--eval-warmup", type=int, default=1)
+    ap.add_argument("--full-json", default=os.path.join("gpurun_out", "bench_full.json"),
+                    help="where rank 0 writes the full record (every roofline of every workload); stdout carries the "
+                         "compact line ('' to skip the file)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle leg (rank 0, N=1)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -427,7 +503,62 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
     return result
 
 
-def bench_sasrec(args, asme, dev, world, rank, ids_kind):
+def bench_eval(args, asme, dev, world, rank, module, get_batch, ids_kind):
+    """Full-catalogue evaluation of the trained SASRec at |I| = args.items: B sequences per GPU,
+    each scored against EVERY item of the catalogue (the reference's AllItemsSampler + argsort, sasrec/components.py:
+    46-61, metrics/common.py:4-27) and its target ranked without materialising the (B, |I|) scores -- one step =
+    the eval-mode transformer forward + asme_catalog_rank (at N > 1: every rank counts the items of its shard above
+    every rank's targets, asme_catalog_count_above, + one all_reduce of the int32 counts) + NDCG@10 / recall@10 from
+    the ranks.  Same contract as the training legs: warm-up, barrier + synchronize around exactly --eval-steps."""
+    B, L, d, V = args.batch, args.seq_len, args.dim, args.items + 3
+    module.eval()
+    ndcg = asme.metrics.NormalizedDiscountedCumulativeGainMetric(10)
+    recall = asme.metrics.RecallMetric(10)
+    batches = []
+    for j in range(2):
+        b = get_batch(10_000 + j)
+        batches.append({"item": b["item"], "item.target": b["positive_samples"][:, -1].contiguous()})
+
+    def step(i):
+        with torch.no_grad():
+            ranks = module.catalog_ranks(batches[i % 2])
+            ndcg.update_ranks(ranks)
+            recall.update_ranks(ranks)
+
+    for i in range(args.eval_warmup):
+        step(i)
+    ndcg.reset()
+    recall.reset()
+    timer = asme._lib.KernelTimer(["asme_catalog_rank", "asme_catalog_count_above", "asme_catalog_target_scores",
+                                   "asme_ws_linear", "asme_attention_fwd", "asme_embedding_ln_fwd"])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.eval_steps):
+        with timer if i >= args.eval_steps - instrumented_steps(args.eval_steps) else contextlib.nullcontext():
+            step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    module.train()
+    nq = B * world  # every rank scores all ranks' queries against its 1/W of the catalogue at N > 1
+    scan = 2.0 * nq * V * d / world
+    work = {"asme_catalog_rank": ("mfma", scan), "asme_catalog_count_above": ("mfma", scan),
+            "asme_catalog_target_scores": ("mfma", 2.0 * B * d), **gemm_work(B * L, d, 4 * d)}
+    rooflines = roofline_entries(timer.summary(), work, {})
+    return {"metric": f"evaluation sequences/sec (SASRec full-catalogue rank + NDCG@10, B={B} L={L} |I|={args.items})",
+            "value": round(B * world * args.eval_steps / elapsed, 2), "unit": "sequences/s",
+            "ms_per_step": round(1000 * elapsed / args.eval_steps, 3), "steps": args.eval_steps,
+            "warmup": args.eval_warmup, "ids": ids_kind,
+            "ndcg@10": round(float(ndcg.compute()), 6), "recall@10": round(float(recall.compute()), 6),
+            "roofline": rooflines[0] if rooflines else None, "rooflines": rooflines}
+
+
+def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
     """The SASRec-neg training step (BASELINE C2 / C4): B sequences per GPU, |I| = args.items, the GPU pos/neg
     producer inside the timed step; ids_kind "uniform" (the headline) or "zipf" (Zipf(1.07) over item rank, seed
     1234: SURVEY §8d's secondary, hot keys for the dedup / occurrence CSR / ordered reduce-apply).  Returns the result
@@ -554,6 +685,9 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind):
     value = B * world * args.steps / elapsed
 
     kstats = timer.summary()
+    asme.ops.SparseTablePlan.release = _orig_release
+    eval_leg = (bench_eval(args, asme, dev, world, rank, module, get_batch, ids_kind)
+                if args.eval_steps > 0 and with_eval else None)
     U = int(last_unique[0].item()) if last_unique else min(3 * B * L, V)
     # distinct rows the sampled head gathers (positive and negative ids of a step's batch): the head's compulsory
     # row bytes -- each further occurrence of a row is served from the L2 / MALL, not re-fetched from HBM
@@ -653,15 +787,98 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind):
         "host_issue_ms": round(1000 * sorted(host_s)[len(host_s) // 2], 3),
         "cpu_baseline": None,
     }
-    asme.ops.SparseTablePlan.release = _orig_release
+    if eval_leg is not None:
+        result["eval"] = eval_leg
     del model, module, opt, batches
     torch.cuda.empty_cache()
     return result
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def resolve_world(args, env=None):
+    """(world, must_launch): the rank count this invocation runs as.  `--gpus N` with no WORLD_SIZE in the
+    environment and N > 1 means "launch N ranks myself" (launch_ranks); under a launcher (torchrun sets WORLD_SIZE)
+    the launcher's world size must equal --gpus, so the printed n_gpus can never disagree with the flag."""
+    env = os.environ if env is None else env
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return args.gpus, args.gpus > 1
+    if int(ws) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {args.gpus}: they must agree")
+    return int(ws), False
+
+
+def rank_envs(n, port, base=None):
+    """the environment of each spawned rank (one process per GPU, torch.distributed's env:// rendezvous on
+    127.0.0.1; HSA_ENABLE_IPC_MODE_LEGACY and the rest of the parent's environment are inherited)"""
+    base = dict(os.environ if base is None else base)
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        out.append(e)
+    return out
+
+
+def launch_ranks(args, argv=None, script=None) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this same script (one per GPU) and
+    wait for them.  This parent never touches the GPU (torch.cuda.device_count() does not initialise HIP on this
+    image), so no process that owns a GPU context is forked or exec'ed.  If any rank fails the others are
+    terminated (exactly the PIDs started here) and its exit code is returned; rank 0 prints the one JSON line."""
+    import signal
+    import subprocess
+    n = args.gpus
+    if args.backend == "nccl":
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} GPUs, {have} visible (use --backend gloo to rehearse several "
+                  f"ranks on fewer GPUs)", file=sys.stderr, flush=True)
+            return 2
+    argv = sys.argv[1:] if argv is None else argv
+    script = os.path.abspath(__file__) if script is None else script
+    procs = [subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e)
+             for e in rank_envs(n, free_port())]
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc:
+        print(f"bench.py: a rank exited with status {rc}; the remaining ranks were stopped", file=sys.stderr,
+              flush=True)
+    return rc
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, must_launch = resolve_world(args)
+    if must_launch:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.backend == "gloo":
@@ -685,7 +902,7 @@ def main():
     if args.workload in ("bert4rec", "kebert4rec"):
         result = bench_bert4rec(args, asme, dev, world, rank, args.workload, args.items)
         if rank == 0:
-            print(json.dumps(result), flush=True)
+            emit(result, args)
         if dist.is_initialized():
             dist.destroy_process_group()
         return
@@ -700,14 +917,14 @@ def main():
             if leg == "sasrec_zipf":
                 if args.ids == "zipf":
                     continue  # the headline already is the Zipf run
-                result["workloads"][leg] = bench_sasrec(args, asme, dev, world, rank, "zipf")
+                result["workloads"][leg] = bench_sasrec(args, asme, dev, world, rank, "zipf", with_eval=False)
             else:
                 result["workloads"][leg] = bench_bert4rec(args, asme, dev, world, rank, leg, items)
             torch.cuda.empty_cache()
     if rank == 0 and world == 1 and args.cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, V)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args)
     if dist.is_initialized():
         dist.destroy_process_group()
 

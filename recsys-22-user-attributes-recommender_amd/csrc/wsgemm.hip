@@ -366,6 +366,12 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    // every feature block needs at least one workgroup of each XCD (the kernel's wg_per_nb = per_xcd / nblk): a
+    // shape with more blocks than an XCD has workgroups would leave Y unwritten, so it is refused here
+    if ((N + NB - 1) / NB > cus / 8) {
+        set_error("asme_ws_linear: more feature blocks than workgroups per XCD for this epilogue");
+        return -1;
+    }
     hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M, W,
                        N, Y, ep);
     return hip_status(hipGetLastError(), "asme_ws_linear");
@@ -421,6 +427,9 @@ int dispatch_k(int K, int ct, const float* X, int64_t M, const float* W, int N, 
 ASME_API int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N) {
     if (M <= 0 || (K != 128 && K != 256 && K != 384 && K != 512)) return 0;
     if (N > 4096 || pick_ct((int)N, (int)K) == 0) return 0;
+    // the activation-factor epilogue runs CT = 8 shapes on 64-feature blocks (dispatch_ct): those must fit an XCD's
+    // 32 workgroups too, so the shape is supported for every epilogue (K = 128, N = 4096)
+    if (pick_ct((int)N, (int)K) == 8 && !(N % 64 == 0 && 32 % (N / 64) == 0)) return 0;
     if (M * N * 4 >= (int64_t)kDrop || M * K * 4 >= ((int64_t)1 << 40)) return 0;
     return 1;
 }

@@ -204,8 +204,9 @@ class PreFusionContextSequenceElementsRepresentationComponent(nn.Module):
 # ------------------------------------------------------------------------------------ transformer
 class LayerNorm(nn.LayerNorm):
     """nn.LayerNorm (same parameters and state_dict keys) whose module call runs the LayerNorm kernel.  The
-    transformer blocks read the parameters directly into their fused kernels; a module call happens only where hooks
-    must see it (block 0's input norm with forward hooks registered, TransformerLayer.forward)."""
+    transformer blocks read the parameters directly into their fused kernels; any of their norms with forward hooks
+    or pre-hooks registered (or global module hooks) is called as a module instead, so the hooks run and may replace
+    its input or output (TransformerLayer.forward, _residual_norm)."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return ops.layer_norm(x, self)
@@ -300,11 +301,20 @@ class TransformerLayer(nn.Module):
             qkv = att.qkv(ln)
             o = ops.attention(qkv, key_valid, att.heads, causal, _p(att.dropout, tr))
             a = ops.linear(o, att.output_linear.weight, att.output_linear.bias)
-            h1, ln2 = ops.residual_ln(x, a, blk.output_sublayer.norm, _p(blk.input_sublayer.dropout, tr), 0.0)
+            h1, ln2 = _residual_norm(x, a, blk.output_sublayer.norm, _p(blk.input_sublayer.dropout, tr), 0.0)
             f2 = ops.ffn(ln2, ff.w_1.weight, ff.w_1.bias, ff.w_2.weight, ff.w_2.bias, _p(ff.dropout, tr))
             nxt = blocks[i + 1].input_sublayer.norm if i + 1 < len(blocks) else None
-            x, ln = ops.residual_ln(h1, f2, nxt, _p(blk.output_sublayer.dropout, tr), _p(blk.dropout, tr))
+            x, ln = _residual_norm(h1, f2, nxt, _p(blk.output_sublayer.dropout, tr), _p(blk.dropout, tr))
         return x
+
+
+def _residual_norm(res, y, norm, p_a: float, p_b: float):
+    """(s, norm(s)) with s = drop_b(res + drop_a(y)): the norm fused into the residual kernel, or -- when it has
+    forward hooks -- called as a module on s, so its hooks see the reference's call"""
+    if norm is not None and has_forward_hooks(norm):
+        s, _ = ops.residual_ln(res, y, None, p_a, p_b)
+        return s, norm(s)
+    return ops.residual_ln(res, y, norm, p_a, p_b)
 
 
 class TransformerSequenceRepresentationComponent(nn.Module):

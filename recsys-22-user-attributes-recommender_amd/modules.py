@@ -106,8 +106,6 @@ class _TableGradMixin:
         self.table_grad = mode
         self._slot_map = None
 
-    # the trainer's accumulate_grad_batches (trainer_builder.py:25): > 1 makes an unconsumed table gradient an error
-    accumulate_grad_batches: int = 1
 
     def _plan_table(self, id_sets):
         if self.table_grad != "sparse" or not self.training:
@@ -119,14 +117,16 @@ class _TableGradMixin:
             self._slot_map = torch.full((table.shape[0],), -1, dtype=torch.int32, device=table.device)
         tg = table._asme_table_grad
         if tg.plan is not None and not tg.plan.consumed:
-            if tg.plan.has_gradient() and (tg.plan.accumulate or self.accumulate_grad_batches > 1):
-                # gradient accumulation was asked for (a backward under GradientAllReduce.no_sync, or the trainer's
-                # accumulate_grad_batches > 1): the per-step row-sparse plan does not merge backward passes
-                raise RuntimeError("table_grad='sparse' takes one backward per optimizer step; use table_grad='dense' "
-                                   "for gradient accumulation")
-            # otherwise a step that never reached the optimizer (a skipped step): its table gradient is dropped, as
-            # zero_grad drops a dense one
-            tg.plan.release()
+            if tg.plan.has_gradient():
+                # a backward's table gradient that neither optimizer.step() applied nor optimizer.zero_grad() dropped
+                # (FusedAdam.zero_grad is the skip signal: GradScaler / a trainer skipping the step call it, gradient
+                # accumulation -- the trainer's accumulate_grad_batches, trainer_builder.py:25 -- does not): the
+                # per-step row-sparse plan cannot merge two backward passes, so this fails instead of dropping it
+                raise RuntimeError("table_grad='sparse' takes one backward per optimizer step (the previous "
+                                   "backward's item-table gradient was neither applied by optimizer.step() nor "
+                                   "dropped by optimizer.zero_grad()); use table_grad='dense' for gradient "
+                                   "accumulation")
+            tg.plan.release()  # a forward without a backward: nothing to lose
         tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map)
 
     @staticmethod

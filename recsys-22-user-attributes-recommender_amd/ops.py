@@ -10,7 +10,6 @@ kernels derive the mask from (seed, element index) with Philox, so the backward 
 from __future__ import annotations
 
 import ctypes
-import os
 import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -26,10 +25,6 @@ _EMB_PARTIALS = 2048  # the embedding backward's (2x the waves in flight: 124 ->
 # lazy table Adam: stage the step's unique rows (asme_lazy_adam_stage) so every reader gathers them in slot order
 # (True), or catch them up in place in the table and gather by id (False; the A/B switch)
 STAGE_ROWS = True
-# reduce the table gradient and apply the staged Adam step in one pass when nothing else needs the gradient rows
-FUSED_APPLY = os.environ.get("ASME_FUSED_APPLY", "1") != "0"
-# a fresh table without weight decay starts with its rows at rest (LazyTableState.start); 0: A/B switch
-REST_ROWS = os.environ.get("ASME_REST_ROWS", "1") != "0"
 
 
 def new_seed(p: float) -> int:
@@ -98,12 +93,13 @@ class LazyTableState:
         self.step = 0
         self.rest = False  # some rows may be at rest (last_step == REST_STEP)
 
-    def start(self, step: int, fresh: bool, wd: float):
+    def start(self, step: int, fresh: bool, wd: float, rest_rows: bool = True):
         """every row is current up to `step`; `fresh` (moments just created, all +0) without weight decay: every row
         starts AT REST (last_step = REST_STEP, csrc/adam_math.h kRestStep) -- its zero-gradient dense update is the
-        identity bit for bit, so no kernel replays, reads or writes it until its first gradient"""
+        identity bit for bit, so no kernel replays, reads or writes it until its first gradient (rest_rows=False:
+        every row starts current, the A/B form; FusedAdam(rest_rows=...))"""
         self.step = step
-        self.rest = bool(REST_ROWS and fresh and wd == 0.0)
+        self.rest = bool(rest_rows and fresh and wd == 0.0)
         self.last_step.fill_(REST_STEP if self.rest else step)
 
     def record(self, step: int, lr, b1, b2, eps, wd):
@@ -144,10 +140,12 @@ class LazyTableState:
              ptr(out[1]), ptr(out[2]), stream())
         return out
 
-    def apply(self, plan: "SparseTablePlan", step: int):
+    def apply(self, plan: "SparseTablePlan", step: int, fused: bool = True):
+        """the step's Adam update of the plan's rows; `fused`: reduce the table gradient and apply the staged step in
+        one pass (asme_table_grad_reduce_apply) when nothing else needs the gradient rows (FusedAdam(fused_apply=...))"""
         D = self.param.shape[1]
         if plan.staged is not None:
-            if FUSED_APPLY and plan.reduce_apply(self, step):
+            if fused and plan.reduce_apply(self, step):
                 plan.staged = None
                 return
             st = plan.staged
@@ -609,9 +607,6 @@ class _EmbeddingLnFn(torch.autograd.Function):
                 g[2] if ctx.has[3] else None, g[3] if ctx.has[3] else None, g[4], g[5], None, None)
 
 
-# the fused next LayerNorm (ln3) is taken when the hidden size allows the 4-wide kernels; 0: A/B switch
-FUSE_EMBEDDING_LN = os.environ.get("ASME_FUSE_EMB_LN", "1") != "0"
-
 
 def embedding(ids, table, pos=None, ln1=None, extra=None, ln2=None, spec: EmbeddingSpec = None, ln3=None):
     """The fused embedding; `ln3` (an nn.LayerNorm): also return ln3(x) from the same kernel -> (x, ln3(x))."""
@@ -619,7 +614,9 @@ def embedding(ids, table, pos=None, ln1=None, extra=None, ln2=None, spec: Embedd
     ln2_w, ln2_b = (None, None) if ln2 is None else ln2
     if ln3 is not None:
         D = table.shape[1]
-        if FUSE_EMBEDDING_LN and D % 4 == 0 and (ln2_w is None or ln2_b is not None):
+        # the fused next LayerNorm (ln3) when the hidden size allows the 4-wide kernels (whether ln3 is handed in at
+        # all is the model's fuse_embedding_norm property)
+        if D % 4 == 0 and (ln2_w is None or ln2_b is not None):
             return _EmbeddingLnFn.apply(ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, ln3.weight, ln3.bias,
                                         spec, float(ln3.eps))
         x = _EmbeddingFn.apply(ids, table, pos, ln1_w, ln1_b, extra, ln2_w, ln2_b, spec)

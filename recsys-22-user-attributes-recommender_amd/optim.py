@@ -18,11 +18,16 @@ from .ops import LazyTableState
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 lazy_table: bool = True):
+                 lazy_table: bool = True, fused_apply: bool = True, rest_rows: bool = True):
+        """lazy_table: the item table's exact lazy Adam (False: every row's update from the compact rows each step);
+        fused_apply: its table gradient reduced and applied in one pass; rest_rows: a fresh table without weight
+        decay starts with its rows at rest.  The last three are bit-identical A/B forms of the same update."""
         if lr < 0.0 or eps < 0.0 or weight_decay < 0.0:
             raise ValueError("invalid Adam hyper-parameter")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
         self.lazy_table = lazy_table
+        self.fused_apply = fused_apply
+        self.rest_rows = rest_rows
 
     def flush(self):
         """Bring lazily-updated item tables fully up to date (exact dense-Adam state)."""
@@ -33,12 +38,20 @@ class FusedAdam(torch.optim.Optimizer):
                     tg.lazy.flush()
 
     def zero_grad(self, set_to_none: bool = True):
+        """as torch's, and for a row-sparse item table: drops the applied plan (the kept ".grad" a step without a new
+        backward would reuse) and a pending plan whose backward ran but whose optimizer step was skipped (GradScaler's
+        inf/NaN skip, a trainer skipping the step) -- the one signal that a table gradient is to be discarded.  A
+        plan that has no gradient yet (zero_grad between training_step and backward, Lightning's closure order)
+        is kept."""
         super().zero_grad(set_to_none=set_to_none)
         for group in self.param_groups:
             for p in group["params"]:
                 tg = getattr(p, "_asme_table_grad", None)
                 if tg is not None:
                     tg.drop_applied()
+                    if tg.plan is not None and not tg.plan.consumed and tg.plan.has_gradient():
+                        tg.plan.release()
+                        tg.plan = None
 
     def state_dict(self):
         """flush first: lazily-deferred table rows must be current in the saved moments"""
@@ -96,11 +109,11 @@ class FusedAdam(torch.optim.Optimizer):
                     if self.lazy_table:
                         if tg.lazy is None:
                             tg.lazy = LazyTableState(p, st["exp_avg"], st["exp_avg_sq"])
-                            tg.lazy.start(st["step"] - 1, fresh, wd)  # every row is current up to now
+                            tg.lazy.start(st["step"] - 1, fresh, wd, self.rest_rows)  # every row current up to now
                         elif reapply:  # no forward caught these rows up this time
                             tg.lazy.catch_up(plan.unique, plan.count, plan.capacity)
                         tg.lazy.record(st["step"], lr, b1, b2, eps, wd)
-                        tg.lazy.apply(plan, st["step"])
+                        tg.lazy.apply(plan, st["step"], self.fused_apply)
                     else:
                         call("asme_adam_rows_step", ptr(p), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), V, D,
                              ptr(plan.row_slot_map()), ptr(plan.grad_rows), lr, b1, b2, eps, wd, st["step"], stream())

@@ -162,3 +162,32 @@ def test_reduce_rows_column_sums(asme, dev, rows, width):
     torch.testing.assert_close(out.double(), want, rtol=1e-5, atol=1e-4)
     asme._lib.call("asme_reduce_rows", part.data_ptr(), rows, width, out.data_ptr(), 0, asme._lib.stream())
     torch.testing.assert_close(out.double(), part.double().sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("which", ["blk0_output", "blk1_input", "blk1_output"])
+def test_hooks_on_every_block_norm_run(asme, dev, which):
+    """A forward hook on any block's input / output norm runs (that norm becomes a module call after the residual
+    kernel) and the outputs and gradients equal the fused path's; a hook that rescales the norm's output changes
+    the result exactly as in nn.LayerNorm semantics"""
+    res = []
+    for variant in ("fused", "hook", "scale"):
+        torch.manual_seed(0)
+        m = asme.SASRecModel(transformer_hidden_size=32, num_transformer_heads=2, num_transformer_layers=2,
+                             item_vocab_size=100, max_seq_length=12, transformer_dropout=0.0).to(dev)
+        blocks = m._sequence_representation_layer.transformer_layer.transformer_blocks
+        norm = {"blk0_output": blocks[0].output_sublayer.norm, "blk1_input": blocks[1].input_sublayer.norm,
+                "blk1_output": blocks[1].output_sublayer.norm}[which]
+        fired = []
+        if variant == "hook":
+            norm.register_forward_hook(lambda mod, inp, out: fired.append(out.shape))
+        elif variant == "scale":
+            norm.register_forward_hook(lambda mod, inp, out: out * 2.0)
+        seq = torch.randint(1, 100, (3, 12), generator=torch.Generator().manual_seed(1)).to(dev)
+        rep = m.encode(asme.InputSequence(seq, seq.ne(0)))
+        rep.square().sum().backward()
+        assert len(fired) == (1 if variant == "hook" else 0)
+        res.append((rep.detach(), {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}))
+    torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-5)
+    for n, g in res[0][1].items():
+        torch.testing.assert_close(res[1][1][n], g, rtol=1e-4, atol=1e-4 * float(g.abs().max()) + 1e-7)
+    assert not torch.allclose(res[2][0], res[0][0])  # the hook's returned output was used

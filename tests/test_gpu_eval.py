@@ -84,3 +84,46 @@ def test_sharded_eval_single_rank(asme, dev):
     finally:
         if fresh:
             dist.destroy_process_group()
+
+
+def test_catalog_rank_and_topk_at_ten_million_items(asme, dev):
+    """SURVEY §8f row 1 at its full size: ranks and top-k of 512 queries over |V| = 10,000,003 items, d = 128
+    (BASELINE C4's catalogue), without materialising the (512, 10M) scores, against a chunked float64 torch
+    reference on the same device.  The kernel scores in fp32, so a target's rank is exact up to the items whose
+    float64 score lies within the fp32 error band of the target's: 1 + #{s > t + eps} <= rank <= 1 + #{s > t - eps}
+    (minus the target itself), and the band holds only a handful of items."""
+    torch.manual_seed(10)
+    nq, V, d, k = 512, 10_000_003, 128, 10
+    E = torch.randn(V, d, device=dev) / d ** 0.5
+    H = torch.randn(nq, d, device=dev)
+    targets = torch.randint(0, V, (nq,), device=dev)
+    # a few targets near the top of their rows, so the ranks are not all ~V/2
+    top_ids = asme.ops.catalog_topk(H[:8], E, 1)[1][:, 0]
+    targets[:8] = top_ids
+    ranks = asme.ops.catalog_rank(H, E, targets)
+    vals, idx = asme.ops.catalog_topk(H, E, k)
+    torch.cuda.synchronize()
+    H64 = H.double()
+    t64 = (H64 * E.index_select(0, targets).double()).sum(1)
+    eps = 2e-6 * H64.abs().sum(1) * float(E.abs().max())
+    lo = torch.zeros(nq, dtype=torch.int64, device=dev)
+    hi = torch.zeros(nq, dtype=torch.int64, device=dev)
+    best_v = torch.full((nq, k), -float("inf"), dtype=torch.float64, device=dev)
+    chunk = 1 << 21
+    for c0 in range(0, V, chunk):
+        s = H64 @ E[c0:c0 + chunk].double().t()
+        lo += (s > (t64 + eps)[:, None]).sum(1)
+        hi += (s > (t64 - eps)[:, None]).sum(1)
+        best_v = torch.topk(torch.cat([best_v, torch.topk(s, k, dim=1).values], 1), k, dim=1).values
+        del s
+    hi -= 1  # the target's own score is inside its band
+    assert bool(((1 + lo) <= ranks).all()) and bool((ranks <= (1 + hi)).all())
+    assert int((hi - lo).max()) <= 64
+    assert int(ranks[:8].max()) <= 1 + int((hi - lo)[:8].max())
+    # top-k: each returned item's float64 score matches its value and belongs to the float64 top-k (up to the band)
+    s_idx = (H64[:, None, :] * E.index_select(0, idx.reshape(-1)).double().view(nq, k, d)).sum(2)
+    assert bool(((s_idx - vals.double()).abs() <= eps[:, None]).all())
+    assert bool((vals[:, :-1] >= vals[:, 1:]).all())
+    assert bool((s_idx >= best_v[:, -1:] - 2 * eps[:, None]).all())
+    assert bool((idx >= 0).all()) and bool((idx < V).all())
+    assert all(len(set(r)) == k for r in idx.tolist())

@@ -114,9 +114,9 @@ def test_staged_rows_match_in_place_catch_up(asme, dev, monkeypatch):
     out = []
     for staged, fused in ((True, True), (True, False), (False, True)):
         monkeypatch.setattr(asme.ops, "STAGE_ROWS", staged)
-        monkeypatch.setattr(asme.ops, "FUSED_APPLY", fused)
         model, module, batch = _sasrec(asme, dev, "sparse")
         opt = module.configure_optimizers()
+        opt.fused_apply = fused  # FusedAdam(fused_apply=...)
         seen = []
         for i in range(4):
             module.train()
@@ -141,7 +141,8 @@ def test_staged_rows_match_in_place_catch_up(asme, dev, monkeypatch):
 def test_skipped_optimizer_step_drops_the_table_gradient(asme, dev):
     """a backward whose optimizer step is skipped (a GradScaler inf/NaN skip, a trainer skipping the step) drops the
     row-sparse table gradient, as zero_grad drops a dense one: the next step equals a run without the skipped
-    backward.  Gradient accumulation (accumulate_grad_batches > 1) raises instead of merging silently."""
+    backward.  Without that zero_grad (gradient accumulation: a second training_step + backward before the step)
+    the next training_step raises instead of dropping or merging the first table gradient."""
     out = []
     for skip in (False, True):
         model, module, batch = _sasrec(asme, dev, "sparse")
@@ -154,7 +155,18 @@ def test_skipped_optimizer_step_drops_the_table_gradient(asme, dev):
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
     model, module, batch = _sasrec(asme, dev, "sparse")
-    module.accumulate_grad_batches = 2
+    opt = module.configure_optimizers()
     module.training_step(batch, 0)["loss"].backward()
     with pytest.raises(RuntimeError, match="gradient accumulation"):
         module.training_step(batch, 1)
+    # zero_grad between training_step and backward (Lightning's closure order) keeps the step's plan
+    model, module, batch = _sasrec(asme, dev, "sparse")
+    opt = module.configure_optimizers()
+    loss = module.training_step(batch, 0)["loss"]
+    opt.zero_grad()
+    asme.modules.backward(loss)
+    opt.step()
+    opt.zero_grad()
+    assert _params(model).keys() == out[0].keys()
+    for k in out[0]:
+        assert torch.equal(_params(model)[k], out[0][k]), k

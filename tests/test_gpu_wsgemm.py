@@ -62,6 +62,24 @@ def test_ws_linear_rejects_unsupported(asme):
     assert lib.asme_ws_linear_supported(100, 128, 100) == 0      # N not a multiple of 64 / 96
     assert lib.asme_ws_linear_supported(100, 512, 384) == 0      # split W block over 160 KiB of LDS
     assert lib.asme_ws_linear_supported(1 << 22, 128, 512) == 0  # Y over 2 GiB
+    # K = 128, N = 4096: 128-feature blocks fit an XCD's 32 workgroups, but the activation-factor epilogue's
+    # 64-feature blocks would not -- refused for every epilogue rather than leaving Y unwritten
+    assert lib.asme_ws_linear_supported(100, 128, 4096) == 0
+    assert lib.asme_ws_linear_supported(100, 128, 2048) == 1
+
+
+def test_ws_gelu_bwd_wide_feature_blocks(asme, dev):
+    """the activation-factor epilogue at K = 128, N = 2048 (a CT = 8 shape that runs on 64-feature blocks): every
+    output element written, equal to (dY W2) * factor"""
+    torch.manual_seed(9)
+    M, D, Fd = 3000, 128, 2048
+    w2 = torch.randn(D, Fd, device=dev) / Fd ** 0.5
+    dy = torch.randn(M, D, device=dev)
+    fac = torch.rand(M, Fd, device=dev)
+    d_pre = _call(asme, dy, w2, Fd, 1, epi=2, pre_in=fac, p=0.0, seed=1)
+    ref = (dy.double() @ w2.double()) * fac.double()
+    assert torch.isfinite(d_pre).all()
+    assert (d_pre.double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.parametrize("p", [0.0, 0.2])

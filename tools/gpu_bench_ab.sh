@@ -8,10 +8,10 @@ rc=$?; tail -3 gpurun_out/tab.log; [ $rc -eq 0 ] || exit $rc
 fi
 for i in $(seq ${ROUNDS:-2}); do
  for lib in recsys-22-user-attributes-recommender_amd/libasme_mi.so ${VARIANTS:-}; do
-  ASME_MI_LIB=$lib timeout -k 10 200 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/bab.log 2>&1 || exit 1
+  ASME_MI_LIB=$lib timeout -k 10 200 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --full-json gpurun_out/bab_full.json ${BENCH_ARGS:-} > gpurun_out/bab.log 2>&1 || exit 1
   python - "$lib" <<'P'
 import json, sys
-j = json.loads(open("gpurun_out/bab.log").read().strip().splitlines()[-1])
+j = json.load(open("gpurun_out/bab_full.json"))
 ks = {r["kernel"]: r["avg_ms"] for r in j.get("rooflines", [])}
 print(sys.argv[1].split("/")[-1], j["value"], j["ms_per_step"], "flush", j.get("flush_ms"), "stage", ks.get("asme_lazy_adam_stage"))
 P

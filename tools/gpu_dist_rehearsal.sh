@@ -1,12 +1,18 @@
-# multi-rank rehearsal of the bench's N > 1 path on ONE GPU over gloo (the driver runs the real N = 2..8 over RCCL):
-# dp + row-shard at 2 and 4 ranks, small steps; then the one-rank sharded path over RCCL
+#!/bin/bash
+# Multi-rank rehearsal of the bench's N > 1 path on ONE GPU over gloo (the driver runs the real N = 2..8 over RCCL on
+# an 8-GPU node): the driver's own form `python bench.py --gpus N` (bench.py launches the N ranks itself), then the
+# torchrun form, then the one-rank sharded path over RCCL.  OUT=gpurun_out/<tag>.
 set -u
-cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
-for N in 2 4; do
-  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-      --master-port $((29600 + N)) bench.py --gpus $N --steps 3 --warmup 1 --cpu-baseline 0 --legs none --backend gloo \
-      > gpurun_out/dist_$N.json 2> gpurun_out/dist_$N.err || exit $?
-  python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], r['value'], r['ms_per_step'], r['config']['parallelism'])" gpurun_out/dist_$N.json $N
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=${OUT:-gpurun_out/dist}; mkdir -p $OUT
+for N in ${NS:-2}; do
+  timeout -k 10 400 python bench.py --gpus $N --backend gloo --legs none --cpu-baseline 0 --steps 3 --warmup 1 \
+      --full-json $OUT/launch_$N.full.json > $OUT/launch_$N.json 2> $OUT/launch_$N.err || { tail -5 $OUT/launch_$N.err; exit 1; }
+  python tools/bench_summary.py $OUT/launch_$N.json
 done
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-baseline 0 --legs none --sharded > gpurun_out/dist_s1.json 2> gpurun_out/dist_s1.err || exit $?
-python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('sharded1', r['value'], r['ms_per_step'], r['config']['parallelism'])" gpurun_out/dist_s1.json
+if [ -n "${TORCHRUN:-}" ]; then
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29602 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-baseline 0 --legs none --backend gloo \
+      --full-json $OUT/torchrun_2.full.json > $OUT/torchrun_2.json 2> $OUT/torchrun_2.err || { tail -5 $OUT/torchrun_2.err; exit 1; }
+  python tools/bench_summary.py $OUT/torchrun_2.json
+fi
