@@ -188,6 +188,8 @@ def test_hooks_on_every_block_norm_run(asme, dev, which):
         assert len(fired) == (1 if variant == "hook" else 0)
         res.append((rep.detach(), {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}))
     torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-5)
+    # (the key projection's bias has an analytically zero gradient: rounding noise, held to the global scale)
+    gmax = max(float(g.abs().max()) for g in res[0][1].values())
     for n, g in res[0][1].items():
-        torch.testing.assert_close(res[1][1][n], g, rtol=1e-4, atol=1e-4 * float(g.abs().max()) + 1e-7)
+        torch.testing.assert_close(res[1][1][n], g, rtol=1e-4, atol=1e-4 * max(float(g.abs().max()), 1e-2 * gmax))
     assert not torch.allclose(res[2][0], res[0][0])  # the hook's returned output was used

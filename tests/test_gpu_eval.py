@@ -90,8 +90,9 @@ def test_catalog_rank_and_topk_at_ten_million_items(asme, dev):
     """SURVEY §8f row 1 at its full size: ranks and top-k of 512 queries over |V| = 10,000,003 items, d = 128
     (BASELINE C4's catalogue), without materialising the (512, 10M) scores, against a chunked float64 torch
     reference on the same device.  The kernel scores in fp32, so a target's rank is exact up to the items whose
-    float64 score lies within the fp32 error band of the target's: 1 + #{s > t + eps} <= rank <= 1 + #{s > t - eps}
-    (minus the target itself), and the band holds only a handful of items."""
+    float64 score lies within the fp32 error band of the target's (eps = 2e-6 of sum |h_k e_k| per score, both
+    sides): 1 + #{s > t + eps} <= rank <= 1 + #{s > t - eps} (minus the target itself).  At 10M items the band holds
+    up to a few hundred items around the median score (~4M items per unit of score), none near the top."""
     torch.manual_seed(10)
     nq, V, d, k = 512, 10_000_003, 128, 10
     E = torch.randn(V, d, device=dev) / d ** 0.5
@@ -104,26 +105,37 @@ def test_catalog_rank_and_topk_at_ten_million_items(asme, dev):
     vals, idx = asme.ops.catalog_topk(H, E, k)
     torch.cuda.synchronize()
     H64 = H.double()
-    t64 = (H64 * E.index_select(0, targets).double()).sum(1)
-    eps = 2e-6 * H64.abs().sum(1) * float(E.abs().max())
+    Et = E.index_select(0, targets).double()
+    t64 = (H64 * Et).sum(1)
+    rel = 2e-6
+    eps_t = rel * (H64.abs() * Et.abs()).sum(1)
+    A64 = H64.abs()
     lo = torch.zeros(nq, dtype=torch.int64, device=dev)
     hi = torch.zeros(nq, dtype=torch.int64, device=dev)
     best_v = torch.full((nq, k), -float("inf"), dtype=torch.float64, device=dev)
-    chunk = 1 << 21
+    best_e = torch.zeros((nq, k), dtype=torch.float64, device=dev)
+    chunk = 1 << 20
     for c0 in range(0, V, chunk):
-        s = H64 @ E[c0:c0 + chunk].double().t()
-        lo += (s > (t64 + eps)[:, None]).sum(1)
-        hi += (s > (t64 - eps)[:, None]).sum(1)
-        best_v = torch.topk(torch.cat([best_v, torch.topk(s, k, dim=1).values], 1), k, dim=1).values
-        del s
+        Ec = E[c0:c0 + chunk].double()
+        s = H64 @ Ec.t()
+        eps = rel * (A64 @ Ec.abs().t()) + eps_t[:, None]
+        lo += (s > t64[:, None] + eps).sum(1)
+        hi += (s > t64[:, None] - eps).sum(1)
+        v, j = torch.topk(s, k, dim=1)
+        cand_v, cand_e = torch.cat([best_v, v], 1), torch.cat([best_e, eps.gather(1, j)], 1)
+        best_v, o = torch.topk(cand_v, k, dim=1)
+        best_e = cand_e.gather(1, o)
+        del s, eps, Ec
     hi -= 1  # the target's own score is inside its band
     assert bool(((1 + lo) <= ranks).all()) and bool((ranks <= (1 + hi)).all())
-    assert int((hi - lo).max()) <= 64
-    assert int(ranks[:8].max()) <= 1 + int((hi - lo)[:8].max())
+    assert int((hi - lo).max()) <= 2000, int((hi - lo).max())
+    assert int(ranks[:8].max()) <= 1 + int((hi - lo)[:8].max())  # the top-1 targets rank (near) first
     # top-k: each returned item's float64 score matches its value and belongs to the float64 top-k (up to the band)
-    s_idx = (H64[:, None, :] * E.index_select(0, idx.reshape(-1)).double().view(nq, k, d)).sum(2)
-    assert bool(((s_idx - vals.double()).abs() <= eps[:, None]).all())
+    Ei = E.index_select(0, idx.reshape(-1)).double().view(nq, k, d)
+    s_idx = (H64[:, None, :] * Ei).sum(2)
+    e_idx = rel * (A64[:, None, :] * Ei.abs()).sum(2)
+    assert bool(((s_idx - vals.double()).abs() <= e_idx).all())
     assert bool((vals[:, :-1] >= vals[:, 1:]).all())
-    assert bool((s_idx >= best_v[:, -1:] - 2 * eps[:, None]).all())
+    assert bool((s_idx >= best_v[:, -1:] - e_idx - best_e[:, -1:]).all())
     assert bool((idx >= 0).all()) and bool((idx < V).all())
     assert all(len(set(r)) == k for r in idx.tolist())
