@@ -380,6 +380,23 @@ int asme_catalog_target_scores(const float* H, int64_t ld_h, int64_t nq, int64_t
 int asme_catalog_count_above(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* E, int64_t ld_e,
                              int64_t V_local, const float* bias, const int64_t* targets, const float* tscore,
                              int64_t id_stride, int64_t id_offset, int32_t* counts, void* stream);
+/* The same ranking on the bf16x6 logits engine (csrc/logits.hip, round 5): scores are the fp32-level products
+ * asme_logits materialises, never stored; dim a multiple of 4 up to 128.  The catalogue is split once into three
+ * bf16 planes (asme_catalog_split, asme_catalog_planes_bytes(V) bytes) and ranked against many query batches;
+ * workspace: asme_catalog_x6_workspace(nq, dim) bytes. */
+int64_t asme_catalog_planes_bytes(int64_t rows);
+int asme_catalog_split(const float* X, int64_t ld, int64_t rows, int64_t dim, void* planes, void* stream);
+int64_t asme_catalog_x6_workspace(int64_t nq, int64_t dim);
+int asme_catalog_rank_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* E, int64_t ld_e,
+                         const void* E_planes, int64_t V, const float* bias, const int64_t* targets, int32_t* counts_ws,
+                         int64_t* ranks, void* workspace, int64_t ws_bytes, void* stream);
+int asme_catalog_target_scores_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* rows,
+                                  int64_t ld_rows, const float* row_bias, float* tscore, void* workspace,
+                                  int64_t ws_bytes, void* stream);
+int asme_catalog_count_above_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const void* E_planes,
+                                int64_t V_local, const float* bias, const int64_t* targets, const float* tscore,
+                                int64_t id_stride, int64_t id_offset, int32_t* counts, void* workspace,
+                                int64_t ws_bytes, void* stream);
 
 
 /* ---- Deterministic table gradient (csrc/sharding.hip; SURVEY §8b embedding_scatter_add_bwd

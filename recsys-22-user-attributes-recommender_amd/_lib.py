@@ -63,6 +63,12 @@ SIGNATURES = {
     "asme_catalog_topk": [p, i64, i64, i64, p, i64, i64, p, i64, i64, i64, p, i64, p, p, p],
     "asme_catalog_target_scores": [p, i64, i64, i64, p, i64, p, p, p],
     "asme_catalog_count_above": [p, i64, i64, i64, p, i64, i64, p, p, p, i64, i64, p, p],
+    "asme_catalog_planes_bytes": [i64],
+    "asme_catalog_split": [p, i64, i64, i64, p, p],
+    "asme_catalog_x6_workspace": [i64, i64],
+    "asme_catalog_rank_x6": [p, i64, i64, i64, p, i64, p, i64, p, p, p, p, p, i64, p],
+    "asme_catalog_target_scores_x6": [p, i64, i64, i64, p, i64, p, p, p, i64, p],
+    "asme_catalog_count_above_x6": [p, i64, i64, i64, p, i64, p, p, p, i64, i64, p, p, i64, p],
     "asme_linear_fwd": [p, i64, i64, i64, p, p, i64, p, i64, p],
     "asme_linear_dx": [p, i64, i64, i64, p, i64, p, i64, i32, p],
     "asme_attention_dropout_mask_bytes": [i64, i64, i64],
@@ -122,7 +128,8 @@ _RESTYPES = {"asme_mi_last_error": ctypes.c_char_p, "asme_dedup_workspace_bytes"
              "asme_catalog_topk_workspace": ctypes.c_int64, "asme_linear_xent_fwd_workspace": ctypes.c_int64,
              "asme_linear_xent_bwd_workspace": ctypes.c_int64,
              "asme_linear_xent_fwd_dh_workspace": ctypes.c_int64, "asme_linear_xent_bwd_dw_workspace": ctypes.c_int64, "asme_logits_workspace": ctypes.c_int64, "asme_bucket_by_owner_workspace": ctypes.c_int64, "asme_occurrence_csr_workspace": ctypes.c_int64,
-             "asme_table_grad_workspace": ctypes.c_int64}
+             "asme_table_grad_workspace": ctypes.c_int64, "asme_catalog_planes_bytes": ctypes.c_int64,
+             "asme_catalog_x6_workspace": ctypes.c_int64}
 
 _lib: Optional[ctypes.CDLL] = None
 

@@ -451,6 +451,12 @@ __global__ __launch_bounds__(256) void lazy_row_kernel(const int64_t* __restrict
 #endif
 constexpr int kPipeRows = ASME_FLUSH_RPW;  // slots per wave
 constexpr int kPipeDepth = ASME_FLUSH_PF;  // rows in the register ring (PF - 1 in flight during a replay)
+#ifndef ASME_STAGE_P_NT
+#define ASME_STAGE_P_NT 0
+#endif
+#ifndef ASME_STAGE_MV_NT
+#define ASME_STAGE_MV_NT 1
+#endif
 template <int NP, int RPW, int PF, bool STAGE>
 __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restrict__ rows,
                                                         const int32_t* __restrict__ count, int64_t cap,
@@ -522,10 +528,24 @@ __global__ __launch_bounds__(256) void lazy_pipe_kernel(const int64_t* __restric
 #pragma unroll
             for (int j = 0; j < NP; ++j) {
                 const int64_t off = orow * D + 2 * lane + 128 * j;
-                if (STAGE) {  // (read again by this step's gathers)
+                if (STAGE) {
+                    // the staged parameters are read again right away by this step's gathers (the embedding
+                    // forward follows this kernel); the staged moments only by the reduce-and-apply at the end of the
+                    // step, ~6 ms and GBs of traffic later: streamed past the L2 / MALL, so their dirty lines do
+                    // not drain into the next kernel's HBM time (an 0.9 GB cached write before the embedding forward
+                    // cost it 55 -> 84 us, tools/emb_ln_bench.py)
+#if ASME_STAGE_P_NT
+                    table_store2(op + off, P[sl][j].x, P[sl][j].y);
+#else
                     *reinterpret_cast<float2*>(op + off) = make_float2(P[sl][j].x, P[sl][j].y);
+#endif
+#if ASME_STAGE_MV_NT
+                    table_store2(om + off, M[sl][j].x, M[sl][j].y);
+                    table_store2(ov + off, Vv[sl][j].x, Vv[sl][j].y);
+#else
                     *reinterpret_cast<float2*>(om + off) = make_float2(M[sl][j].x, M[sl][j].y);
                     *reinterpret_cast<float2*>(ov + off) = make_float2(Vv[sl][j].x, Vv[sl][j].y);
+#endif
                 } else {
                     table_store2(op + off, P[sl][j].x, P[sl][j].y);
                     table_store2(om + off, M[sl][j].x, M[sl][j].y);

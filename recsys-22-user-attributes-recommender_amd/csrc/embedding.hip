@@ -196,6 +196,58 @@ __device__ __forceinline__ uint32_t emb_keep_bits(uint64_t seed, uint64_t chunk,
 
 __host__ __device__ inline uint64_t emb_seed(uint64_t s1, uint64_t s2) { return s1 ^ (s2 * 0x9E3779B97F4A7C15ull); }
 
+// Keep bytes of token t: (T, D/4) bytes.  When the row layout covers the row exactly (LPR * NV * 4 == D: D = 128 on
+// 16 lanes x 2 chunks, D = 512 on 64 x 2, and every one-chunk layout) a lane's NV bytes are adjacent -- byte
+// sub * NV + j holds chunk sub + LPR * j -- so each lane stores / loads them as ONE 8- or 16-bit access per token
+// (16-lane groups move 32 contiguous bytes) instead of NV byte accesses; other layouts keep chunk order (byte = chunk).
+// ops.embedding_keep_chunks() converts to chunk order.
+template <class R>
+__device__ __forceinline__ bool emb_keep_packed(int D) { return R::LPR * R::NV * 4 == D; }
+// the 16-lane, two-chunk layout is taken for D = 128 only (with_emb_layout): there the width is a compile-time
+// constant, so the column bounds checks and the 1 / D of the statistics fold away
+template <class R>
+__device__ __forceinline__ int emb_width(int D) { return (R::LPR == 16 && R::NV == 2) ? 128 : D; }
+template <class R>
+__device__ __forceinline__ void emb_keep_store(uint8_t* __restrict__ keep, int64_t t, int sub, int D,
+                                               const uint32_t (&bits)[R::NV]) {
+    uint8_t* row = keep + (uint64_t)t * (D >> 2);
+    if (emb_keep_packed<R>(D)) {
+        if constexpr (R::NV == 2) {
+            *reinterpret_cast<uint16_t*>(row + sub * 2) = (uint16_t)(bits[0] | (bits[1] << 8));
+        } else {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j) row[sub * R::NV + j] = (uint8_t)bits[j];
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < R::NV; ++j) {
+        const int c = R::col(sub, j);
+        if (c < D) row[c >> 2] = (uint8_t)bits[j];
+    }
+}
+template <class R>
+__device__ __forceinline__ void emb_keep_load(const uint8_t* __restrict__ keep, int64_t t, int sub, int D,
+                                              uint32_t (&bits)[R::NV]) {
+    const uint8_t* row = keep + (uint64_t)t * (D >> 2);
+    if (emb_keep_packed<R>(D)) {
+        if constexpr (R::NV == 2) {
+            const uint32_t v = *reinterpret_cast<const uint16_t*>(row + sub * 2);
+            bits[0] = v & 0xFFu;
+            bits[1] = v >> 8;
+        } else {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j) bits[j] = row[sub * R::NV + j];
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < R::NV; ++j) {
+        const int c = R::col(sub, j);
+        bits[j] = row[(c < D ? c : 0) >> 2];
+    }
+}
+
 // LN3 (the fused next LayerNorm): the first transformer block's input norm applied to the embedding output in the
 // same pass (transformer_layers.py:251-258 SublayerConnection: x + dropout(sublayer(norm(x))) of block 0), so the
 // block reads `out3` and keeps `out` as its residual stream: no separate LayerNorm launch re-reading the rows.
@@ -212,14 +264,23 @@ struct EmbLn3 {
 #ifndef ASME_EMB_FWD_HOIST
 #define ASME_EMB_FWD_HOIST 1
 #endif
+// diagnostic builds only (tools/build_variant.sh): 1 = the forward's LayerNorm statistics skipped (mean 0, rstd 1),
+// 2 = its dropout decisions not drawn (every element kept, keep bytes still stored)
+#ifndef ASME_EMB_DIAG
+#define ASME_EMB_DIAG 0
+#endif
+#ifndef ASME_EMB_NT
+#define ASME_EMB_NT 1
+#endif
 template <class R, int kEmbK, bool LN3, bool LN2 = true>  // kEmbK: tokens per lane group; LN2: as the backward's
 __global__ __launch_bounds__(256) void emb_fwd4_kernel(
-    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
+    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D_,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float eps1, float p1,
     const float* __restrict__ extra, const float* __restrict__ w2, const float* __restrict__ b2, float eps2,
     float p2, uint64_t seed, float* __restrict__ out, float* __restrict__ stats, uint8_t* __restrict__ keep,
     int* __restrict__ err, EmbLn3 l3) {
     static_assert(R::W == 4, "4-wide layout only");
+    const int D = emb_width<R>(D_);
     const int lane = threadIdx.x & 63, sub = lane % R::LPR;
     const int64_t t0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * R::RPW * kEmbK + lane / R::LPR;
     int64_t id[kEmbK];
@@ -289,7 +350,7 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
         float m1 = 0.f, r1 = 1.f, m2 = 0.f, r2 = 1.f;
         RowVals<R> tmp;
         if (w1) {
-            row_ln_stats<R>(x[k], sub, D, eps1, m1, r1);
+            if (ASME_EMB_DIAG != 1) row_ln_stats<R>(x[k], sub, D, eps1, m1, r1);
             row_normalise<R>(x[k], sub, D, m1, r1, tmp);
 #pragma unroll
             for (int j = 0; j < R::NV; ++j)
@@ -301,7 +362,8 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 #pragma unroll
             for (int j = 0; j < R::NV; ++j) {
                 const int c = R::col(sub, j);
-                bits[j] = c < D ? emb_keep_bits(seed, ((uint64_t)t * D + c) >> 2, th1, th2) : 0u;
+                bits[j] = c < D ? (ASME_EMB_DIAG == 2 ? 0xFFu : emb_keep_bits(seed, ((uint64_t)t * D + c) >> 2, th1, th2))
+                                : 0u;
                 if (p1 > 0.f)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
@@ -313,7 +375,7 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 #pragma unroll
                 for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
         if (LN2 && w2) {
-            row_ln_stats<R>(x[k], sub, D, eps2, m2, r2);
+            if (ASME_EMB_DIAG != 1) row_ln_stats<R>(x[k], sub, D, eps2, m2, r2);
             row_normalise<R>(x[k], sub, D, m2, r2, tmp);
 #pragma unroll
             for (int j = 0; j < R::NV; ++j)
@@ -321,23 +383,21 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
                 for (int i = 0; i < 4; ++i) x[k][j][i] = tmp[j][i] * w2v[j][i] + b2v[j][i];
         }
         if (drop) {
+            if (p2 > 0.f)
 #pragma unroll
-            for (int j = 0; j < R::NV; ++j) {
-                if (p2 > 0.f)
+                for (int j = 0; j < R::NV; ++j)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
-                const int c = R::col(sub, j);
-                if (keep && c < D) keep[((uint64_t)t * D + c) >> 2] = (uint8_t)bits[j];
-            }
+            if (keep) emb_keep_store<R>(keep, t, sub, D, bits);
         }
-        row_store<R>(out + t * D, sub, D, x[k]);
+        row_store<R, ASME_EMB_NT>(out + t * D, sub, D, x[k]);
         if (sub == 0 && stats) *reinterpret_cast<float4*>(stats + t * 4) = make_float4(m1, r1, m2, r2);
         if constexpr (LN3) {
-            float m3, r3;
-            row_ln_stats<R>(x[k], sub, D, l3.eps, m3, r3);
+            float m3 = 0.f, r3 = 1.f;
+            if (ASME_EMB_DIAG != 1) row_ln_stats<R>(x[k], sub, D, l3.eps, m3, r3);
             row_normalise<R>(x[k], sub, D, m3, r3, tmp);
             row_affine<R>(tmp, sub, D, w3p, b3p, x[k]);
-            row_store<R>(l3.out + t * D, sub, D, x[k]);
+            row_store<R, ASME_EMB_NT>(l3.out + t * D, sub, D, x[k]);
             if (sub == 0) *reinterpret_cast<float2*>(l3.stats + t * 2) = make_float2(m3, r3);
         }
     }
@@ -364,12 +424,13 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 // (in-step 0.150-0.154 -> 0.139-0.140 ms per call, same box; forcing a fourth wave spills: 0.315 ms)
 template <class R, int kPass, bool LN3, bool LN2>  // kPass: tokens per lane group per grid-stride pass
 __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
-    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D,
+    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V, int D_,
     const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1,
     const float* __restrict__ extra, const float* __restrict__ w2, float p2, uint64_t seed,
     const uint8_t* __restrict__ keep, const float* __restrict__ dout, const float* __restrict__ stats,
     float* __restrict__ d_rows, float* __restrict__ d_extra, float* __restrict__ partials, EmbLn3 l3) {
     static_assert(R::W == 4, "4-wide layout only");
+    const int D = D_;  // (a compile-time width here costs 20 spilled VGPRs at the 168-VGPR cap)
     constexpr int NACC = LN3 ? 6 : 4;
     const int lane = threadIdx.x & 63, sub = lane % R::LPR, wave = threadIdx.x >> 6;
     float acc[NACC][R::NV][R::W];
@@ -432,11 +493,12 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                 row_load<R>(l3.dln + tt * D, sub, D, dl[k]);
                 st3[k] = *reinterpret_cast<const float2*>(l3.stats + tt * 2);
             }
-            // the stored keep bits ride with the row loads (one round trip per pass, not one per byte)
+            // the stored keep bits ride with the row loads (one round trip per pass, one access per lane)
+            if (keep_in) {
+                emb_keep_load<R>(keep, tt, sub, D, kb[k]);
+            } else {
 #pragma unroll
-            for (int j = 0; j < R::NV; ++j) {
-                const int c = R::col(sub, j);
-                kb[k][j] = keep_in ? (uint32_t)keep[((uint64_t)tt * D + (c < D ? c : 0)) >> 2] : 0xFFu;
+                for (int j = 0; j < R::NV; ++j) kb[k][j] = 0xFFu;
             }
         }
 #pragma unroll
@@ -551,9 +613,9 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
                     }
                 RowVals<R> gx;
                 row_ln_bwd<R>(gz, xh1, w1p, st[k].y, sub, D, gx);
-                if (live) row_store<R>(d_rows + t * D, sub, D, gx);
+                if (live) row_store<R, ASME_EMB_NT>(d_rows + t * D, sub, D, gx);
             } else if (live) {
-                row_store<R>(d_rows + t * D, sub, D, gz);
+                row_store<R, ASME_EMB_NT>(d_rows + t * D, sub, D, gz);
             }
         }
     }
@@ -769,7 +831,7 @@ inline int vpl_of(int64_t D) { return (int)((D + 63) / 64); }
 #define ASME_EMB_BWD_LPR16 1
 #endif
 #ifndef ASME_EMB_K
-#define ASME_EMB_K 2
+#define ASME_EMB_K 1
 #endif
 template <class F>
 int with_emb_layout(int64_t D, F&& f, bool lpr16 = ASME_EMB_LPR16) {

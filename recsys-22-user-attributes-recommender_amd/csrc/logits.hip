@@ -62,10 +62,11 @@ constexpr int kTS = 64;                  // streamed rows per LDS tile
 // 512 registers) for the gradient passes, whose stationary fragments + 128-feature accumulators need more
 constexpr int kRowPad = 256;             // plane rows are padded to a multiple of this (>= 32 W, kTS)
 template <int MODE> struct EngineWaves { static constexpr int W = (MODE == 1 || MODE == 2 || MODE == 4) ? 4 : 8; };
+// M_RANK / M_TSCORE (modes 5 / 6): the full-catalogue evaluation's target ranks on the same score product
 constexpr int kPlaneTile = kTS * kRowB;  // 16 KiB: one plane of one tile
 constexpr int kTile = 3 * kPlaneTile;    // 48 KiB
 
-enum { M_STATS = 0, M_DH = 1, M_DW = 2, M_LOGITS = 3, M_FDH = 4 };
+enum { M_STATS = 0, M_DH = 1, M_DW = 2, M_LOGITS = 3, M_FDH = 4, M_RANK = 5, M_TSCORE = 6 };
 
 __host__ __device__ constexpr int64_t pad_rows(int64_t r) { return (r + kRowPad - 1) / kRowPad * kRowPad; }
 
@@ -135,6 +136,11 @@ struct LogitsArgs {
     float* out;              // logits: (n, ld_out)
     int64_t ld_out;
     float* upart;            // fdh: (nchunks, n, d) unnormalised softmax-weighted item rows per chunk
+    // full-catalogue ranking (rank: stationary = queries, streamed = items; tscore: streamed = the queries' gathered
+    // target rows, row q = the target of query q): global item id of streamed row j = j * id_stride + id_offset
+    const float* tscore;     // rank: the target's score per query (from the tscore pass: the same products)
+    int32_t* counts;         // rank: per query, items ranked above the target (atomically summed over chunks)
+    int64_t id_stride, id_offset;
 };
 
 __device__ __forceinline__ bool valid_target(int64_t t, int64_t ignore, int64_t V) {
@@ -196,8 +202,9 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
     const int chunk_id = (int)(blockIdx.x % (unsigned)a.nchunks);
     const int64_t sblock = blockIdx.x / (unsigned)a.nchunks;
     const int64_t srow = sblock * (32 * W) + wave * 32 + r32;  // this lane's stationary row (MFMA column)
-    const int64_t s_begin = (int64_t)chunk_id * a.chunk;
-    const int64_t s_end = std::min(a.strm_pad, s_begin + a.chunk);  // tiles past n_strm read zero planes
+    // (M_TSCORE: the streamed rows are the stationary block's own gathered target rows)
+    const int64_t s_begin = MODE == M_TSCORE ? sblock * (32 * W) : (int64_t)chunk_id * a.chunk;
+    const int64_t s_end = std::min(a.strm_pad, s_begin + (MODE == M_TSCORE ? 32 * W : a.chunk));  // past n_strm: zero planes
 
     // stationary fragments (B operand): row srow, k = 16 ks + 8 h .. +7, three planes
     Bf3 st[KS];
@@ -222,6 +229,17 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
     }
     float run_max = -INFINITY, run_sum = 0.f, t_logit = 0.f;
     bool have_t = false;
+    // M_RANK: this query's target score and, in local row numbers j of the streamed table (item j * id_stride +
+    // id_offset), the target's own row (j_eq, -1 when another shard holds it) and the rows of lower item ids
+    // (j < j_lt): every per-element test below is 32-bit
+    float r_ts = 0.f;
+    int r_jeq = -1, r_jlt = 0, r_cnt = 0;
+    if (MODE == M_RANK && srow < a.n_stat) {
+        r_ts = a.tscore[srow];
+        const int64_t rel = a.targets[srow] - a.id_offset;
+        r_jeq = (rel >= 0 && rel % a.id_stride == 0) ? (int)(rel / a.id_stride) : -1;
+        r_jlt = rel > 0 ? (int)((rel + a.id_stride - 1) / a.id_stride) : 0;
+    }
     floatx16 y[NFT];  // gradient product: Y^T[feature 32 ft + acc_row(i, h)][stationary row r32]
 #pragma unroll
     for (int f = 0; f < NFT; ++f)
@@ -416,6 +434,29 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
 #pragma unroll
             for (int sub = 0; sub < kTS / 32; ++sub) {
                 floatx16 x = score(sub);
+                if (MODE == M_RANK) {
+                    // item i is ranked above the target t iff s_i > s_t, or s_i == s_t and i < t (ties to the lower
+                    // id, the reference argsort's order on tie-free data); s = products + bias exactly as M_TSCORE and
+                    // M_LOGITS form it, so the target compares bit-identically with itself
+                    const int j0 = (int)r0 + 32 * sub, jn = (int)a.n_strm;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int j = j0 + acc_row(i, h);
+                        const float sc = x[i] + tf[32 * sub + acc_row(i, h)];
+                        const bool above = j < jn && j != r_jeq && (sc > r_ts || (sc == r_ts && j < r_jlt));
+                        r_cnt += above ? 1 : 0;
+                    }
+                    continue;
+                }
+                if (MODE == M_TSCORE) {
+                    // the diagonal: streamed row == stationary row (query q's gathered target row)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int lr = 32 * sub + acc_row(i, h);
+                        if (r0 + lr == srow && srow < a.n_stat) a.part2[srow] = x[i] + tf[lr];
+                    }
+                    continue;
+                }
                 if (MODE == M_LOGITS) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
@@ -460,7 +501,12 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
         __syncthreads();
     }
 
-    if (MODE == M_LOGITS) return;
+    if (MODE == M_LOGITS || MODE == M_TSCORE) return;
+    if (MODE == M_RANK) {
+        r_cnt += __shfl_xor(r_cnt, 32, 64);  // the two lane halves hold different streamed rows of one query
+        if (h == 0 && srow < a.n_stat && r_cnt) atomicAdd(a.counts + srow, r_cnt);
+        return;
+    }
     if (MODE == M_FDH) {
         run_sum += __shfl_xor(run_sum, 32, 64);  // (the halves share the running max)
         if (srow < a.n_stat) {
@@ -637,8 +683,9 @@ __global__ __launch_bounds__(kGradW * 64) void logits_grad_kernel(LogitsArgs a) 
     const int chunk_id = (int)(blockIdx.x % (unsigned)a.nchunks);
     const int64_t sblock = blockIdx.x / (unsigned)a.nchunks;
     const int64_t srow = sblock * (32 * W) + wave * 32 + r32;  // this lane's stationary row (MFMA column)
-    const int64_t s_begin = (int64_t)chunk_id * a.chunk;
-    const int64_t s_end = std::min(a.strm_pad, s_begin + a.chunk);  // tiles past n_strm read zero planes
+    // (M_TSCORE: the streamed rows are the stationary block's own gathered target rows)
+    const int64_t s_begin = MODE == M_TSCORE ? sblock * (32 * W) : (int64_t)chunk_id * a.chunk;
+    const int64_t s_end = std::min(a.strm_pad, s_begin + (MODE == M_TSCORE ? 32 * W : a.chunk));  // past n_strm: zero planes
     const int ntiles = (int)((s_end - s_begin) / kTS);
 
     // stationary fragments, loaded straight into AGPRs (the MFMAs read their B operand there): the 256
@@ -1514,4 +1561,169 @@ ASME_API int asme_logits(const float* H, int64_t ld_h, int64_t n, int64_t dim, c
     a.out = out;
     a.ld_out = ld_out;
     return launch_kb<M_LOGITS>(a, p.sblocks, s);
+}
+
+// ------------------------------------------------------------------------------ full-catalogue ranking (bf16x6)
+// The evaluation's target ranks (SASRecProjectionComponent inference, sasrec/components.py:46-61; AllItemsSampler +
+// argsort + get_true_positives, metrics_sampler.py:51-72 and metrics/common.py:4-27) on this engine: the scores are
+// the products asme_logits materialises (bf16x6, 0.53 of the bf16 peak / 6 in the stats pass at the C3 shape, vs
+// 0.49 of the 4x smaller fp32 MFMA peak for csrc/catalog.hip's kernel), never stored.  Two passes: M_TSCORE scores
+// each query against its own gathered target row (the same products, so the target compares bit-identically with
+// itself), then M_RANK streams the catalogue's planes and counts the items ranked above the target.
+namespace {
+__global__ __launch_bounds__(256) void gather_targets_kernel(const float* __restrict__ E, int64_t ld_e, int64_t V,
+                                                             const float* __restrict__ bias,
+                                                             const int64_t* __restrict__ targets, int64_t nq, int d,
+                                                             float* __restrict__ rows, float* __restrict__ tbias) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per 4 features
+    const int c4 = (d + 3) / 4;
+    if (t >= nq * c4) return;
+    const int64_t q = t / c4;
+    const int c = (int)(t % c4) * 4;
+    int64_t it = targets[q];
+    it = (it < 0 || it >= V) ? 0 : it;
+    *reinterpret_cast<float4*>(rows + q * d + c) = *reinterpret_cast<const float4*>(E + it * ld_e + c);
+    if (c == 0 && tbias) tbias[q] = bias ? bias[it] : 0.f;
+}
+
+__global__ void rank_from_counts_kernel(const int32_t* __restrict__ counts, int64_t n, int64_t* __restrict__ ranks) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ranks[i] = (int64_t)counts[i] + 1;
+}
+
+bool catalog_shape_ok(int64_t dim, int64_t ld_h, const void* H) {
+    return dim >= 4 && dim <= kDP && dim % 4 == 0 && ld_h % 4 == 0 && aligned16(H);
+}
+}  // namespace
+
+// bytes of the three bf16 planes of a (rows x dim <= 128) operand (asme_catalog_split)
+ASME_API int64_t asme_catalog_planes_bytes(int64_t rows) { return planes_bytes(rows); }
+
+// planes = the exact three-way bf16 split of X (rows x dim), rows zero-padded: split a catalogue once, rank many
+// query batches against it
+ASME_API int asme_catalog_split(const float* X, int64_t ld, int64_t rows, int64_t dim, void* planes, void* stream) {
+    ASME_CHECK_ARG(X && planes, "asme_catalog_split: null pointer");
+    ASME_CHECK_ARG(catalog_shape_ok(dim, ld, X) && rows >= 1 && rows < (1LL << 31),
+                   "asme_catalog_split: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    return split(X, ld, rows, (int)dim, reinterpret_cast<__bf16*>(planes), (hipStream_t)stream);
+}
+
+// workspace of asme_catalog_target_scores_x6 / asme_catalog_count_above_x6 / asme_catalog_rank_x6 for nq queries
+ASME_API int64_t asme_catalog_x6_workspace(int64_t nq, int64_t dim) {
+    (void)dim;
+    return 2 * align256(planes_bytes(nq)) + align256(nq * kDP * 4) + 2 * align256(nq * 4) + 256;
+}
+
+namespace {
+int target_scores_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* rows, int64_t ld_rows,
+                     const float* row_bias, float* tscore, char* w, hipStream_t s) {
+    __bf16* hp = reinterpret_cast<__bf16*>(w);
+    __bf16* tp = reinterpret_cast<__bf16*>(w + align256(planes_bytes(nq)));
+    int rc = split(H, ld_h, nq, (int)dim, hp, s);
+    if (rc == 0) rc = split(rows, ld_rows, nq, (int)dim, tp, s);
+    if (rc != 0) return rc;
+    const Plan p = make_plan<M_TSCORE>(nq, nq, device_cus());
+    LogitsArgs a{};
+    a.stat = hp;
+    a.strm = tp;
+    a.stat_pad = p.stat_pad;
+    a.strm_pad = p.stat_pad;  // (the same padding: stationary block b reads streamed rows of block b)
+    a.n_stat = nq;
+    a.n_strm = nq;
+    a.chunk = p.stat_pad;
+    a.nchunks = 1;
+    a.d = (int)dim;
+    a.bias = row_bias;
+    a.part2 = tscore;
+    return launch_kb<M_TSCORE>(a, p.sblocks, s);
+}
+
+int count_above_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const void* E_planes, int64_t V,
+                   const float* bias, const int64_t* targets, const float* tscore, int64_t id_stride,
+                   int64_t id_offset, int32_t* counts, char* w, hipStream_t s) {
+    __bf16* hp = reinterpret_cast<__bf16*>(w);
+    int rc = split(H, ld_h, nq, (int)dim, hp, s);
+    if (rc != 0) return rc;
+    if (hipMemsetAsync(counts, 0, nq * sizeof(int32_t), s) != hipSuccess) return hip_status(hipGetLastError(), "memset");
+    const Plan p = make_plan<M_RANK>(nq, V, device_cus());
+    LogitsArgs a{};
+    a.stat = hp;
+    a.strm = reinterpret_cast<const __bf16*>(E_planes);
+    a.stat_pad = p.stat_pad;
+    a.strm_pad = p.strm_pad;
+    a.n_stat = nq;
+    a.n_strm = V;
+    a.chunk = p.chunk;
+    a.nchunks = p.nchunks;
+    a.d = (int)dim;
+    a.bias = bias;
+    a.targets = targets;
+    a.V = V;
+    a.tscore = tscore;
+    a.counts = counts;
+    a.id_stride = id_stride;
+    a.id_offset = id_offset;
+    return launch_kb<M_RANK>(a, p.sblocks, s);
+}
+}  // namespace
+
+// tscore[q] = H[q] . rows[q] (+ row_bias[q]) by the products the ranking pass forms (the sharded evaluation's
+// target scores from the rows their owners sent)
+ASME_API int asme_catalog_target_scores_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* rows,
+                                           int64_t ld_rows, const float* row_bias, float* tscore, void* workspace,
+                                           int64_t ws_bytes, void* stream) {
+    ASME_CHECK_ARG(H && rows && tscore && workspace, "asme_catalog_target_scores_x6: null pointer");
+    ASME_CHECK_ARG(catalog_shape_ok(dim, ld_h, H) && ld_rows % 4 == 0 && aligned16(rows) && nq < (1LL << 31),
+                   "asme_catalog_target_scores_x6: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    ASME_CHECK_ARG(ws_bytes >= asme_catalog_x6_workspace(nq, dim), "asme_catalog_target_scores_x6: workspace too small");
+    if (nq == 0) return 0;
+    const int rc = target_scores_x6(H, ld_h, nq, dim, rows, ld_rows, row_bias, tscore,
+                                    reinterpret_cast<char*>(workspace), (hipStream_t)stream);
+    if (rc != 0) return rc;
+    ASME_LAUNCH_CHECK("asme_catalog_target_scores_x6");
+}
+
+// counts[q] = #{local rows j of E_planes (V rows, asme_catalog_split) ranked above query q's target}: item id
+// j * id_stride + id_offset, ranked above iff its score is higher, or equal with a lower id (overwrites counts)
+ASME_API int asme_catalog_count_above_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const void* E_planes,
+                                         int64_t V, const float* bias, const int64_t* targets, const float* tscore,
+                                         int64_t id_stride, int64_t id_offset, int32_t* counts, void* workspace,
+                                         int64_t ws_bytes, void* stream) {
+    ASME_CHECK_ARG(H && E_planes && targets && tscore && counts && workspace, "asme_catalog_count_above_x6: null pointer");
+    ASME_CHECK_ARG(catalog_shape_ok(dim, ld_h, H) && V >= 1 && V < (1LL << 31) && nq < (1LL << 31),
+                   "asme_catalog_count_above_x6: bad shape");
+    ASME_CHECK_ARG(ws_bytes >= asme_catalog_x6_workspace(nq, dim), "asme_catalog_count_above_x6: workspace too small");
+    if (nq == 0) return 0;
+    const int rc = count_above_x6(H, ld_h, nq, dim, E_planes, V, bias, targets, tscore, id_stride, id_offset, counts,
+                                  reinterpret_cast<char*>(workspace), (hipStream_t)stream);
+    if (rc != 0) return rc;
+    ASME_LAUNCH_CHECK("asme_catalog_count_above_x6");
+}
+
+// ranks[q] = 1 + #{items scoring above query q's target, or equal with a lower id} over the whole catalogue E
+// (V x dim); E_planes = asme_catalog_split(E) (a catalogue split once for many batches); counts_ws nq int32
+ASME_API int asme_catalog_rank_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const float* E, int64_t ld_e,
+                                  const void* E_planes, int64_t V, const float* bias, const int64_t* targets,
+                                  int32_t* counts_ws, int64_t* ranks, void* workspace, int64_t ws_bytes, void* stream) {
+    ASME_CHECK_ARG(H && E && E_planes && targets && counts_ws && ranks && workspace, "asme_catalog_rank_x6: null pointer");
+    ASME_CHECK_ARG(catalog_shape_ok(dim, ld_h, H) && ld_e % 4 == 0 && aligned16(E) && V >= 1 && V < (1LL << 31) &&
+                       nq < (1LL << 31),
+                   "asme_catalog_rank_x6: dim must be a multiple of 4 in [4, 128], rows 16-B aligned");
+    ASME_CHECK_ARG(ws_bytes >= asme_catalog_x6_workspace(nq, dim), "asme_catalog_rank_x6: workspace too small");
+    if (nq == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    char* w = reinterpret_cast<char*>(workspace);
+    float* rows = reinterpret_cast<float*>(w + 2 * align256(planes_bytes(nq)));
+    float* tbias = reinterpret_cast<float*>(reinterpret_cast<char*>(rows) + align256(nq * kDP * 4));
+    float* tscore = tbias + align256(nq * 4) / 4;
+    const int64_t nt = nq * ((dim + 3) / 4);
+    hipLaunchKernelGGL(gather_targets_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, E, ld_e, V, bias,
+                       targets, nq, (int)dim, rows, tbias);
+    int rc = target_scores_x6(H, ld_h, nq, dim, rows, dim, bias ? tbias : nullptr, tscore, w, s);
+    if (rc == 0)
+        rc = count_above_x6(H, ld_h, nq, dim, E_planes, V, bias, targets, tscore, 1, 0, counts_ws, w, s);
+    if (rc != 0) return rc;
+    hipLaunchKernelGGL(rank_from_counts_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, counts_ws, nq,
+                       ranks);
+    ASME_LAUNCH_CHECK("asme_catalog_rank_x6");
 }

@@ -85,16 +85,24 @@ __device__ __forceinline__ void row_load(const float* __restrict__ p, int sub, i
     }
 }
 
-template <class R>
+// NT: non-temporal (streaming) stores -- rows the next kernels read back from HBM anyway; a 1-read / 2-write row
+// stream runs at 0.89 of 8 TB/s with them vs 0.79 cached (tools/probe/stream_probe.py)
+template <class R, bool NT = false>
 __device__ __forceinline__ void row_store(float* __restrict__ p, int sub, int D, const RowVals<R>& x) {
 #pragma unroll
     for (int j = 0; j < R::NV; ++j) {
         const int c = R::col(sub, j);
         if (c >= D) continue;
-        if constexpr (R::W == 4)
-            *reinterpret_cast<float4*>(p + c) = make_float4(x[j][0], x[j][1], x[j][2], x[j][3]);
-        else
+        if constexpr (R::W == 4) {
+            if constexpr (NT) {
+                typedef float f4 __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(f4{x[j][0], x[j][1], x[j][2], x[j][3]}, reinterpret_cast<f4*>(p + c));
+            } else {
+                *reinterpret_cast<float4*>(p + c) = make_float4(x[j][0], x[j][1], x[j][2], x[j][3]);
+            }
+        } else {
             p[c] = x[j][0];
+        }
     }
 }
 
@@ -125,6 +133,14 @@ __device__ __forceinline__ void row_mul(RowVals<R>& x, const RowVals<R>& f) {
         for (int i = 0; i < R::W; ++i) x[j][i] *= f[j][i];
 }
 
+// v / D: a multiply by the exact reciprocal when D is a power of two (every transformer width here: bit-identical to
+// the division, without the ~10-instruction IEEE divide sequence per statistic per lane -- the row kernels are VALU-
+// bound at 16 lanes per row), else the division
+__device__ __forceinline__ float div_by_width(float v, int D) {
+    return (D & (D - 1)) == 0 ? v * __builtin_bit_cast(float, (127 - (31 - __builtin_clz((unsigned)D))) << 23)
+                              : v / (float)D;
+}
+
 template <class R>
 __device__ __forceinline__ void row_ln_stats(const RowVals<R>& x, int sub, int D, float eps, float& mean,
                                              float& rstd) {
@@ -133,7 +149,7 @@ __device__ __forceinline__ void row_ln_stats(const RowVals<R>& x, int sub, int D
     for (int j = 0; j < R::NV; ++j)
 #pragma unroll
         for (int i = 0; i < R::W; ++i) s += x[j][i];  // out-of-row values are loaded as 0
-    mean = row_sum<R::LPR>(s) / (float)D;
+    mean = div_by_width(row_sum<R::LPR>(s), D);
     float q = 0.f;
 #pragma unroll
     for (int j = 0; j < R::NV; ++j) {
@@ -144,7 +160,7 @@ __device__ __forceinline__ void row_ln_stats(const RowVals<R>& x, int sub, int D
             q += c * c;
         }
     }
-    rstd = rsqrtf(row_sum<R::LPR>(q) / (float)D + eps);
+    rstd = rsqrtf(div_by_width(row_sum<R::LPR>(q), D) + eps);
 }
 
 // xhat = (x - mean) * rstd (0 outside the row)
@@ -187,8 +203,8 @@ __device__ __forceinline__ void row_ln_bwd(const RowVals<R>& gy, const RowVals<R
             a += dxh[j][i];
             b += dxh[j][i] * xh[j][i];
         }
-    a = row_sum<R::LPR>(a) / (float)D;
-    b = row_sum<R::LPR>(b) / (float)D;
+    a = div_by_width(row_sum<R::LPR>(a), D);
+    b = div_by_width(row_sum<R::LPR>(b), D);
 #pragma unroll
     for (int j = 0; j < R::NV; ++j)
 #pragma unroll

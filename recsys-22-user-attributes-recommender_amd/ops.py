@@ -464,6 +464,17 @@ class EmbeddingSpec:
     table_grad: Optional[TableGrad] = None
 
 
+def embedding_keep_chunks(keep: torch.Tensor, D: int) -> torch.Tensor:
+    """the embedding forward's stored keep bytes (T, D/4) in chunk order (byte c: elements 4c..4c+3; bit i: drop1 of
+    element 4c+i, bit 4+i: drop2).  The kernels store a lane's chunks adjacently when the row layout covers the row
+    exactly (csrc/embedding.hip emb_keep_store: D = 128 on 16 lanes x 2 chunks, D = 512 on 64 x 2)"""
+    T = keep.shape[0]
+    lanes = {128: 16, 512: 64}.get(D)
+    if lanes is None:
+        return keep
+    return keep.reshape(T, lanes, 2).transpose(1, 2).reshape(T, D // 4)
+
+
 class _EmbeddingFn(torch.autograd.Function):
     """transformer_layers.py:55-80 (+ kebert4rec/components.py:54-63):
     drop2(LN2(drop1(LN1(E[ids] + P[pos])) + extra))"""
@@ -1610,10 +1621,27 @@ def target_rank(scores: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------------ full-catalogue eval
+def catalog_planes(table: torch.Tensor) -> torch.Tensor:
+    """the exact three-way bf16 split of a (V, d <= 128) catalogue (asme_catalog_split): the streamed operand of the
+    ranking pass; split once and pass to catalog_rank / catalog_count_above to rank many query batches against it"""
+    E = _f32(table)
+    V, d = E.shape
+    planes = torch.empty(int(_lib.load().asme_catalog_planes_bytes(V)), device=E.device, dtype=torch.uint8)
+    call("asme_catalog_split", ptr(E), E.stride(0), V, d, ptr(planes), stream())
+    return planes
+
+
+def _catalog_ws(n: int, d: int, dev) -> Tuple[torch.Tensor, int]:
+    nbytes = int(_lib.load().asme_catalog_x6_workspace(n, d))
+    return torch.empty(nbytes, device=dev, dtype=torch.uint8), nbytes
+
+
 def catalog_rank(hidden: torch.Tensor, table: torch.Tensor, targets: torch.Tensor,
-                 bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 bias: Optional[torch.Tensor] = None, planes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Rank (1-based, ties to the lower id) of each row's target among all |V| items scored as
-    hidden . table^T (+ bias) -- the (rows, |V|) logits are never materialised (asme_catalog_rank).
+    hidden . table^T (+ bias) -- the (rows, |V|) logits are never materialised (asme_catalog_rank_x6: the bf16x6
+    score products asme_logits materialises, so the ranks are those of the materialised scores).  `planes`: a
+    catalog_planes(table) split made earlier (else the table is split here).
     Reference: SASRecProjectionComponent inference + AllItemsSampler + argsort (sasrec/components.py:46-61,
     metrics/common.py:4-27)."""
     h = _f32(hidden)
@@ -1623,8 +1651,11 @@ def catalog_rank(hidden: torch.Tensor, table: torch.Tensor, targets: torch.Tenso
     tg = _i64(targets).reshape(n)
     counts = torch.empty(n, device=h.device, dtype=torch.int32)
     ranks = torch.empty(n, device=h.device, dtype=torch.int64)
-    call("asme_catalog_rank", ptr(h), h.stride(0), n, d, ptr(E), E.stride(0), V,
-         ptr(_f32(bias)) if bias is not None else None, ptr(tg), ptr(counts), ptr(ranks), stream())
+    if planes is None:
+        planes = catalog_planes(E)
+    ws, nbytes = _catalog_ws(n, d, h.device)
+    call("asme_catalog_rank_x6", ptr(h), h.stride(0), n, d, ptr(E), E.stride(0), ptr(planes), V,
+         ptr(_f32(bias)) if bias is not None else None, ptr(tg), ptr(counts), ptr(ranks), ptr(ws), nbytes, stream())
     return ranks
 
 
@@ -1648,24 +1679,29 @@ def catalog_topk(hidden: torch.Tensor, table: torch.Tensor, k: int, bias: Option
 
 def catalog_target_scores(hidden: torch.Tensor, target_rows: torch.Tensor,
                           target_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """score of each row's target from its gathered table row, computed by the same MFMA sequence as the
-    shard scan (so the owner's scan compares bit-identically against it)."""
+    """score of each row's target from its gathered table row, by the same products as the shard scan
+    (asme_catalog_target_scores_x6: the owner's scan compares bit-identically against it)."""
     h, rows = _f32(hidden), _f32(target_rows)
     n, d = h.shape
     out = torch.empty(n, device=h.device, dtype=torch.float32)
-    call("asme_catalog_target_scores", ptr(h), h.stride(0), n, d, ptr(rows), rows.stride(0),
-         ptr(_f32(target_bias)) if target_bias is not None else None, ptr(out), stream())
+    ws, nbytes = _catalog_ws(n, d, h.device)
+    call("asme_catalog_target_scores_x6", ptr(h), h.stride(0), n, d, ptr(rows), rows.stride(0),
+         ptr(_f32(target_bias)) if target_bias is not None else None, ptr(out), ptr(ws), nbytes, stream())
     return out
 
 
 def catalog_count_above(hidden: torch.Tensor, table_shard: torch.Tensor, targets: torch.Tensor,
                         target_scores: torch.Tensor, id_stride: int, id_offset: int,
-                        bias_shard: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """#items of this table shard (local row j = item j*id_stride + id_offset) ranked above each row's target."""
+                        bias_shard: Optional[torch.Tensor] = None, planes: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """#items of this table shard (local row j = item j*id_stride + id_offset) ranked above each row's target
+    (asme_catalog_count_above_x6; `planes`: catalog_planes(table_shard) made earlier)."""
     h, E = _f32(hidden), _f32(table_shard)
     n, d = h.shape
     counts = torch.empty(n, device=h.device, dtype=torch.int32)
-    call("asme_catalog_count_above", ptr(h), h.stride(0), n, d, ptr(E), E.stride(0), E.shape[0],
+    if planes is None:
+        planes = catalog_planes(E)
+    ws, nbytes = _catalog_ws(n, d, h.device)
+    call("asme_catalog_count_above_x6", ptr(h), h.stride(0), n, d, ptr(planes), E.shape[0],
          ptr(_f32(bias_shard)) if bias_shard is not None else None, ptr(_i64(targets).reshape(n)),
-         ptr(_f32(target_scores)), id_stride, id_offset, ptr(counts), stream())
+         ptr(_f32(target_scores)), id_stride, id_offset, ptr(counts), ptr(ws), nbytes, stream())
     return counts

@@ -139,3 +139,32 @@ def test_catalog_rank_and_topk_at_ten_million_items(asme, dev):
     assert bool((s_idx >= best_v[:, -1:] - e_idx - best_e[:, -1:]).all())
     assert bool((idx >= 0).all()) and bool((idx < V).all())
     assert all(len(set(r)) == k for r in idx.tolist())
+
+
+@pytest.mark.parametrize("nq,V,d,with_bias", [(300, 5003, 128, True), (1024, 27003, 128, False), (37, 999, 64, True)])
+def test_catalog_rank_equals_rank_of_materialised_scores(asme, dev, nq, V, d, with_bias):
+    """asme_catalog_rank_x6 (bf16x6 scores streamed, never stored) == the rank read off asme_logits' materialised
+    scores (the same products): 1 + #{s > s_t} + #{s == s_t, id < t}, exactly; a catalogue split once
+    (ops.catalog_planes) and reused gives the same ranks"""
+    torch.manual_seed(nq + V)
+    H = torch.randn(nq, d, device=dev)
+    E = torch.randn(V, d, device=dev) / d ** 0.5
+    b = torch.randn(V, device=dev) if with_bias else None
+    targets = torch.randint(0, V, (nq,), device=dev)
+    ranks = asme.ops.catalog_rank(H, E, targets, b)
+    with torch.no_grad():
+        S = asme.ops.logits(H, E, b)
+    st = S.gather(1, targets[:, None])
+    ids = torch.arange(V, device=dev)[None, :]
+    want = 1 + ((S > st) | ((S == st) & (ids < targets[:, None]))).sum(1)
+    assert torch.equal(ranks, want)
+    planes = asme.ops.catalog_planes(E)
+    assert torch.equal(asme.ops.catalog_rank(H, E, targets, b, planes=planes), want)
+    # ties: duplicated item rows score identically; the lower id ranks first
+    E2 = E.clone()
+    E2[1::2] = E2[0::2][: E2[1::2].shape[0]]
+    r2 = asme.ops.catalog_rank(H, E2, targets, None)
+    S2 = asme.ops.logits(H, E2, None)
+    st2 = S2.gather(1, targets[:, None])
+    want2 = 1 + ((S2 > st2) | ((S2 == st2) & (ids < targets[:, None]))).sum(1)
+    assert torch.equal(r2, want2)

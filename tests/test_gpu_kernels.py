@@ -157,7 +157,7 @@ def test_embedding_dropout_keep_mask(asme, dev, D, L, p1, p2):
     gpu = [t.to(dev).clone().requires_grad_(True) for t in (E, P, w1, b1, w2, b2)]
     spec = asme.ops.EmbeddingSpec(seq_len=L, p1=p1, p2=p2)
     yd = asme.ops.embedding(ids.to(dev), gpu[0], gpu[1], (gpu[2], gpu[3]), None, (gpu[4], gpu[5]), spec)
-    keep = yd.grad_fn.saved_tensors[-1].cpu().to(torch.int64)          # (T, D/4) bytes
+    keep = asme.ops.embedding_keep_chunks(yd.grad_fn.saved_tensors[-1], D).cpu().to(torch.int64)  # (T, D/4)
     bits = (keep.unsqueeze(-1) >> torch.arange(8)) & 1                  # (T, D/4, 8)
     k1 = bits[..., :4].reshape(B, L, D).float()
     k2 = bits[..., 4:].reshape(B, L, D).float()

@@ -9,11 +9,13 @@ fi
 for i in $(seq ${ROUNDS:-2}); do
  for lib in recsys-22-user-attributes-recommender_amd/libasme_mi.so ${VARIANTS:-}; do
   ASME_MI_LIB=$lib timeout -k 10 200 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --full-json gpurun_out/bab_full.json ${BENCH_ARGS:-} > gpurun_out/bab.log 2>&1 || exit 1
-  python - "$lib" <<'P'
+  python - "$lib" ${KERNELS:-} <<'P'
 import json, sys
 j = json.load(open("gpurun_out/bab_full.json"))
 ks = {r["kernel"]: r["avg_ms"] for r in j.get("rooflines", [])}
-print(sys.argv[1].split("/")[-1], j["value"], j["ms_per_step"], "flush", j.get("flush_ms"), "stage", ks.get("asme_lazy_adam_stage"))
+keys = ["asme_lazy_adam_stage", "asme_embedding_ln_fwd", "asme_embedding_ln_bwd"] + sys.argv[2:]
+print(sys.argv[1].split("/")[-1], j["value"], j["ms_per_step"], "flush", j.get("flush_ms"),
+      " ".join(f"{k.replace('asme_', '')}={ks.get(k)}" for k in keys))
 P
  done
 done
