@@ -73,7 +73,8 @@ __device__ __forceinline__ uint8_t keep_bits(const float4& f) {
 }
 __device__ __forceinline__ float4 bits_keep(uint8_t m, float p) {
     const float k = 1.f / (1.f - p);
-    return make_float4(m & 1 ? k : 0.f, m & 2 ? k : 0.f, m & 4 ? k : 0.f, m & 8 ? k : 0.f);
+    return make_float4(keep_factor_bit(m, 0, k), keep_factor_bit(m, 1, k), keep_factor_bit(m, 2, k),
+                       keep_factor_bit(m, 3, k));
 }
 // A second copy serves the dK/dV pass, whose lanes own keys: u16 words [B*H][ceil(L/16) query groups]
 // [4*ceil(L/4) keys], bit i of word (j, key) = query 16j+i kept.  It follows the nibble image, 256-B aligned.
@@ -589,6 +590,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
 // per-tile barriers, each K/V row is read from HBM once per head (not once per 64-query block), and
 // fully-masked 16-key sub-tiles are skipped.  Used when 2 * ceil(L/16)*16 * (dk+4) * 4 B fits the
 // 160 KiB LDS (L <= 300 at dk = 64); the streaming kernels above cover the rest.
+#ifndef ASME_ATTN_DIAG
+#define ASME_ATTN_DIAG 0  // diagnostic builds only: 1 = the resident kernels skip their per-head operand loads
+#endif
 #ifndef ASME_RES_THREADS
 #define ASME_RES_THREADS 768  // 12 waves: 3 per SIMD (512: 245/605 us fwd/bwd, 768: 231/588)
 #endif
@@ -687,7 +691,8 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
     const float* qh = q + tok0 * ldq + h * DK;
 
     stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
-    load_pair_resident<DK>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks, Vs);
+    if (ASME_ATTN_DIAG != 1)
+        load_pair_resident<DK>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks, Vs);
     __syncthreads();
     const int last_valid = ctl[0];
     const bool any_valid = last_valid >= 0;
@@ -818,7 +823,8 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dq_res_kernel(
     const int64_t tok0 = (int64_t)b * L;
 
     stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
-    load_pair_resident<DK>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks, Vs);
+    if (ASME_ATTN_DIAG != 1)
+        load_pair_resident<DK>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks, Vs);
     __syncthreads();
     const int last_valid = ctl[0];
     const bool any_valid = last_valid >= 0;
@@ -926,8 +932,9 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
     const int64_t tok0 = (int64_t)b * L;
 
     stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
-    load_pair_resident<DK, kResThreadsKV>(q + tok0 * ldq + h * DK, ldq, dout + tok0 * lddo + h * DK, lddo, L, Lp, Qs,
-                                          Ds);
+    if (ASME_ATTN_DIAG != 1)
+        load_pair_resident<DK, kResThreadsKV>(q + tok0 * ldq + h * DK, ldq, dout + tok0 * lddo + h * DK, lddo, L, Lp,
+                                              Qs, Ds);
     for (int i = threadIdx.x; i < Lp; i += kResThreadsKV) {
         const bool ok = i < L;
         mx_s[i] = ok ? stats[((int64_t)bh * L + i) * 2] : 0.f;
@@ -935,7 +942,7 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
         if (!DS) dsum_s[i] = ok ? dsum[(int64_t)bh * L + i] : 0.f;
     }
     __syncthreads();
-    if (DS) {
+    if (DS && ASME_ATTN_DIAG != 1) {
         // D_i = dO_i . O_i: 16 lanes per query row (a float4 of features each, dO from the LDS image); a thread's
         // O loads for four rows are all issued before the first is used (one round trip per four rows: a dependent
         // load per row cost ~2 us each in this prologue, which nothing overlaps at one workgroup per CU)

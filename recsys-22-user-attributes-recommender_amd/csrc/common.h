@@ -108,9 +108,14 @@ __device__ __forceinline__ uint32_t gelu_keep_bits8(uint64_t seed, uint64_t chun
 __device__ __forceinline__ uint32_t gelu_keep_bits4(uint64_t seed, uint64_t chunk, uint32_t thr) {
     return (gelu_keep_bits8(seed, chunk, thr) >> (((uint32_t)(chunk >> 2) & 1u) * 4u)) & 0xFu;
 }
+// keep bit b of `bits` -> the factor k (kept) or +0 (dropped): the sign-extended one-bit field (v_bfe_i32: 0 or -1)
+// ANDed with k's bits -- two VALU instead of extract, compare and select; x * factor is the same value either way
+__device__ __forceinline__ float keep_factor_bit(uint32_t bits, int b, float k) {
+    return __int_as_float(__builtin_amdgcn_sbfe((int)bits, (unsigned)b, 1u) & __float_as_int(k));
+}
 __device__ __forceinline__ void gelu_keep_factors(uint32_t bits4, float k, float (&u)[4]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = (bits4 >> i) & 1u ? k : 0.f;
+    for (int i = 0; i < 4; ++i) u[i] = keep_factor_bit(bits4, i, k);
 }
 __device__ __forceinline__ float gelu_keep_factor(uint64_t seed, uint64_t idx, float p) {
     return (gelu_keep_bits4(seed, idx >> 2, gelu_thresh(p)) >> (idx & 3)) & 1u ? 1.0f / (1.0f - p) : 0.0f;

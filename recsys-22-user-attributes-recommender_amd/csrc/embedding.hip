@@ -196,6 +196,7 @@ __device__ __forceinline__ uint32_t emb_keep_bits(uint64_t seed, uint64_t chunk,
 
 __host__ __device__ inline uint64_t emb_seed(uint64_t s1, uint64_t s2) { return s1 ^ (s2 * 0x9E3779B97F4A7C15ull); }
 
+
 // Keep bytes of token t: (T, D/4) bytes.  When the row layout covers the row exactly (LPR * NV * 4 == D: D = 128 on
 // 16 lanes x 2 chunks, D = 512 on 64 x 2, and every one-chunk layout) a lane's NV bytes are adjacent -- byte
 // sub * NV + j holds chunk sub + LPR * j -- so each lane stores / loads them as ONE 8- or 16-bit access per token
@@ -366,7 +367,7 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
                                 : 0u;
                 if (p1 > 0.f)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
+                    for (int i = 0; i < 4; ++i) x[k][j][i] *= keep_factor_bit(bits[j], i, k1);
             }
         }
         if (extra)
@@ -387,7 +388,7 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
+                    for (int i = 0; i < 4; ++i) x[k][j][i] *= keep_factor_bit(bits[j], 4 + i, k2);
             if (keep) emb_keep_store<R>(keep, t, sub, D, bits);
         }
         row_store<R, ASME_EMB_NT>(out + t * D, sub, D, x[k]);
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) x[k][j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
+                    for (int i = 0; i < 4; ++i) x[k][j][i] *= keep_factor_bit(bits[j], i, k1);
             if (LN2) {
                 if (extra && live) {
                     row_load<R>(extra + t * D, sub, D, q[k]);
@@ -561,7 +562,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
 #pragma unroll
                     for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) xo[j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
+                        for (int i = 0; i < 4; ++i) xo[j][i] *= keep_factor_bit(bits[j], 4 + i, k2);
                 row_normalise<R>(xo, sub, D, st3[k].x, st3[k].y, xh3);
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
@@ -580,7 +581,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) g[k][j][i] *= (bits[j] >> (4 + i)) & 1u ? k2 : 0.f;
+                    for (int i = 0; i < 4; ++i) g[k][j][i] *= keep_factor_bit(bits[j], 4 + i, k2);
             RowVals<R> gz;
             if (LN2) {
 #pragma unroll
@@ -602,7 +603,7 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) gz[j][i] *= (bits[j] >> i) & 1u ? k1 : 0.f;
+                    for (int i = 0; i < 4; ++i) gz[j][i] *= keep_factor_bit(bits[j], i, k1);
             if (w1) {
 #pragma unroll
                 for (int j = 0; j < R::NV; ++j)
