@@ -87,7 +87,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
 
 // X: M x K row-major.  TRANS = false: W is N x K (nn.Linear.weight), Y = X W^T.  TRANS = true: W is K x N
 // (the input gradient dX = dY W of a layer whose weight is N_out x N_in = K x N).
-template <int K, int CT, bool TRANS, int EPI>
+// XP: X arrives already split into its three bf16 planes ([3][M][ldx] bf16, written by its producer): the ring holds
+// the planes and the loop issues no split VALU (an experiment: asme_ws_linear_planes)
+template <int K, int CT, bool TRANS, int EPI, bool XP = false>
 __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ws_gemm_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W, int N, float* __restrict__ Y, WsEpi ep) {
     constexpr int NB = 16 * CT;  // output features per workgroup
@@ -150,7 +152,35 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const int64_t t0 = lo + widx;
     auto xrow = [&](int64_t j) -> const float* {  // clamped rows are computed and dropped at the store
         int64_t m = (t0 + (j < my_tiles ? j : my_tiles - 1) * wcount) * 16 + c16;
-        return X + (m < M ? m : M - 1) * ep.ldx + ep.kofs + 8 * g;
+        // (XP: the same element offset into the h plane, as a float pointer of half the distance)
+        return XP ? reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(X) +
+                                                   (m < M ? m : M - 1) * ep.ldx + ep.kofs + 8 * g)
+                  : X + (m < M ? m : M - 1) * ep.ldx + ep.kofs + 8 * g;
+    };
+    const int64_t pl_bytes = M * ep.ldx * 2;  // XP: bytes between the planes
+    // k32 block d of X at row pointer r: fp32 (two float4) or the three planes' 16 B
+    auto xload = [&](const float* rp, int d, float4& a, float4& b, float4& c) {
+        if constexpr (XP) {
+            const char* pb = reinterpret_cast<const char*>(rp) + d * 64;
+            a = *reinterpret_cast<const float4*>(pb);
+            b = *reinterpret_cast<const float4*>(pb + pl_bytes);
+            c = *reinterpret_cast<const float4*>(pb + 2 * pl_bytes);
+        } else {
+            a = *reinterpret_cast<const float4*>(rp + d * 32);
+            b = *reinterpret_cast<const float4*>(rp + d * 32 + 4);
+        }
+    };
+    auto xsplit = [&](const float4& a, const float4& b, const float4& c) -> Bf3 {
+        if constexpr (XP) {
+            Bf3 r;
+            r.h = __builtin_bit_cast(bf16x8, a);
+            r.m = __builtin_bit_cast(bf16x8, b);
+            r.l = __builtin_bit_cast(bf16x8, c);
+            return r;
+        } else {
+            (void)c;
+            return split_bf3(a, b);
+        }
     };
     const __amdgpu_buffer_rsrc_t yr = rsrc(Y, M * N * 4);
     const bool nt_out = N >= kNtMinN;
@@ -175,10 +205,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const float* rc = xrow(0);
     const float* rn = xrow(1);
     float4 ring[2 * RD];  // k32 block d of X: ring[2d] (k 8g..8g+3), ring[2d + 1] (k 8g+4..8g+7)
+    float4 ring3[XP ? RD : 1];  // XP: the l plane of block d (ring[2d] = h, ring[2d + 1] = m)
 #pragma unroll
     for (int d = 0; d < RD; ++d) {
-        ring[2 * d] = *reinterpret_cast<const float4*>(rc + d * 32);
-        ring[2 * d + 1] = *reinterpret_cast<const float4*>(rc + d * 32 + 4);
+        xload(rc, d, ring[2 * d], ring[2 * d + 1], ring3[XP ? d : 0]);
         __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's vmcnt waits assume it
     }
     float4 stash[CT], pre[CT];
@@ -207,7 +237,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     Bf3 wc[WR];  // wc[ct % WR] holds tile ct's fragment of the current block when its MFMAs run
 #pragma unroll
     for (int ct = 0; ct < WR; ++ct) wc[ct] = wload(ct, 0);
-    Bf3 xs = split_bf3(ring[0], ring[1]);
+    Bf3 xs = xsplit(ring[0], ring[1], ring3[0]);
     // the stashed tile's epilogue for one 16-feature tile
     auto epilogue = [&](int ct) {
         if constexpr (kStage) {
@@ -308,16 +338,15 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             }
             // refill the slot just consumed: block kb + RD of this tile or of the next one (unconditional,
             // so the vmcnt bookkeeping stays exact; past the last tile it re-reads the last one)
-            const float* src = (kb + RD < NKB ? rc : rn) + ((kb + RD) % NKB) * 32;
+            const float* src = kb + RD < NKB ? rc : rn;
 #if ASME_WS_DIAG != 4
-            ring[2 * d] = *reinterpret_cast<const float4*>(src);
-            ring[2 * d + 1] = *reinterpret_cast<const float4*>(src + 4);
+            xload(src, (kb + RD) % NKB, ring[2 * d], ring[2 * d + 1], ring3[XP ? d : 0]);
 #else
             ring[2 * d].x += (float)(uintptr_t)src;
 #endif
             // the next block's X terms
             const int dn = (kb + 1) % RD;
-            xs = split_bf3(ring[2 * dn], ring[2 * dn + 1]);
+            xs = xsplit(ring[2 * dn], ring[2 * dn + 1], ring3[XP ? dn : 0]);
             // the previous tile's epilogue, spread over the blocks (late in the tile, so the pre-activation
             // loads WS_GELU_BWD issued at the tile boundary have landed)
 #pragma unroll
@@ -353,14 +382,14 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     for (int ct = 0; ct < CT; ++ct) epilogue(ct);  // the last tile
 }
 
-template <int K, int CT, bool TRANS, int EPI>
+template <int K, int CT, bool TRANS, int EPI, bool XP = false>
 int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
     constexpr int NB = 16 * CT;
     const size_t planes = (size_t)NB * K * 6;  // three bf16 planes
     const size_t stage = (size_t)kWaves * 16 * (CT == 8 ? NB : NB + 4) * 4;  // (the kernel's SROW)
     const size_t lds = planes + (CT >= 4 && planes + stage <= (size_t)kLdsMax ? stage : 0);
     // opt in above 64 KiB of dynamic LDS once per instantiation (a function-local static: thread-safe initialisation)
-    static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI>,
+    static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI, XP>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return hip_status(attr, "asme_ws_linear: LDS opt-in");
     int dev = 0, cus = 256;
@@ -372,8 +401,8 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
         set_error("asme_ws_linear: more feature blocks than workgroups per XCD for this epilogue");
         return -1;
     }
-    hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M, W,
-                       N, Y, ep);
+    hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI, XP>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M,
+                       W, N, Y, ep);
     return hip_status(hipGetLastError(), "asme_ws_linear");
 }
 
@@ -470,4 +499,46 @@ ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W
     if (epi == 0) return dispatch_k<false, WS_STORE>((int)K, ct, X, M, W, (int)N, Y, ep, s);
     if (epi == 1) return dispatch_k<false, WS_GELU_DROP>((int)K, ct, X, M, W, (int)N, Y, ep, s);
     return dispatch_k<false, WS_GELU_BWD>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+}
+
+// ---- experiment: X pre-split into its bf16 planes by its producer
+namespace {
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ X, int64_t n8, int64_t plane,
+                                                         __bf16* __restrict__ P) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per 8 elements
+    if (t >= n8) return;
+    const Bf3 b = split_bf3(*reinterpret_cast<const float4*>(X + 8 * t), *reinterpret_cast<const float4*>(X + 8 * t + 4));
+    *reinterpret_cast<bf16x8*>(P + 8 * t) = b.h;
+    *reinterpret_cast<bf16x8*>(P + plane + 8 * t) = b.m;
+    *reinterpret_cast<bf16x8*>(P + 2 * plane + 8 * t) = b.l;
+}
+}  // namespace
+
+// planes [3][M][K] bf16 = the exact split of X (M x K, contiguous); the standalone form of what a producer's epilogue
+// would write
+ASME_API int asme_ws_split_planes(const float* X, int64_t M, int64_t K, void* planes, void* stream) {
+    ASME_CHECK_ARG(X && planes && K % 8 == 0, "asme_ws_split_planes: bad arguments");
+    const int64_t n8 = M * K / 8;
+    hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, X, n8,
+                       M * K, reinterpret_cast<__bf16*>(planes));
+    ASME_LAUNCH_CHECK("asme_ws_split_planes");
+}
+
+// asme_ws_linear (trans = 0, K = 128, epilogue 0 or 1) reading X as its three bf16 planes ([3][M][128])
+ASME_API int asme_ws_linear_planes(const void* Xp, int64_t M, int64_t K, const float* W, int64_t N, const float* bias,
+                                   int epi, float* pre_out, float p, uint64_t seed, float* Y, void* stream) {
+    ASME_CHECK_ARG(Xp && W && Y && K == 128 && (epi == 0 || epi == 1) && asme_ws_linear_supported(M, K, N),
+                   "asme_ws_linear_planes: unsupported");
+    const WsEpi ep{bias, pre_out, nullptr, p, seed, K, K, 0};
+    const int ct = pick_ct((int)N, (int)K);
+    hipStream_t s = (hipStream_t)stream;
+    const float* X = reinterpret_cast<const float*>(Xp);
+    if (epi == 1) {
+        if (ct == 8) return launch_ws<128, 8, false, WS_GELU_DROP, true>(X, M, W, (int)N, Y, ep, s);
+        if (ct == 6) return launch_ws<128, 6, false, WS_GELU_DROP, true>(X, M, W, (int)N, Y, ep, s);
+        return launch_ws<128, 4, false, WS_GELU_DROP, true>(X, M, W, (int)N, Y, ep, s);
+    }
+    if (ct == 8) return launch_ws<128, 8, false, WS_STORE, true>(X, M, W, (int)N, Y, ep, s);
+    if (ct == 6) return launch_ws<128, 6, false, WS_STORE, true>(X, M, W, (int)N, Y, ep, s);
+    return launch_ws<128, 4, false, WS_STORE, true>(X, M, W, (int)N, Y, ep, s);
 }

@@ -3,10 +3,12 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp
 TAG=${TAG:-r3z}; OUT=gpurun_out/final_${TAG}; mkdir -p $OUT
+if [ "${BENCH:-1}" != "0" ]; then
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
 tail -1 $OUT/bench.json | python -c "import json,sys; r=json.loads(sys.stdin.read()); print(r['value'], r['ms_per_step'], [(w, x['value']) for w, x in r.get('workloads', {}).items()])"
+fi
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "ws_gemm|weight_grad|attn|sum_slabs" \
-    -d $OUT/mfma -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --cpu-baseline 0 --legs none \
+    -d $OUT/mfma -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --cpu-baseline 0 --legs none --eval-steps 0 \
     --kernel-events off > $OUT/mfma.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "logits_engine|logits_grad|fdh_finish|scale_rows|lce_" \
     -d $OUT/mfma_b4r -o run --output-format csv -- python bench.py --workload bert4rec --items 27000 --steps 2 --warmup 1 \

@@ -14,10 +14,10 @@ for W in ${WORKLOADS:-sasrec-neg bert4rec kebert4rec}; do
   OUT=gpurun_out/pmc_${TAG}/$W
   mkdir -p $OUT
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- \
-      python bench.py $ARGS --steps 5 --warmup 2 --cpu-baseline 0 --legs none > $OUT/kt.log 2>&1 || exit $?
+      python bench.py $ARGS --steps 5 --warmup 2 --cpu-baseline 0 --legs none --eval-steps 0 > $OUT/kt.log 2>&1 || exit $?
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "$RX" -d $OUT/pmc_$C -o run --output-format csv -- \
-        python bench.py $ARGS --steps 2 --warmup 1 --cpu-baseline 0 --legs none --kernel-events off > $OUT/pmc_$C.log 2>&1 || exit $?
+        python bench.py $ARGS --steps 2 --warmup 1 --cpu-baseline 0 --legs none --eval-steps 0 --kernel-events off > $OUT/pmc_$C.log 2>&1 || exit $?
   done
   echo "$W done"
 done
