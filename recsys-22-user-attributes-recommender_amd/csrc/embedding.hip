@@ -207,11 +207,20 @@ __device__ __forceinline__ bool emb_keep_packed(int D) { return R::LPR * R::NV *
 // the 16-lane, two-chunk layout is taken for D = 128 only (with_emb_layout): there the width is a compile-time
 // constant, so the column bounds checks and the 1 / D of the statistics fold away
 template <class R>
-__device__ __forceinline__ int emb_width(int D) { return (R::LPR == 16 && R::NV == 2) ? 128 : D; }
+__device__ __forceinline__ int emb_width(int D) {
+    return ((R::LPR == 16 && R::NV == 2) || (R::LPR == 8 && R::NV == 4)) ? 128 : D;
+}
 template <class R>
 __device__ __forceinline__ void emb_keep_store(uint8_t* __restrict__ keep, int64_t t, int sub, int D,
                                                const uint32_t (&bits)[R::NV]) {
     uint8_t* row = keep + (uint64_t)t * (D >> 2);
+    if constexpr (R::LPR == 8 && R::NV == 4) {
+        // D = 128 on 8 lanes x 4 chunks (chunks sub + 8j): the bytes of the 16-lane layout -- 16-bit word w holds
+        // chunks w and w + 16 -- so the backward (16 lanes) reads them as it always does
+        *reinterpret_cast<uint16_t*>(row + sub * 2) = (uint16_t)(bits[0] | (bits[2] << 8));
+        *reinterpret_cast<uint16_t*>(row + (sub + 8) * 2) = (uint16_t)(bits[1] | (bits[3] << 8));
+        return;
+    }
     if (emb_keep_packed<R>(D)) {
         if constexpr (R::NV == 2) {
             *reinterpret_cast<uint16_t*>(row + sub * 2) = (uint16_t)(bits[0] | (bits[1] << 8));
@@ -293,11 +302,20 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
 #if ASME_EMB_FWD_HOIST
     // LN3's w / b staged in LDS with the id loads in flight, instead of a global round trip (which also waits for the
     // output row stores: vmcnt counts stores) between the first token's stores and its LN3 affine
-    __shared__ __attribute__((aligned(16))) float prm3[2][512];
-    if constexpr (LN3) {
+    // (the 8-lane layout keeps LN1 / LN2's w / b here too: rows 2-5)
+    __shared__ __attribute__((aligned(16))) float prm3[R::NV >= 4 ? 6 : 2][512];
+    if constexpr (LN3 || R::NV >= 4) {
         for (int e = threadIdx.x; e < D; e += blockDim.x) {
-            prm3[0][e] = l3.w[e];
-            prm3[1][e] = l3.b[e];
+            if (LN3) {
+                prm3[0][e] = l3.w[e];
+                prm3[1][e] = l3.b[e];
+            }
+            if constexpr (R::NV >= 4) {
+                prm3[2][e] = w1 ? w1[e] : 0.f;
+                prm3[3][e] = w1 ? b1[e] : 0.f;
+                prm3[4][e] = (LN2 && w2) ? w2[e] : 0.f;
+                prm3[5][e] = (LN2 && w2) ? b2[e] : 0.f;
+            }
         }
         __syncthreads();
     }
@@ -332,13 +350,16 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
                 for (int i = 0; i < 4; ++i) x[k][j][i] += q[k][j][i];
     }
     RowVals<R> w1v, b1v, w2v, b2v;
-    if (w1) {
-        row_load<R>(w1, sub, D, w1v);
-        row_load<R>(b1, sub, D, b1v);
-    }
-    if (LN2 && w2) {
-        row_load<R>(w2, sub, D, w2v);
-        row_load<R>(b2, sub, D, b2v);
+    constexpr bool kPrmLds = R::NV >= 4;  // 16 values per lane: LN1 / LN2 read from LDS where they are used
+    if (!kPrmLds) {
+        if (w1) {
+            row_load<R>(w1, sub, D, w1v);
+            row_load<R>(b1, sub, D, b1v);
+        }
+        if (LN2 && w2) {
+            row_load<R>(w2, sub, D, w2v);
+            row_load<R>(b2, sub, D, b2v);
+        }
     }
     const bool drop = p1 > 0.f || p2 > 0.f;
     const uint32_t th1 = emb_thresh(p1), th2 = emb_thresh(p2);
@@ -353,10 +374,14 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
         if (w1) {
             if (ASME_EMB_DIAG != 1) row_ln_stats<R>(x[k], sub, D, eps1, m1, r1);
             row_normalise<R>(x[k], sub, D, m1, r1, tmp);
+            if constexpr (kPrmLds) {
+                row_affine<R>(tmp, sub, D, prm3[2], prm3[3], x[k]);
+            } else {
 #pragma unroll
-            for (int j = 0; j < R::NV; ++j)
+                for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) x[k][j][i] = tmp[j][i] * w1v[j][i] + b1v[j][i];
+                    for (int i = 0; i < 4; ++i) x[k][j][i] = tmp[j][i] * w1v[j][i] + b1v[j][i];
+            }
         }
         uint32_t bits[R::NV];
         if (drop) {
@@ -378,10 +403,14 @@ __global__ __launch_bounds__(256) void emb_fwd4_kernel(
         if (LN2 && w2) {
             if (ASME_EMB_DIAG != 1) row_ln_stats<R>(x[k], sub, D, eps2, m2, r2);
             row_normalise<R>(x[k], sub, D, m2, r2, tmp);
+            if constexpr (kPrmLds) {
+                row_affine<R>(tmp, sub, D, prm3[4], prm3[5], x[k]);
+            } else {
 #pragma unroll
-            for (int j = 0; j < R::NV; ++j)
+                for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) x[k][j][i] = tmp[j][i] * w2v[j][i] + b2v[j][i];
+                    for (int i = 0; i < 4; ++i) x[k][j][i] = tmp[j][i] * w2v[j][i] + b2v[j][i];
+            }
         }
         if (drop) {
             if (p2 > 0.f)
@@ -844,6 +873,11 @@ int with_emb_layout(int64_t D, F&& f, bool lpr16 = ASME_EMB_LPR16) {
 }
 
 namespace {
+// the forward at D = 128 on 8 lanes per row (16 values per lane): the per-row work every lane of a row repeats --
+// statistics reductions, rsqrt, addressing, ids, stores of statistics -- runs on half as many lanes
+#ifndef ASME_EMB_FWD_LPR8
+#define ASME_EMB_FWD_LPR8 1
+#endif
 int embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const float* table, int64_t vocab,
                   int64_t dim, const float* pos_table, const float* ln1_w, const float* ln1_b, float ln1_eps, float p1,
                   uint64_t seed1, const float* extra, const float* ln2_w, const float* ln2_b, float ln2_eps, float p2,
@@ -853,7 +887,7 @@ int embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const f
     ASME_CHECK_ARG(dim >= 1 && dim <= 512 && seq_len >= 1 && n_tokens >= 0, "asme_embedding_fwd: bad shape");
     ASME_CHECK_ARG(p1 >= 0.f && p1 < 1.f && p2 >= 0.f && p2 < 1.f, "asme_embedding_fwd: dropout p must be in [0,1)");
     if (n_tokens == 0) return 0;
-    if (with_emb_layout(dim, [&](auto layout) {
+    auto body = [&](auto layout) {
             using R = decltype(layout);
             if constexpr (R::W == 4) {
                 constexpr int K = ASME_EMB_K;  // tokens per lane group
@@ -880,7 +914,10 @@ int embedding_fwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const f
                                    ln1_w, ln1_b, ln1_eps, p1, seed1, extra, ln2_w, ln2_b, ln2_eps, p2, seed2, out,
                                    stats, err_flag);
             }
-        }))
+        };
+    if (ASME_EMB_FWD_LPR8 && dim == 128)
+        body(RowLayout<4, 8, 4>{});
+    else if (with_emb_layout(dim, body))
         return -1;
     ASME_LAUNCH_CHECK("asme_embedding_fwd");
 }

@@ -141,7 +141,31 @@ struct LogitsArgs {
     const float* tscore;     // rank: the target's score per query (from the tscore pass: the same products)
     int32_t* counts;         // rank: per query, items ranked above the target (atomically summed over chunks)
     int64_t id_stride, id_offset;
+    int64_t sblocks, per_xcd;  // set by launch_engine: the grid's work items and work items per XCD slot group
 };
+
+// workgroup -> (chunk, stationary block), chunk-major within an XCD.  Workgroups b, b + 8, b + 16, ... share an XCD
+// (the dispatcher deals them round-robin; a speed assumption only -- any placement gives the same results), so slot
+// group b % 8 takes the contiguous run [(b % 8) per_xcd, (b % 8 + 1) per_xcd) of the chunk-major work list: the CUs
+// of one XCD stream the same chunk's tiles at about the same time and keep one copy of them in that XCD's L2 (with
+// chunk = b % nchunks every XCD streamed every chunk whenever nchunks was not a multiple of 8).  The grid's few
+// padding workgroups (w >= sblocks x nchunks) return before touching anything.
+#ifndef ASME_LOGITS_XCD
+#define ASME_LOGITS_XCD 1  // 0: chunk = b % nchunks (the round-4 mapping, for A/B)
+#endif
+__device__ __forceinline__ bool work_item(const LogitsArgs& a, int& chunk_id, int64_t& sblock) {
+    if (!ASME_LOGITS_XCD) {
+        if (blockIdx.x >= a.sblocks * a.nchunks) return false;
+        chunk_id = (int)(blockIdx.x % (unsigned)a.nchunks);
+        sblock = blockIdx.x / (unsigned)a.nchunks;
+        return true;
+    }
+    const int64_t w = (int64_t)(blockIdx.x & 7u) * a.per_xcd + (blockIdx.x >> 3);
+    if (w >= a.sblocks * a.nchunks) return false;
+    chunk_id = (int)(w / a.sblocks);
+    sblock = w - (int64_t)chunk_id * a.sblocks;
+    return true;
+}
 
 __device__ __forceinline__ bool valid_target(int64_t t, int64_t ignore, int64_t V) {
     return t != ignore && t >= 0 && t < V;
@@ -199,8 +223,9 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
     constexpr int KS = 2 * KB;  // 16-k steps of the score product
     constexpr int NFT = KB;     // 32-feature tiles of the gradient product
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r32 = lane & 31;
-    const int chunk_id = (int)(blockIdx.x % (unsigned)a.nchunks);
-    const int64_t sblock = blockIdx.x / (unsigned)a.nchunks;
+    int chunk_id;
+    int64_t sblock;
+    if (!work_item(a, chunk_id, sblock)) return;  // grid padding (whole workgroup)
     const int64_t srow = sblock * (32 * W) + wave * 32 + r32;  // this lane's stationary row (MFMA column)
     // (M_TSCORE: the streamed rows are the stationary block's own gathered target rows)
     const int64_t s_begin = MODE == M_TSCORE ? sblock * (32 * W) : (int64_t)chunk_id * a.chunk;
@@ -680,8 +705,9 @@ __global__ __launch_bounds__(kGradW * 64) void logits_grad_kernel(LogitsArgs a) 
     constexpr int NA = 2 * KS;   // stage-A steps (sub-tile, k step)
     constexpr int NB = 4 * NFT;  // stage-B steps (sub-tile, 16-row half, feature tile)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r32 = lane & 31;
-    const int chunk_id = (int)(blockIdx.x % (unsigned)a.nchunks);
-    const int64_t sblock = blockIdx.x / (unsigned)a.nchunks;
+    int chunk_id;
+    int64_t sblock;
+    if (!work_item(a, chunk_id, sblock)) return;  // grid padding (whole workgroup)
     const int64_t srow = sblock * (32 * W) + wave * 32 + r32;  // this lane's stationary row (MFMA column)
     // (M_TSCORE: the streamed rows are the stationary block's own gathered target rows)
     const int64_t s_begin = MODE == M_TSCORE ? sblock * (32 * W) : (int64_t)chunk_id * a.chunk;
@@ -1201,13 +1227,16 @@ constexpr bool kGradKernel = ASME_LOGITS_XTILE && ASME_LOGITS_DIAG == 0 && (MODE
 
 template <int MODE, int KB>
 int launch_engine(const LogitsArgs& a, int64_t sblocks, hipStream_t s) {
+    LogitsArgs g = a;
+    g.sblocks = sblocks;
+    g.per_xcd = (sblocks * a.nchunks + 7) / 8;  // grid = 8 per_xcd workgroups (work_item)
     if constexpr (kGradKernel<MODE>) {
         static const hipError_t attr = hipFuncSetAttribute((const void*)logits_grad_kernel<MODE, KB>,
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemGrad);
         if (attr != hipSuccess) return hip_status(attr, "logits: LDS opt-in");
         static_assert(EngineWaves<MODE>::W == kGradW, "the plan's stationary blocks are kGradW waves");
-        hipLaunchKernelGGL((logits_grad_kernel<MODE, KB>), dim3((unsigned)(sblocks * a.nchunks)), dim3(kGradW * 64),
-                           kSmemGrad, s, a);
+        hipLaunchKernelGGL((logits_grad_kernel<MODE, KB>), dim3((unsigned)(8 * g.per_xcd)), dim3(kGradW * 64),
+                           kSmemGrad, s, g);
         return hip_status(hipGetLastError(), "logits: gradient pass");
     }
     // LDS opt-in once per instantiation (a function-local static: thread-safe initialisation)
@@ -1216,8 +1245,8 @@ int launch_engine(const LogitsArgs& a, int64_t sblocks, hipStream_t s) {
         (int)kSmem);
     if (attr != hipSuccess) return hip_status(attr, "logits: LDS opt-in");
     constexpr int W = EngineWaves<MODE>::W;
-    hipLaunchKernelGGL((logits_engine_kernel<MODE, KB, W>), dim3((unsigned)(sblocks * a.nchunks)), dim3(W * 64), kSmem,
-                       s, a);
+    hipLaunchKernelGGL((logits_engine_kernel<MODE, KB, W>), dim3((unsigned)(8 * g.per_xcd)), dim3(W * 64), kSmem, s,
+                       g);
     return hip_status(hipGetLastError(), "logits: engine");
 }
 

@@ -12,9 +12,10 @@ for i in $(seq ${ROUNDS:-2}); do
   python - "$lib" ${KERNELS:-} <<'P'
 import json, sys
 j = json.load(open("gpurun_out/bab_full.json"))
-ks = {r["kernel"]: r["avg_ms"] for r in j.get("rooflines", [])}
+ks = {r["kernel"]: r["avg_ms"] for r in j.get("rooflines", []) + (j.get("eval") or {}).get("rooflines", [])}
 keys = ["asme_lazy_adam_stage", "asme_embedding_ln_fwd", "asme_embedding_ln_bwd"] + sys.argv[2:]
 print(sys.argv[1].split("/")[-1], j["value"], j["ms_per_step"], "flush", j.get("flush_ms"),
+      "eval", (j.get("eval") or {}).get("value"),
       " ".join(f"{k.replace('asme_', '')}={ks.get(k)}" for k in keys))
 P
  done
