@@ -105,9 +105,12 @@ class _TableGradMixin:
                              "use table_grad='dense'")
         self.table_grad = mode
         self._slot_map = None
+        # the catalogue's bf16 planes for fused evaluation, split once per validation pass (ops.CatalogPlanes)
+        self._catalog_planes = ops.CatalogPlanes()
 
 
     def _plan_table(self, id_sets):
+        self._catalog_planes.clear()  # training again: the evaluation's catalogue planes are stale (and 6 B / element)
         if self.table_grad != "sparse" or not self.training:
             return
         table = self.model.item_table()
@@ -209,7 +212,7 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         if q is None:
             raise NotImplementedError("model projection is not a dot product with an item table")
         h, table, bias = q
-        return ops.catalog_rank(h, table, targets, bias)
+        return ops.catalog_rank(h, table, targets, bias, planes=self._catalog_planes.get(table))
 
     def validation_step(self, batch, batch_idx):
         input_seq, targets = batch[ITEM_SEQ_ENTRY_NAME], batch[TARGET_ENTRY_NAME]
@@ -432,7 +435,7 @@ class MaskedTrainingModule(_TableGradMixin, _Base):
             raise ValueError("fused masked evaluation needs exactly one masked position per sequence")
         w, b = self.model.head_weight_bias()
         h = self.model.encode_rows(sequence, rows)
-        ranks = ops.catalog_rank(h, w, targets, b)
+        ranks = ops.catalog_rank(h, w, targets, b, planes=self._catalog_planes.get(w))
         loss = None
         if with_loss:
             pad = self.item_tokenizer.pad_token_id

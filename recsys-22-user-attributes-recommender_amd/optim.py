@@ -13,6 +13,7 @@ import ctypes
 import torch
 
 from ._lib import call, ptr, stream
+from . import ops
 from .ops import LazyTableState
 
 
@@ -88,6 +89,7 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        ops.note_param_write()  # (the kernels below write the parameters behind torch's version counter)
         for group in self.param_groups:
             b1, b2 = group["betas"]
             lr, eps, wd = float(group["lr"]), float(group["eps"]), float(group["weight_decay"])

@@ -358,7 +358,8 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
             emb._table_override = None
         if q is None or q[2] is not None:
             raise NotImplementedError("sharded evaluation needs the tied dot-product projection")
-        return catalog_ranks(self.exchange, q[0], targets, self.model.item_table().detach())
+        shard = self.model.item_table().detach()
+        return catalog_ranks(self.exchange, q[0], targets, shard, planes=self._catalog_planes.get(shard))
 
     def validation_step(self, batch, batch_idx):
         """NDCG / recall / MRR of the sharded model, identical to the unsharded model's (ranks over all |V|)"""
@@ -401,14 +402,15 @@ def _gather_queries(x: torch.Tensor, group) -> torch.Tensor:
 
 
 def catalog_ranks(exchange: RowShardExchange, hidden: torch.Tensor, targets: torch.Tensor,
-                  table_shard: torch.Tensor) -> torch.Tensor:
+                  table_shard: torch.Tensor, planes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Full-catalogue rank of every query's target with the item table row-sharded.
 
     Every rank holds its own queries (hidden (n, d), targets (n,), n equal on all ranks).  The target rows
     come from their owners (one all_to_all pair), the target scores are computed once by the same MFMA
     sequence the shard scans use; every rank then counts, for the queries of ALL ranks, the items of ITS
     shard that rank above the target (asme_catalog_count_above, no logits); one all_reduce(sum) of the
-    int32 counts gives the global ranks.  The table shard must be up to date (flush the lazy Adam first)."""
+    int32 counts gives the global ranks.  The table shard must be up to date (flush the lazy Adam first); `planes`:
+    ops.catalog_planes(table_shard) made earlier (a validation pass splits its shard once)."""
     group, W, rank = exchange.group, exchange.world, exchange.rank
     uniq, inv = torch.unique(targets, return_inverse=True)
     st = exchange.request(uniq)
@@ -417,7 +419,7 @@ def catalog_ranks(exchange: RowShardExchange, hidden: torch.Tensor, targets: tor
     h_all = _gather_queries(hidden, group)
     t_all = _gather_queries(targets.to(torch.int64), group)
     s_all = _gather_queries(tscore, group)
-    counts = ops.catalog_count_above(h_all, table_shard, t_all, s_all, W, rank)
+    counts = ops.catalog_count_above(h_all, table_shard, t_all, s_all, W, rank, planes=planes)
     _all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
     n = hidden.shape[0]
     return counts[rank * n:(rank + 1) * n].to(torch.int64) + 1

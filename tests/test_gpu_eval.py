@@ -168,3 +168,58 @@ def test_catalog_rank_equals_rank_of_materialised_scores(asme, dev, nq, V, d, wi
     st2 = S2.gather(1, targets[:, None])
     want2 = 1 + ((S2 > st2) | ((S2 == st2) & (ids < targets[:, None]))).sum(1)
     assert torch.equal(r2, want2)
+
+
+def test_catalog_planes_cache_follows_every_table_write(asme, dev):
+    """ops.CatalogPlanes reuses the split while the catalogue is unchanged and re-splits after any write: a torch
+    in-place op (version counter), a FusedAdam step (kernels writing behind the counter); the module's validation
+    ranks after a training step equal a fresh split's."""
+    ops = asme.ops
+    torch.manual_seed(3)
+    E = torch.randn(5003, 64, device=dev)
+    c = ops.CatalogPlanes()
+    p1 = c.get(E)
+    assert c.get(E) is p1 and c.get(E.detach()) is p1  # (detach shares storage and version counter)
+    assert torch.equal(p1, ops.catalog_planes(E))
+    E.add_(1e-3)
+    p2 = c.get(E)
+    assert p2 is not p1 and torch.equal(p2, ops.catalog_planes(E))
+    ops.note_param_write()
+    assert c.get(E) is not p2
+    # a table _f32 has to copy (not contiguous) is never cached
+    En = torch.randn(5003, 128, device=dev)[:, :64]
+    assert c.get(En) is not c.get(En)
+
+    from helpers import build_model, load, state_dict
+    z = load("sasrec_neg")
+    V = int(z["cfg"][5])
+    model = build_model(asme, "sasrec_neg", z)
+    model.load_state_dict(state_dict(z))
+    model.to(dev)
+    tok = asme.tokenization.Tokenizer(V - 3)
+    seq = torch.from_numpy(z["seq"]).to(dev)
+    pos = torch.from_numpy(z["pos"]).to(dev)
+    neg = torch.from_numpy(z["neg"]).to(dev)
+    eval_batch = {"item": seq, "item.target": pos[:, -1].contiguous()}
+    module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
+                                                            fused_eval=True)
+    opt = module.configure_optimizers()
+    module.eval()
+    with torch.no_grad():
+        r0 = module.catalog_ranks(eval_batch)
+        planes = module._catalog_planes._planes
+        assert torch.equal(module.catalog_ranks(eval_batch), r0) and module._catalog_planes._planes is planes
+    module.train()
+    out = module.training_step({"item": seq, "positive_samples": pos, "negative_samples": neg}, 0)
+    asme.modules.backward(out["loss"])
+    opt.step()
+    opt.zero_grad()
+    module.eval()
+    with torch.no_grad():
+        r1 = module.catalog_ranks(eval_batch)
+        table = model.item_table()
+        h, _, bias = model.catalog_query(asme.sequence.InputSequence(
+            seq, asme.modules.get_padding_mask(seq, tok), {}))
+        fresh = ops.catalog_rank(h, table, eval_batch["item.target"], bias)
+    assert module._catalog_planes._planes is not planes
+    assert torch.equal(r1, fresh)
