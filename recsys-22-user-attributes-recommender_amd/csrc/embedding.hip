@@ -699,6 +699,50 @@ __global__ __launch_bounds__(256) void pos_partial_kernel(const float* __restric
     }
 }
 
+// The same partial sums with float4 loads: 256 threads = G groups of D / 4 lanes (one whole row per group, one
+// 16-B chunk per lane); group g sums the chunk's rows b0 + g, b0 + g + G, ... in four independent chains (the
+// loads of four rows in flight per lane), and the G group sums are added in group order through LDS.  D / 4 must
+// divide 256 (D a power of two, 4 <= D <= 1024).
+__global__ __launch_bounds__(256) void pos_partial4_kernel(const float* __restrict__ rows, int64_t B, int64_t L,
+                                                           int D, int64_t chunk, float* __restrict__ part) {
+    __shared__ float4 red[256];
+    const int64_t p = blockIdx.x, c = blockIdx.y;
+    const int lanes = D >> 2, G = 256 / lanes, g = threadIdx.x / lanes, lane = threadIdx.x % lanes;
+    const int64_t b0 = c * chunk, b1 = min(B, b0 + chunk);
+    const float4* src = reinterpret_cast<const float4*>(rows) + p * lanes + lane;
+    const int64_t rstride = L * lanes;  // float4s between consecutive batch rows of position p
+    float4 a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t b = b0 + g;
+    for (; b + 3 * G < b1; b += 4 * G) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 v = src[(b + j * G) * rstride];
+            a[j] = make_float4(a[j].x + v.x, a[j].y + v.y, a[j].z + v.z, a[j].w + v.w);
+        }
+    }
+    // at most three rows of this group are left (constant indices: the accumulators stay in registers)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (b + j * G < b1) {
+            const float4 v = src[(b + j * G) * rstride];
+            a[j] = make_float4(a[j].x + v.x, a[j].y + v.y, a[j].z + v.z, a[j].w + v.w);
+        }
+    }
+    red[threadIdx.x] = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
+                                   (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
+    __syncthreads();
+    if (g == 0) {
+        float4 t = red[lane];
+        for (int k = 1; k < G; ++k) {
+            const float4 v = red[k * lanes + lane];
+            t = make_float4(t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w);
+        }
+        reinterpret_cast<float4*>(part)[(c * L + p) * lanes + lane] = t;
+    }
+}
+
 // column sums of a (nrows, width) matrix: a block owns 64 columns; its 16 row-groups of 64 threads each
 // sum every 16th row (coalesced 256-B row segments), then a fixed-order LDS tree adds the 16 partials.
 constexpr int kRedCols = 64, kRedGroups = 16;
@@ -1050,8 +1094,14 @@ ASME_API int asme_position_grad(const float* rows, int64_t batch, int64_t seq_le
                                 int64_t n_chunks, float* grad_pos, int accumulate, void* stream) {
     ASME_CHECK_ARG(rows && workspace && grad_pos && n_chunks >= 1, "asme_position_grad: bad argument");
     const int64_t chunk = (batch + n_chunks - 1) / n_chunks;
-    hipLaunchKernelGGL(pos_partial_kernel, dim3((unsigned)seq_len, (unsigned)n_chunks), dim3(128), 0,
-                       (hipStream_t)stream, rows, batch, seq_len, (int)dim, chunk, workspace);
+    const bool wide = dim >= 4 && dim <= 1024 && (dim & (dim - 1)) == 0 && ((uintptr_t)rows & 15) == 0 &&
+                      ((uintptr_t)workspace & 15) == 0;
+    if (wide)
+        hipLaunchKernelGGL(pos_partial4_kernel, dim3((unsigned)seq_len, (unsigned)n_chunks), dim3(256), 0,
+                           (hipStream_t)stream, rows, batch, seq_len, (int)dim, chunk, workspace);
+    else
+        hipLaunchKernelGGL(pos_partial_kernel, dim3((unsigned)seq_len, (unsigned)n_chunks), dim3(128), 0,
+                           (hipStream_t)stream, rows, batch, seq_len, (int)dim, chunk, workspace);
     const int64_t width = seq_len * dim;
     hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)((width + kRedCols - 1) / kRedCols)), dim3(1024), 0,
                        (hipStream_t)stream, workspace, n_chunks, width, grad_pos, accumulate);
