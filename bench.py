@@ -54,17 +54,29 @@ def committed_profile(name, config):
     return j if j.get("config") == config else {}
 
 
-def gemm_work(T, d, ffn):
+def gemm_work(T, d, ffn, fused_o=False):
     """algorithmic work per launch of the transformer's GEMM calls.  Per block: the forward QKV
     (d -> 3d), O (d -> d), FFN in (d -> ffn, its epilogue writing the activation and the factor keep * GELU'(pre) the
     backward needs in place of the pre-activation) and FFN out (ffn -> d), and the same four shapes as input
     gradients (the GELU one reading the factor), 8 asme_ws_linear calls: bytes in units of T x 4 B = 2 (8d + 3 ffn);
-    the four weight gradients on asme_linear_weight_grad: dY + X = 8d + 2 ffn"""
+    the four weight gradients on asme_linear_weight_grad: dY + X = 8d + 2 ffn.  fused_o: the O projection's forward
+    runs as asme_ws_linear_residual_ln (X and the residual in, s and LN(s) out + the row statistics), the other 7
+    calls per block on asme_ws_linear"""
     wg_flops = 2.0 * T * (3 * d * d + d * d + ffn * d + d * ffn)
     ws_bytes = 2 * T * 4.0 * (8 * d + 3 * ffn)
     wg_bytes = T * 4.0 * (8 * d + 2 * ffn)
-    return {"asme_ws_linear": ("gemm", 2 * wg_flops / 8, ws_bytes / 8),
-            "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4)}
+    out = {"asme_ws_linear": ("gemm", 2 * wg_flops / 8, ws_bytes / 8),
+           "asme_linear_weight_grad": ("gemm", wg_flops / 4, wg_bytes / 4)}
+    if fused_o:
+        o_flops, o_bytes = 2.0 * T * d * d, T * 4.0 * 2 * d
+        out["asme_ws_linear"] = ("gemm", (2 * wg_flops - o_flops) / 7, (ws_bytes - o_bytes) / 7)
+        out["asme_ws_linear_residual_ln"] = ("gemm", o_flops, T * 4.0 * 4 * d + T * 8)
+    return out
+
+
+def fused_o_projection(asme, d):
+    """the transformer's O projection runs fused with its residual + pre-LN (layers.TransformerLayer)"""
+    return bool(asme.layers.TransformerLayer.fuse_output_projection) and d == 128
 
 
 def roofline_entries(kstats, work, traffic, busy=None):
@@ -447,7 +459,8 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
         step(i)
     torch.cuda.synchronize()
     timer = asme._lib.KernelTimer(["asme_attention_fwd", "asme_attention_bwd", "asme_ws_linear",
-                                   "asme_linear_weight_grad", "asme_cross_entropy_fwd", "asme_cross_entropy_bwd",
+                                   "asme_ws_linear_residual_ln", "asme_linear_weight_grad", "asme_cross_entropy_fwd",
+                                   "asme_cross_entropy_bwd",
                                    "asme_linear_xent_fwd", "asme_linear_xent_bwd", "asme_linear_xent_fwd_dh",
                                    "asme_linear_xent_bwd_dw", "asme_cloze_mask",
                                    "asme_residual_ln_fwd", "asme_residual_ln_bwd", "asme_embedding_fwd",
@@ -470,7 +483,7 @@ def bench_bert4rec(args, asme, dev, world, rank, workload, items):
     ffn = 4 * d
     M = 0.9 * 0.2 * T + 0.1 * B  # expected non-ignored rows of a cloze batch
     work = {"asme_attention_fwd": ("mfma", 4.0 * pairs * dk), "asme_attention_bwd": ("mfma", 10.0 * pairs * dk),
-            **gemm_work(T, d, ffn),
+            **gemm_work(T, d, ffn, fused_o_projection(asme, d)),
             "asme_linear_xent_fwd": ("mfma", 2.0 * M * V * d), "asme_linear_xent_bwd": ("mfma", 4.0 * M * V * d),
             # training form: the forward computes the logits and dH (both algorithmic), the backward dW (its logits
             # recompute is not counted)
@@ -536,7 +549,8 @@ def bench_eval(args, asme, dev, world, rank, module, get_batch, ids_kind):
     recall.reset()
     module._catalog_planes.clear()  # the timed pass makes its own catalogue split
     timer = asme._lib.KernelTimer(["asme_catalog_rank_x6", "asme_catalog_count_above_x6", "asme_catalog_split",
-                                   "asme_catalog_target_scores_x6", "asme_ws_linear", "asme_attention_fwd",
+                                   "asme_catalog_target_scores_x6", "asme_ws_linear", "asme_ws_linear_residual_ln",
+                                   "asme_attention_fwd",
                                    "asme_embedding_ln_fwd"])
     if world > 1:
         dist.barrier()
@@ -557,7 +571,7 @@ def bench_eval(args, asme, dev, world, rank, module, get_batch, ids_kind):
     # the ranking scan: 2 nq |I| d FLOP per step (the target-score pass's 2 nq d is negligible; the catalogue split,
     # 5.1 GB in -> 7.7 GB of planes out, is an HBM pass of its own)
     work = {"asme_catalog_rank_x6": ("mfma", scan), "asme_catalog_count_above_x6": ("mfma", scan),
-            "asme_catalog_split": ("hbm", (V // world) * d * (4.0 + 6.0)), **gemm_work(B * L, d, 4 * d)}
+            "asme_catalog_split": ("hbm", (V // world) * d * (4.0 + 6.0)), **gemm_work(B * L, d, 4 * d, fused_o_projection(asme, d))}
     rooflines = roofline_entries(timer.summary(), work, {})
     return {"metric": f"evaluation sequences/sec (SASRec full-catalogue rank + NDCG@10, B={B} L={L} |I|={args.items})",
             "value": round(B * world * args.eval_steps / elapsed, 2), "unit": "sequences/s",
@@ -652,7 +666,8 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
                                    "asme_lazy_adam_apply", "asme_lazy_adam_stage", "asme_lazy_adam_apply_staged",
                                    "asme_sampled_logits_fwd", "asme_sampled_logits_bwd", "asme_gelu_dropout_fwd", "asme_gelu_dropout_bwd",
                                    "asme_linear_weight_grad", "asme_residual_ln_fwd", "asme_residual_ln_bwd",
-                                   "asme_ws_linear", "asme_posneg_sample", "asme_table_grad_reduce_apply",
+                                   "asme_ws_linear", "asme_ws_linear_residual_ln", "asme_posneg_sample",
+                                   "asme_table_grad_reduce_apply",
                                    "asme_dedup_ids", "asme_dedup_ids_segments", "asme_occurrence_csr",
                                    "asme_position_grad", "asme_reduce_rows", "asme_sasrec_bce_fwd",
                                    "asme_sasrec_bce_bwd"])
@@ -714,7 +729,7 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
         "asme_attention_fwd": ("mfma", 2 * 2.0 * pairs * dk),
         "asme_attention_bwd": ("mfma", 5 * 2.0 * pairs * dk),
         # the GEMM calls per block, averaged per launch (gemm_work)
-        **gemm_work(T, d, ffn),
+        **gemm_work(T, d, ffn, fused_o_projection(asme, d)),
         "asme_gelu_dropout_fwd": ("hbm", 2 * T * ffn * 4),
         "asme_residual_ln_fwd": ("hbm", 4 * T * d * 4 + T * 8),
         "asme_residual_ln_bwd": ("hbm", 5 * T * d * 4 + T * 8),

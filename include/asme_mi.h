@@ -437,6 +437,15 @@ int asme_table_grad_reduce_apply(const int32_t* order, const int32_t* sorted_slo
 int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N);
 int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W, int64_t N, int trans, const float* bias,
                    int epi, float* pre_out, const float* pre_in, float p, uint64_t seed, float* Y, void* stream);
+/* The attention output projection fused with the SublayerConnection residual and the next pre-LayerNorm
+ * (transformer_layers.py:120-130 + 251-258): s_out = drop_b(res + drop_a(X W^T + bias)), ln_out = LN(s_out),
+ * stats = (mean, rstd) per row -- bit-identical to asme_ws_linear (epi 0) + asme_residual_ln_fwd with the same seeds.
+ * K = N = 128 only (asme_ws_linear_residual_ln_supported); ln_w null: s_out only. */
+int asme_ws_linear_residual_ln_supported(int64_t M, int64_t K, int64_t N);
+int asme_ws_linear_residual_ln(const float* X, int64_t M, int64_t K, const float* W, int64_t N, const float* bias,
+                               const float* res, float p_a, uint64_t seed_a, float p_b, uint64_t seed_b,
+                               const float* ln_w, const float* ln_b, float eps, float* s_out, float* ln_out,
+                               float* stats, void* stream);
 
 /* ---- NARM encoders (csrc/narm.hip).  Global encoder: one nn.GRU layer, batch_first, h_0 = 0
  * (core/models/narm/components.py:32-56; the reference packs the padded batch, the recurrence is causal so the

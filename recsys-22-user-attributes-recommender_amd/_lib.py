@@ -43,6 +43,8 @@ SIGNATURES = {
     "asme_occurrence_csr_workspace": [i64],
     "asme_ws_linear_supported": [i64, i64, i64],
     "asme_ws_linear": [p, i64, i64, p, i64, i32, p, i32, p, p, f32, u64, p, p],
+    "asme_ws_linear_residual_ln_supported": [i64, i64, i64],
+    "asme_ws_linear_residual_ln": [p, i64, i64, p, i64, p, p, f32, u64, f32, u64, p, p, f32, p, p, p, p],
     "asme_occurrence_csr": [p, i64, i64, p, i64, p, p, p, p],
     "asme_table_grad_workspace": [i64, i64],
     "asme_table_grad_reduce": [p, p, p, p, i64, i64, i64, i32, p, p, p, p, f32, p, i64, p, p],

@@ -6,7 +6,10 @@
 //                       of counter idx/4 are exactly the chunk's 4 dropout decisions);
 //   W = 1 (other D):    the scalar fallback, LPR = 64.
 // LPR is the smallest power of two >= D/W (capped at 64), so D = 128 puts 2 rows in a wave and no lane
-// idles.  Row reductions are xor butterflies inside the LPR-lane group.
+// idles.  Row reductions are xor butterflies inside the LPR-lane group.  The LayerNorm statistics and affine spell
+// their fused multiply-adds out: clang's contractible a*b+c (llvm.fmuladd) is fused or not per call site, and kernels
+// that must agree bit for bit (asme_residual_ln_fwd and the ws GEMM's residual-LN epilogue) inline these helpers in
+// different surroundings.
 #pragma once
 #include "common.h"
 
@@ -157,7 +160,7 @@ __device__ __forceinline__ void row_ln_stats(const RowVals<R>& x, int sub, int D
 #pragma unroll
         for (int i = 0; i < R::W; ++i) {
             const float c = ok ? x[j][i] - mean : 0.f;
-            q += c * c;
+            q = __builtin_fmaf(c, c, q);  // (explicit: a contractible a*b+c is fused or not per call site)
         }
     }
     rstd = rsqrtf(div_by_width(row_sum<R::LPR>(q), D) + eps);
@@ -185,7 +188,7 @@ __device__ __forceinline__ void row_affine(const RowVals<R>& xh, int sub, int D,
 #pragma unroll
     for (int j = 0; j < R::NV; ++j)
 #pragma unroll
-        for (int i = 0; i < R::W; ++i) y[j][i] = xh[j][i] * wv[j][i] + bv[j][i];
+        for (int i = 0; i < R::W; ++i) y[j][i] = __builtin_fmaf(xh[j][i], wv[j][i], bv[j][i]);
 }
 
 // LayerNorm input gradient: gx = rstd * (gy*w - mean(gy*w) - xhat * mean(gy*w*xhat))

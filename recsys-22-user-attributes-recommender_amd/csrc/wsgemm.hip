@@ -23,6 +23,11 @@
 //            WS_GELU_DROP   pre = C + bias; Y = dropout(GELU(pre)); A = keep * GELU'(pre)   (FFN inner, forward)
 //            WS_GELU_BWD    Y = C * A                                                   (through the activation)
 //            WS_ACCUM       Y = C + Y                        (the second K = 256 half of a K = 512 product)
+//            WS_RESID_LN    s = drop_b(res + drop_a(C + bias)) -> Y;  LN(s) -> ln_out, (mean, rstd) -> stats
+//                           (the attention output projection fused with the SublayerConnection residual and the
+//                           next pre-LN, transformer_layers.py:120-130 + 251-258: one 128-feature block is a whole
+//                           row, so the row statistics are a 32-lane reduction in the epilogue -- the same
+//                           rows.h sequence as asme_residual_ln_fwd, bit-identical to the unfused pair)
 // A (the activation factor, written by the forward in place of the pre-activation, same bytes) makes the
 // backward epilogue a single multiply: no Philox, erf or exp in the input-gradient GEMM.
 // Dropout decisions are exactly those of asme_gelu_dropout_fwd/bwd (norm.hip): one Philox block per pair of
@@ -31,6 +36,7 @@
 // K=128 -> N=128 165 TF/s, K=384 -> N=128 (input gradient) 181, K=128 -> N=512 142 (row-staged stores),
 // K=512 -> N=128 145 (as two K = 256 halves); the fp32-MFMA version of this kernel (157 TF/s ceiling): 113-126.
 #include "common.h"
+#include "rows.h"
 
 using namespace asme;
 
@@ -43,7 +49,7 @@ constexpr int kWaves = 8;           // 512-thread workgroups, one per CU, two wa
 constexpr int kLdsMax = 160 * 1024;
 constexpr uint32_t kDrop = 0x80000000u;  // >= every buffer's record count: the access is dropped / reads 0
 
-enum { WS_STORE = 0, WS_GELU_DROP = 1, WS_GELU_BWD = 2, WS_ACCUM = 3 };
+enum { WS_STORE = 0, WS_GELU_DROP = 1, WS_GELU_BWD = 2, WS_ACCUM = 3, WS_RESID_LN = 4 };
 
 struct WsEpi {
     const float* bias;   // [N] or null
@@ -55,6 +61,14 @@ struct WsEpi {
     // first k column
     int64_t ldx, ldw;
     int kofs;
+    // WS_RESID_LN (pre_in = the residual, pre_out = the LayerNorm output; p / seed = drop_a): drop_b, the LayerNorm
+    // parameters (null: no LayerNorm, s only) and its per-row (mean, rstd)
+    float p2;
+    uint64_t seed2;
+    const float* ln_w;
+    const float* ln_b;
+    float eps;
+    float* stats;
 };
 
 __device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s ^ (r & 15)); }
@@ -190,6 +204,16 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const __amdgpu_buffer_rsrc_t pr = EPI == WS_ACCUM ? yr
                                     : rsrc(EPI == WS_GELU_DROP ? (const void*)ep.pre_out : (const void*)ep.pre_in,
                                            EPI == WS_STORE ? 0 : M * N * 4);
+    static_assert(EPI != WS_RESID_LN || (kStage && CT == 8 && NB == 128),
+                  "the residual + LayerNorm epilogue needs whole 128-feature rows in the staged tile");
+    // WS_RESID_LN: the LayerNorm output stream and this lane's four LayerNorm weights / biases (its staged float4 is
+    // always features 4 (lane % 32) .. +3), held in registers: no parameter load inside the epilogue
+    const __amdgpu_buffer_rsrc_t lr = rsrc(ep.pre_out, EPI == WS_RESID_LN && ep.ln_w ? M * N * 4 : 0);
+    float4 lnw = make_float4(0.f, 0.f, 0.f, 0.f), lnb = lnw;
+    if (EPI == WS_RESID_LN && ep.ln_w) {
+        lnw = *reinterpret_cast<const float4*>(ep.ln_w + 4 * (threadIdx.x & 31));
+        lnb = *reinterpret_cast<const float4*>(ep.ln_b + 4 * (threadIdx.x & 31));
+    }
     // the bias: added where the staged tile is read back when every read of a lane falls on the same float4 of
     // the feature block (64 % NB4 == 0: one register set instead of CT), else to the accumulators at the tile's end
     constexpr bool kBiasEpi = kStage && 64 % NB4 == 0;
@@ -277,6 +301,35 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                 gelu_erf_and_grad(v.w, gl[3], gd[3]);
                 bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off, nt_out);
                 bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off, nt_out);
+            } else if constexpr (EPI == WS_RESID_LN) {
+                // the asme_residual_ln_fwd sequence (norm.hip) on RowLayout<4, 32, 1>: lanes 0-31 hold row idx / 32 of
+                // the tile, lanes 32-63 the next one, lane sub the features 4 sub .. 4 sub + 3
+                using R = RowLayout<4, 32, 1>;
+                const int sub = threadIdx.x & 31;
+                const int64_t t = srow0 + idx / NB4;
+                RowVals<R> a, h, f;
+                a[0][0] = v.x, a[0][1] = v.y, a[0][2] = v.z, a[0][3] = v.w;
+                h[0][0] = pre[ct].x, h[0][1] = pre[ct].y, h[0][2] = pre[ct].z, h[0][3] = pre[ct].w;
+                if (ep.p > 0.f) {
+                    row_keep<R>(ep.seed, 3u, (uint64_t)t * 128, sub, ep.p, f);
+                    row_mul<R>(a, f);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) h[0][i] += a[0][i];
+                if (ep.p2 > 0.f) {
+                    row_keep<R>(ep.seed2, 4u, (uint64_t)t * 128, sub, ep.p2, f);
+                    row_mul<R>(h, f);
+                }
+                bstore(make_float4(h[0][0], h[0][1], h[0][2], h[0][3]), yr, off, nt_out);
+                if (ep.ln_w) {
+                    float m, r;
+                    row_ln_stats<R>(h, sub, 128, ep.eps, m, r);
+                    row_normalise<R>(h, sub, 128, m, r, a);
+                    bstore(make_float4(__builtin_fmaf(a[0][0], lnw.x, lnb.x), __builtin_fmaf(a[0][1], lnw.y, lnb.y),
+                                       __builtin_fmaf(a[0][2], lnw.z, lnb.z), __builtin_fmaf(a[0][3], lnw.w, lnb.w)),
+                           lr, off, nt_out);  // (row_affine's explicit fma)
+                    if (sub == 0 && t < M) *reinterpret_cast<float2*>(ep.stats + 2 * t) = make_float2(m, r);
+                }
             } else {
                 const float4 f = pre[ct];
                 bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off, nt_out);
@@ -365,14 +418,15 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                     kBiasEpi ? make_float4(acc[ct][0], acc[ct][1], acc[ct][2], acc[ct][3])
                              : make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
                                            acc[ct][3] + breg[ct].w);
-                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM) pre[ct] = bload(pr, staged_off(ct, srow0));
+                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM || EPI == WS_RESID_LN)
+                    pre[ct] = bload(pr, staged_off(ct, srow0));
             }
         } else {
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 stash[ct] = make_float4(acc[ct][0] + breg[kBiasEpi ? 0 : ct].x, acc[ct][1] + breg[kBiasEpi ? 0 : ct].y,
                                         acc[ct][2] + breg[kBiasEpi ? 0 : ct].z, acc[ct][3] + breg[kBiasEpi ? 0 : ct].w);
-                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM) pre[ct] = bload(pr, soff + ct * 64);
+                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM || EPI == WS_RESID_LN) pre[ct] = bload(pr, soff + ct * 64);
             }
         }
         rc = rn;
@@ -499,6 +553,41 @@ ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W
     if (epi == 0) return dispatch_k<false, WS_STORE>((int)K, ct, X, M, W, (int)N, Y, ep, s);
     if (epi == 1) return dispatch_k<false, WS_GELU_DROP>((int)K, ct, X, M, W, (int)N, Y, ep, s);
     return dispatch_k<false, WS_GELU_BWD>((int)K, ct, X, M, W, (int)N, Y, ep, s);
+}
+
+// 1 when asme_ws_linear_residual_ln takes the shape: K = N = 128 (one 128-feature block is a whole row) and the
+// plain kernel's limits
+ASME_API int asme_ws_linear_residual_ln_supported(int64_t M, int64_t K, int64_t N) {
+    return K == 128 && N == 128 && asme_ws_linear_supported(M, K, N) && pick_ct(128, 128) == 8 ? 1 : 0;
+}
+
+// The attention output projection with the SublayerConnection residual and the next pre-LayerNorm in its epilogue:
+//   s_out = drop_b(res + drop_a(X W^T + bias));  ln_out = LN(s_out; ln_w, ln_b, eps);  stats = (mean, rstd) per row
+// bit-identical to asme_ws_linear (epi 0) followed by asme_residual_ln_fwd with the same seeds (same products, same
+// dropout streams, same row-statistics sequence), without the Y round trip.  ln_w null: s_out only (ln_b, ln_out,
+// stats unused).  X, res, s_out, ln_out: M x 128 contiguous rows, 16-B aligned; W: 128 x 128 (nn.Linear.weight).
+ASME_API int asme_ws_linear_residual_ln(const float* X, int64_t M, int64_t K, const float* W, int64_t N,
+                                        const float* bias, const float* res, float p_a, uint64_t seed_a, float p_b,
+                                        uint64_t seed_b, const float* ln_w, const float* ln_b, float eps,
+                                        float* s_out, float* ln_out, float* stats, void* stream) {
+    ASME_CHECK_ARG(X && W && res && s_out, "asme_ws_linear_residual_ln: null pointer");
+    ASME_CHECK_ARG(!ln_w || (ln_b && ln_out && stats), "asme_ws_linear_residual_ln: LayerNorm outputs missing");
+    ASME_CHECK_ARG(asme_ws_linear_residual_ln_supported(M, K, N), "asme_ws_linear_residual_ln: unsupported shape");
+    ASME_CHECK_ARG(p_a >= 0.f && p_a < 1.f && p_b >= 0.f && p_b < 1.f, "asme_ws_linear_residual_ln: bad dropout p");
+    ASME_CHECK_ARG(((uintptr_t)X & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)res & 15) == 0 &&
+                       ((uintptr_t)s_out & 15) == 0 && (!ln_w || (((uintptr_t)ln_out & 15) == 0 &&
+                                                                   ((uintptr_t)ln_w & 15) == 0 &&
+                                                                   ((uintptr_t)ln_b & 15) == 0 &&
+                                                                   ((uintptr_t)stats & 7) == 0)),
+                   "asme_ws_linear_residual_ln: alignment");
+    WsEpi ep{bias, ln_w ? ln_out : nullptr, res, p_a, seed_a, 128, 128, 0};
+    ep.p2 = p_b;
+    ep.seed2 = seed_b;
+    ep.ln_w = ln_w;
+    ep.ln_b = ln_b;
+    ep.eps = eps;
+    ep.stats = stats;
+    return launch_ws<128, 8, false, WS_RESID_LN>(X, M, W, 128, s_out, ep, (hipStream_t)stream);
 }
 
 // ---- experiment: X pre-split into its bf16 planes by its producer

@@ -300,12 +300,26 @@ class TransformerLayer(nn.Module):
             att, ff = blk.attention, blk.feed_forward
             qkv = att.qkv(ln)
             o = ops.attention(qkv, key_valid, att.heads, causal, _p(att.dropout, tr))
-            a = ops.linear(o, att.output_linear.weight, att.output_linear.bias)
-            h1, ln2 = _residual_norm(x, a, blk.output_sublayer.norm, _p(blk.input_sublayer.dropout, tr), 0.0)
+            h1, ln2 = self._projection_residual_norm(o, att.output_linear, x, blk.output_sublayer.norm,
+                                                     _p(blk.input_sublayer.dropout, tr))
             f2 = ops.ffn(ln2, ff.w_1.weight, ff.w_1.bias, ff.w_2.weight, ff.w_2.bias, _p(ff.dropout, tr))
             nxt = blocks[i + 1].input_sublayer.norm if i + 1 < len(blocks) else None
             x, ln = _residual_norm(h1, f2, nxt, _p(blk.output_sublayer.dropout, tr), _p(blk.dropout, tr))
         return x
+
+    # True: the attention output projection, its residual and the next pre-LN in one kernel where it tiles (d = 128:
+    # asme_ws_linear_residual_ln, bit-identical to the separate Linear + residual-LN kernels).  Off: measured slower in
+    # the step (128 us per call vs 48 + 65 us for the two kernels, -0.6 % per step, tools/rln_step_ab.py): at two
+    # waves per SIMD the epilogue's row reductions and dropout do not hide under the GEMM's streaming
+    fuse_output_projection = False
+
+    def _projection_residual_norm(self, o, lin: nn.Linear, res, norm, p_a: float):
+        """(h1, LN(h1)) with h1 = res + drop_a(lin(o)) (transformer_layers.py:120-130 around :181-199)"""
+        if (self.fuse_output_projection and (norm is None or not has_forward_hooks(norm))
+                and ops.linear_residual_ln_ok(o, lin.weight, res)):
+            return ops.linear_residual_ln(o, lin.weight, lin.bias, res, norm, p_a, 0.0)
+        a = ops.linear(o, lin.weight, lin.bias)
+        return _residual_norm(res, a, norm, p_a, 0.0)
 
 
 def _residual_norm(res, y, norm, p_a: float, p_b: float):

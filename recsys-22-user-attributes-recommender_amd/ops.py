@@ -1254,23 +1254,92 @@ class _ResidualLNFn(torch.autograd.Function):
     def backward(ctx, d_s, d_ln):
         s, w, stats = ctx.saved_tensors
         p_a, sa, p_b, sb, has_ln, shape = ctx.meta
-        n, D = s.shape
-        ds2 = None if d_s is None else _f32(d_s).reshape(n, D)
-        dl2 = None if (d_ln is None or not has_ln) else _f32(d_ln).reshape(n, D)
-        d_res = torch.empty_like(s)
-        d_y = torch.empty_like(s) if p_a > 0 else None
-        part = torch.empty(_N_PARTIALS, 2 * D, device=s.device, dtype=torch.float32) if dl2 is not None else None
-        call("asme_residual_ln_bwd", ptr(s), n, D, p_a, sa, p_b, sb, ptr(w), ptr(stats), ptr(ds2), ptr(dl2),
-             ptr(d_res), ptr(d_y), ptr(part), _N_PARTIALS, stream())
-        gw = gb = None
-        if has_ln:
-            if part is not None:
-                red = _reduce_partials(part, 2 * D)
-                gw, gb = red[:D], red[D:]
-            else:
-                gw, gb = torch.zeros_like(w), torch.zeros_like(w)
-        dy = d_y if d_y is not None else d_res
+        d_res, dy, gw, gb = _residual_ln_backward(s, w, stats, (p_a, sa, p_b, sb, has_ln), d_s, d_ln)
         return d_res.view(shape), dy.view(shape), gw, gb, None, None, None
+
+
+def _residual_ln_backward(s, w, stats, meta, d_s, d_ln):
+    """(d_res, d_y, d_w, d_b) of s = drop_b(res + drop_a(y)), ln = LN(s) (asme_residual_ln_bwd)"""
+    p_a, sa, p_b, sb, has_ln = meta
+    n, D = s.shape
+    ds2 = None if d_s is None else _f32(d_s).reshape(n, D)
+    dl2 = None if (d_ln is None or not has_ln) else _f32(d_ln).reshape(n, D)
+    d_res = torch.empty_like(s)
+    d_y = torch.empty_like(s) if p_a > 0 else None
+    part = torch.empty(_N_PARTIALS, 2 * D, device=s.device, dtype=torch.float32) if dl2 is not None else None
+    call("asme_residual_ln_bwd", ptr(s), n, D, p_a, sa, p_b, sb, ptr(w), ptr(stats), ptr(ds2), ptr(dl2),
+         ptr(d_res), ptr(d_y), ptr(part), _N_PARTIALS, stream())
+    gw = gb = None
+    if has_ln:
+        if part is not None:
+            red = _reduce_partials(part, 2 * D)
+            gw, gb = red[:D], red[D:]
+        else:
+            gw, gb = torch.zeros_like(w), torch.zeros_like(w)
+    return d_res, (d_y if d_y is not None else d_res), gw, gb
+
+
+class _LinearResidualLNFn(torch.autograd.Function):
+    """_LinearFn followed by _ResidualLNFn as ONE kernel (asme_ws_linear_residual_ln: the residual, dropouts and the
+    next pre-LN in the GEMM's epilogue, no Y round trip): s = drop_b(res + drop_a(x W^T + b)), ln = LN(s).  The
+    attention output projection and the SublayerConnection around it (transformer_layers.py:120-130, 181-199,
+    251-258).  Values and gradients are bit-identical to the two separate ops with the same seeds; the backward is
+    theirs (asme_residual_ln_bwd, then the Linear's input and weight gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, res, ln_w, ln_b, eps: float, p_a: float, p_b: float):
+        shape = res.shape
+        N, K = w.shape
+        x2 = _f32(x).reshape(-1, K)
+        r2 = _f32(res).reshape(-1, N)
+        n = r2.shape[0]
+        s = torch.empty_like(r2)
+        has_ln = ln_w is not None
+        ln = torch.empty_like(r2) if has_ln else None
+        stats = torch.empty(n, 2, device=res.device, dtype=torch.float32) if has_ln else None
+        sa, sb = new_seed(p_a), new_seed(p_b)  # (drawn in _ResidualLNFn's order)
+        call("asme_ws_linear_residual_ln", ptr(x2), n, K, ptr(_f32(w)), N, ptr(_f32(b)) if b is not None else None,
+             ptr(r2), p_a, sa, p_b, sb, ptr(ln_w), ptr(ln_b), eps, ptr(s), ptr(ln), ptr(stats), stream())
+        ctx.save_for_backward(x2, w, s, ln_w, stats)
+        ctx.meta = (p_a, sa, p_b, sb, has_ln)
+        ctx.has_bias = b is not None
+        ctx.shapes = (x.shape, shape)
+        if has_ln:
+            return s.view(shape), ln.view(shape)
+        return s.view(shape), s.new_empty(0)
+
+    @staticmethod
+    def backward(ctx, d_s, d_ln):
+        x2, w, s, ln_w, stats = ctx.saved_tensors
+        xshape, shape = ctx.shapes
+        d_res, d_y, gw, gb = _residual_ln_backward(s, ln_w, stats, ctx.meta, d_s, d_ln)
+        N, K = w.shape
+        dx = _linear_dx(d_y, w).view(xshape) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw, db = _weight_grad(d_y, x2, ctx.has_bias)
+        return dx, dw, db, d_res.view(shape), gw, gb, None, None, None
+
+
+def linear_residual_ln_ok(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor) -> bool:
+    """the fused output projection + residual + LayerNorm kernel takes this call"""
+    N, K = w.shape
+    if not (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and res.dtype == torch.float32
+            and x.shape[-1] == K and res.shape[-1] == N and x.shape[:-1] == res.shape[:-1]):
+        return False
+    M = res.numel() // N
+    key = ("rln", M, K, N)
+    if key not in _WS_SUPPORTED:
+        _WS_SUPPORTED[key] = bool(_lib.load().asme_ws_linear_residual_ln_supported(M, K, N))
+    return _WS_SUPPORTED[key]
+
+
+def linear_residual_ln(x, w, b, res, norm: Optional[torch.nn.LayerNorm], p_a: float, p_b: float):
+    """(s, LN(s) or None) with s = drop_b(res + drop_a(linear(x, w, b))) in one kernel (linear_residual_ln_ok)"""
+    if norm is None:
+        s, _ = _LinearResidualLNFn.apply(x, w, b, res, None, None, 1e-5, p_a, p_b)
+        return s, None
+    return _LinearResidualLNFn.apply(x, w, b, res, norm.weight, norm.bias, norm.eps, p_a, p_b)
 
 
 def residual_ln(res, y, norm: Optional[torch.nn.LayerNorm], p_a: float, p_b: float):

@@ -55,9 +55,10 @@ def test_model_train_step_matches_reference(asme, dev, name, fused_xent, monkeyp
     if not fused_xent and base_name(name) == "sasrec_neg":
         pytest.skip("no full-catalogue CE head")
     monkeypatch.setattr(asme.modules, "FUSED_XENT", fused_xent)
-    calls = {"ws": 0, "wgrad": 0, "ffn": 0}
+    calls = {"ws": 0, "wgrad": 0, "ffn": 0, "ws_rln": 0}
     if name.endswith("_d128"):
         ws, wg, ffn_fwd = asme.ops._ws, asme.ops._weight_grad, asme.ops._FFNFn.forward
+        rln_fwd = asme.ops._LinearResidualLNFn.forward
 
         def count(key, fn):
             def wrapped(*a, **k):
@@ -71,6 +72,7 @@ def test_model_train_step_matches_reference(asme, dev, name, fused_xent, monkeyp
         monkeypatch.setattr(asme.ops, "_ws", count("ws", ws))
         monkeypatch.setattr(asme.ops, "_weight_grad", count("wgrad", wg))
         monkeypatch.setattr(asme.ops._FFNFn, "forward", staticmethod(count("ffn", ffn_fwd)))
+        monkeypatch.setattr(asme.ops._LinearResidualLNFn, "forward", staticmethod(count("ws_rln", rln_fwd)))
         library_linear = torch.nn.functional.linear
         if fused_xent:
             monkeypatch.setattr(torch.nn.functional, "linear", no_library_linear)
@@ -88,7 +90,11 @@ def test_model_train_step_matches_reference(asme, dev, name, fused_xent, monkeyp
     if name.endswith("_d128"):
         n_blocks = int(z["cfg"][4])
         assert calls["ffn"] == n_blocks, calls        # fused GELU/dropout FFN per block
-        assert calls["ws"] >= 8 * n_blocks, calls     # QKV + O + FFN(2) forward + input-gradient GEMMs
+        # QKV + O + FFN(2) forward + input-gradient GEMMs; the O projection's forward as the fused projection +
+        # residual + LayerNorm kernel (asme_ws_linear_residual_ln, one per block)
+        fused_o = asme.layers.TransformerLayer.fuse_output_projection
+        assert calls["ws_rln"] == (n_blocks if fused_o else 0), calls
+        assert calls["ws"] + calls["ws_rln"] >= 8 * n_blocks, calls
         assert calls["wgrad"] >= 4 * n_blocks, calls  # QKV, O, W1, W2 weight gradients
         monkeypatch.setattr(torch.nn.functional, "linear", library_linear)
     grads = prefixed(z, "grad")
@@ -255,3 +261,33 @@ def test_bert4rec_anchor_ndcg(asme, dev, fused_eval):
     assert len(logged["val_loss"]) == (n_users + 511) // 512
     got = float(ndcg.compute())
     assert abs(got - float(z["ndcg10"])) <= 1e-4, (got, float(z["ndcg10"]))
+
+
+def test_fused_output_projection_is_bit_identical_in_the_model(asme, dev, monkeypatch):
+    """TransformerLayer.fuse_output_projection (asme_ws_linear_residual_ln) trains the d = 128 SASRec step to the
+    same loss and gradients, bit for bit, as the separate Linear + residual-LN kernels"""
+    name = "sasrec_neg_d128"
+    z = load(name)
+    V = int(z["cfg"][5])
+    results = []
+    for fused in (False, True):
+        monkeypatch.setattr(asme.layers.TransformerLayer, "fuse_output_projection", fused)
+        model = build_model(asme, name, z)
+        model.load_state_dict(state_dict(z), strict=True)
+        model.to(dev)
+        module = _module(asme, name, model, V)
+        torch.manual_seed(7)
+        loss = module.training_step(_batch(name, z, dev), 0)["loss"]
+        loss.backward()
+        grads = {k: (p.grad.clone() if p.grad is not None else None) for k, p in model.named_parameters()}
+        table = model.item_table()
+        tg = getattr(table, "_asme_table_grad", None)
+        if tg is not None and tg.plan is not None:
+            grads["table_rows"] = tg.plan.grad_rows[:tg.plan.n_unique()].clone()
+        results.append((loss.detach(), grads))
+    (l0, g0), (l1, g1) = results
+    assert torch.equal(l0, l1)
+    assert g0.keys() == g1.keys()
+    for k in g0:
+        assert (g0[k] is None) == (g1[k] is None), k
+        assert g0[k] is None or torch.equal(g0[k], g1[k]), k

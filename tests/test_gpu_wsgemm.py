@@ -143,3 +143,51 @@ def test_fused_ffn_matches_composition(asme, dev, p):
         xx = x.clone().requires_grad_(True)
         y = ff["w_2"](F.gelu(ff["w_1"](xx)))
         assert torch.allclose(y1, y.detach(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("p_a,p_b,with_ln", [(0.0, 0.0, True), (0.2, 0.0, True), (0.2, 0.3, True), (0.1, 0.0, False)])
+def test_linear_residual_ln_fused_is_bit_identical(asme, dev, p_a, p_b, with_ln):
+    """asme_ws_linear_residual_ln (output projection + residual + dropouts + next pre-LN in one epilogue) equals
+    asme_ws_linear followed by asme_residual_ln_fwd bit for bit -- outputs, statistics and every gradient"""
+    ops = asme.ops
+    torch.manual_seed(11)
+    M, d = 3 * 4096 + 77, 128  # ragged tail rows
+    x = torch.randn(M, d, device=dev)
+    w = torch.randn(d, d, device=dev) / d ** 0.5
+    b = torch.randn(d, device=dev)
+    res = torch.randn(M, d, device=dev)
+    norm = torch.nn.LayerNorm(d).to(dev) if with_ln else None
+    if norm is not None:
+        with torch.no_grad():
+            norm.weight.add_(torch.randn(d, device=dev) * 0.1)
+            norm.bias.add_(torch.randn(d, device=dev) * 0.1)
+    ds, dl = torch.randn(M, d, device=dev), torch.randn(M, d, device=dev)
+    assert ops.linear_residual_ln_ok(x, w, res)
+    outs = []
+    for fused in (False, True):
+        xs, ws, bs, rs = (t.clone().requires_grad_(True) for t in (x, w, b, res))
+        if norm is not None:
+            norm.weight.grad = norm.bias.grad = None
+        torch.manual_seed(5)  # the dropout seeds
+        if fused:
+            s, ln = ops.linear_residual_ln(xs, ws, bs, rs, norm, p_a, p_b)
+        else:
+            s, ln = ops.residual_ln(rs, ops.linear(xs, ws, bs), norm, p_a, p_b)
+        loss = (s * ds).sum() + ((ln * dl).sum() if ln is not None else 0.0)
+        loss.backward()
+        grads = [xs.grad, ws.grad, bs.grad, rs.grad]
+        if norm is not None:
+            grads += [norm.weight.grad.clone(), norm.bias.grad.clone()]
+        outs.append((s.detach(), None if ln is None else ln.detach(), grads))
+    (s0, l0, g0), (s1, l1, g1) = outs
+    assert torch.equal(s0, s1)
+    assert (l0 is None) == (l1 is None) and (l0 is None or torch.equal(l0, l1))
+    for a, c in zip(g0, g1):
+        assert torch.equal(a, c)
+
+
+def test_linear_residual_ln_refuses_other_widths(asme, dev):
+    ops = asme.ops
+    x, w, res = (torch.randn(256, 64, device=dev), torch.randn(64, 64, device=dev), torch.randn(256, 64, device=dev))
+    assert not ops.linear_residual_ln_ok(x, w, res)
+    assert asme._lib.load().asme_ws_linear_residual_ln_supported(256, 256, 128) == 0
