@@ -463,13 +463,28 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
                     // item i is ranked above the target t iff s_i > s_t, or s_i == s_t and i < t (ties to the lower
                     // id, the reference argsort's order on tie-free data); s = products + bias exactly as M_TSCORE and
                     // M_LOGITS form it, so the target compares bit-identically with itself
-                    const int j0 = (int)r0 + 32 * sub, jn = (int)a.n_strm;
+                    // (row j = j0 + c, c = acc_row(i, h) in [0, 32); tests without short-circuit branches)
+                    const int j0 = (int)r0 + 32 * sub;
+                    const int t_lt = r_jlt - j0, t_eq = r_jeq - j0, t_n = (int)a.n_strm - j0;
+                    // the common case: for every lane of the wave the sub-tile holds neither its target's row nor its
+                    // lower-id boundary and every row exists; then "above" is sc > r_ts (no row below the target's
+                    // id) or sc >= r_ts (all rows below it) = sc > the float just below r_ts -- one compare per element
+                    // (r_ts finite and non-zero, so the float below is a normal number or the largest negative one)
+                    const bool clean = t_n >= 32 && (t_eq < 0 || t_eq >= 32) && (t_lt <= 0 || t_lt >= 32) &&
+                                       __builtin_isfinite(r_ts) && r_ts != 0.f;
+                    if (__ballot(!clean) == 0ull) {
+                        const float thr = t_lt >= 32 ? __int_as_float(__float_as_int(r_ts) + (r_ts > 0.f ? -1 : 1))
+                                                     : r_ts;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int j = j0 + acc_row(i, h);
-                        const float sc = x[i] + tf[32 * sub + acc_row(i, h)];
-                        const bool above = j < jn && j != r_jeq && (sc > r_ts || (sc == r_ts && j < r_jlt));
-                        r_cnt += above ? 1 : 0;
+                        for (int i = 0; i < 16; ++i) r_cnt += (x[i] + tf[32 * sub + acc_row(i, h)]) > thr ? 1 : 0;
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const int c = acc_row(i, h);
+                            const float sc = x[i] + tf[32 * sub + c];
+                            const bool above = ((sc > r_ts) | ((sc == r_ts) & (c < t_lt))) & (c < t_n) & (c != t_eq);
+                            r_cnt += above ? 1 : 0;
+                        }
                     }
                     continue;
                 }
