@@ -475,8 +475,13 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
                     if (__ballot(!clean) == 0ull) {
                         const float thr = t_lt >= 32 ? __int_as_float(__float_as_int(r_ts) + (r_ts > 0.f ? -1 : 1))
                                                      : r_ts;
+                        if (!a.bias) {  // (no bias: every row of a clean sub-tile adds +0, which no comparison sees)
 #pragma unroll
-                        for (int i = 0; i < 16; ++i) r_cnt += (x[i] + tf[32 * sub + acc_row(i, h)]) > thr ? 1 : 0;
+                            for (int i = 0; i < 16; ++i) r_cnt += x[i] > thr ? 1 : 0;
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 16; ++i) r_cnt += (x[i] + tf[32 * sub + acc_row(i, h)]) > thr ? 1 : 0;
+                        }
                     } else {
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
