@@ -229,24 +229,45 @@ __device__ __forceinline__ void replay_steps(float2v (&P)[NP], float2v (&M)[NP],
         if (t0 >= upto) return;
         AdamHyper hp = hist[upto];
         const float2* __restrict__ lr = reinterpret_cast<const float2*>(hist) + 3;  // (neg_step_size, inv_bc2_sqrt)
-        float2 nx = lr[4 * (t0 + 1)];
-        if (hp.wd != 0.f) {
-            for (int32_t t = t0 + 1; t <= upto; ++t) {
-                hp.neg_step_size = nx.x;
-                hp.inv_bc2_sqrt = nx.y;
-                nx = lr[4 * min(t + 1, upto)];
+        // two steps per trip, their constants loaded a trip ahead: the scalar loads' wait sits behind two steps of
+        // vector work, and the loop and address arithmetic (which had matched the replay's VALU count one for one in
+        // the flush's PMC pass: SALU 482M vs VALU 455M) is paid once per two steps
+        float2 n0 = lr[4 * (t0 + 1)], n1 = lr[4 * min(t0 + 2, upto)];
+        int32_t t = t0 + 1;
+        auto steps = [&](auto op) {
+            auto two = [&](const float2 c0, const float2 c1) {
+                hp.neg_step_size = c0.x;
+                hp.inv_bc2_sqrt = c0.y;
 #pragma unroll
-                for (int j = 0; j < NP; ++j) adam_elem2(P[j], float2v{0.f, 0.f}, M[j], Vv[j], hp);
-            }
-        } else {
-            for (int32_t t = t0 + 1; t <= upto; ++t) {
-                hp.neg_step_size = nx.x;
-                hp.inv_bc2_sqrt = nx.y;
-                nx = lr[4 * min(t + 1, upto)];
+                for (int j = 0; j < NP; ++j) op(P[j], M[j], Vv[j], hp);
+                hp.neg_step_size = c1.x;
+                hp.inv_bc2_sqrt = c1.y;
 #pragma unroll
-                for (int j = 0; j < NP; ++j) adam_decay2(P[j], M[j], Vv[j], hp);
+                for (int j = 0; j < NP; ++j) op(P[j], M[j], Vv[j], hp);
+            };
+            // steps t, t + 1 while the pair after them exists (t + 3 <= upto): its constants by a running pointer,
+            // no clamp
+            const float2* q = lr + 4 * (t0 + 3);
+            for (; t + 3 <= upto; t += 2, q += 8) {
+                const float2 c0 = n0, c1 = n1;
+                n0 = q[0];
+                n1 = q[4];
+                __builtin_amdgcn_sched_barrier(0);  // (the loads first: their wait is the trip's end, after its work)
+                two(c0, c1);
             }
-        }
+            if (t < upto) {  // the last two steps (n0, n1 hold steps t and t + 1)
+                two(n0, n1);
+            } else if (t == upto) {  // or the last one
+                hp.neg_step_size = n0.x;
+                hp.inv_bc2_sqrt = n0.y;
+#pragma unroll
+                for (int j = 0; j < NP; ++j) op(P[j], M[j], Vv[j], hp);
+            }
+        };
+        if (hp.wd != 0.f)
+            steps([](float2v& p, float2v& m, float2v& v, const AdamHyper& h) { adam_elem2(p, float2v{0.f, 0.f}, m, v, h); });
+        else
+            steps([](float2v& p, float2v& m, float2v& v, const AdamHyper& h) { adam_decay2(p, m, v, h); });
         return;
     }
     for (int32_t t = t0 + 1; t <= upto; ++t) {
