@@ -1719,6 +1719,7 @@ class CatalogPlanes:
     def __init__(self):
         self._key = None
         self._planes: Optional[torch.Tensor] = None
+        self._table: Optional[torch.Tensor] = None  # held: its storage cannot be freed and reused under the same key
 
     def get(self, table: torch.Tensor) -> torch.Tensor:
         E = _f32(table)
@@ -1726,13 +1727,13 @@ class CatalogPlanes:
             return catalog_planes(E)
         key = (E.data_ptr(), tuple(E.shape), E.stride(0), E._version, _PARAM_WRITES[0])
         if key != self._key:
-            self._planes = self._key = None  # (the old planes are freed before the new ones are allocated)
+            self.clear()  # (the old planes are freed before the new ones are allocated)
             self._planes = catalog_planes(E)
-            self._key = key
+            self._key, self._table = key, E.detach()
         return self._planes
 
     def clear(self):
-        self._planes = self._key = None
+        self._planes = self._key = self._table = None
 
 
 def _catalog_ws(n: int, d: int, dev) -> Tuple[torch.Tensor, int]:

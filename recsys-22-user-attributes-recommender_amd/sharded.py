@@ -284,6 +284,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         return st, own, compact, inv
 
     def training_step(self, batch, batch_idx):
+        self._catalog_planes.clear()  # (the evaluation's shard planes are stale from here on)
         originals = tuple(batch[k] for k in self._ID_KEYS)
         batch = self._ids_i64(batch, self._ID_KEYS)
         id_sets = [batch[k] for k in self._ID_KEYS]
