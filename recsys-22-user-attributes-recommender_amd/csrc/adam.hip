@@ -255,13 +255,18 @@ __device__ __forceinline__ void replay_steps(float2v (&P)[NP], float2v (&M)[NP],
                 __builtin_amdgcn_sched_barrier(0);  // (the loads first: their wait is the trip's end, after its work)
                 two(c0, c1);
             }
-            if (t < upto) {  // the last two steps (n0, n1 hold steps t and t + 1)
-                two(n0, n1);
-            } else if (t == upto) {  // or the last one
-                hp.neg_step_size = n0.x;
-                hp.inv_bc2_sqrt = n0.y;
+            // one, two or three steps are left (t + 3 > upto); n0, n1 hold steps t and t + 1
+            auto one = [&](const float2 c) {
+                hp.neg_step_size = c.x;
+                hp.inv_bc2_sqrt = c.y;
 #pragma unroll
                 for (int j = 0; j < NP; ++j) op(P[j], M[j], Vv[j], hp);
+            };
+            if (t < upto) {
+                two(n0, n1);
+                if (t + 2 == upto) one(lr[4 * upto]);
+            } else if (t == upto) {
+                one(n0);
             }
         };
         if (hp.wd != 0.f)
