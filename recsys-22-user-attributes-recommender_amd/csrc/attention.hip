@@ -90,10 +90,11 @@ __device__ __forceinline__ uint16_t* mask_keys(uint8_t* m, int64_t bh_total, int
 // key4..key4+3 with key4 = ks + 4g): the nibble for the dQ pass, and via ballots the key-major words
 // (one 8-byte store of 4 keys' words per lane group).
 __device__ __forceinline__ void store_drop_bits(uint8_t* __restrict__ nib, uint16_t* __restrict__ keyw, int bh,
-                                                int L, int qi, int q0, int ks, int g, int c16, const float4& f) {
+                                                int L, int qi, int q0, int ks, int g, int c16, const float4& f,
+                                                bool with_nib = true) {
     const int L4 = (L + 3) / 4;
     const int key4 = ks + 4 * g;
-    if (qi < L && key4 < L) nib[((int64_t)bh * L + qi) * L4 + key4 / 4] = keep_bits(f);
+    if (with_nib && qi < L && key4 < L) nib[((int64_t)bh * L + qi) * L4 + key4 / 4] = keep_bits(f);
     // bit 16g + c16 of each ballot: (key ks+4g+r, query q0+c16)
     const uint64_t b0 = __ballot(f.x != 0.f), b1 = __ballot(f.y != 0.f), b2 = __ballot(f.z != 0.f),
                    b3 = __ballot(f.w != 0.f);
@@ -676,7 +677,8 @@ template <int DK>
 __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
     int64_t ldv, float* __restrict__ o, int64_t ldo, float* __restrict__ stats, const uint8_t* __restrict__ key_valid,
-    int H, int L, int causal, float scale, float p_drop, uint64_t seed, uint8_t* __restrict__ drop_mask) {
+    int H, int L, int causal, float scale, float p_drop, uint64_t seed, uint8_t* __restrict__ drop_mask,
+    int with_nib) {
     constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int Lp = res_rows(L);
@@ -775,7 +777,7 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
                     // NS == 4 chunks start at multiples of 64 keys, so sub-tile pairs share a block
                     if (NS == 1 || (sub & 1) == 0) rnd = attn_philox(seed, drow, key4);
                     const float4 f = keep_from(rnd, (key4 >> 4) & 1, thr, kf);
-                    if (drop_mask) store_drop_bits(drop_mask, keyw, bh, L, qi, q0, k0 + sub * 16, g, c16, f);
+                    if (drop_mask) store_drop_bits(drop_mask, keyw, bh, L, qi, q0, k0 + sub * 16, g, c16, f, with_nib);
                     p[sub][0] *= f.x;
                     p[sub][1] *= f.y;
                     p[sub][2] *= f.z;
@@ -1268,6 +1270,16 @@ bool res_prepare(K kernel, size_t lds) {
                                (int)lds) == hipSuccess;
 }
 
+#ifndef ASME_ATTN_SKIP_NIB
+#define ASME_ATTN_SKIP_NIB 1  // 0: the forward always stores the keep nibbles (A/B)
+#endif
+// the family-0 backward runs the dS-storing resident pair (asme_attention_bwd_kernels' first branch)
+template <int DK>
+bool bwd_stores_ds(int L) {
+    return res_prepare(attn_bwd_dkdv_res_kernel<DK, true>, res_lds_bytes(L, DK, true)) &&
+           res_prepare(attn_bwd_dq_ds_kernel<DK>, ds_lds_bytes(L, DK));
+}
+
 #define ASME_DK_DISPATCH(DKV, ...)                                  \
     switch (DKV) {                                                  \
         case 16: { constexpr int DK = 16; __VA_ARGS__; } break;     \
@@ -1300,10 +1312,14 @@ ASME_API int asme_attention_fwd_kernels(int kernels, const float* q, const float
     const dim3 grid((unsigned)((seq_len + kQB - 1) / kQB), (unsigned)(batch * heads));
     const size_t lds = res_lds_bytes((int)seq_len, (int)head_dim, false);
     ASME_DK_DISPATCH(head_dim,
+        // the query-major keep nibbles are read only by the dQ passes that regenerate P (families 1 and 2, and family
+        // 0 when its dS-storing backward does not fit); the family-0 backward's dK/dV pass reads the key-major words
+        // and its dQ pass the stored dS -- so this forward stores the nibbles only when some backward will read them
+        const int with_nib = !(kernels == 0 && ASME_ATTN_SKIP_NIB && bwd_stores_ds<DK>((int)seq_len));
         if (kernels != 1 && res_prepare(attn_fwd_res_kernel<DK>, lds))
             hipLaunchKernelGGL(attn_fwd_res_kernel<DK>, dim3((unsigned)(batch * heads)), dim3(kResThreads), lds,
                                (hipStream_t)stream, q, k, v, ld_q, ld_k, ld_v, out, ld_out, lse, key_valid,
-                               (int)heads, (int)seq_len, causal, scale, p_drop, seed, drop_mask);
+                               (int)heads, (int)seq_len, causal, scale, p_drop, seed, drop_mask, with_nib);
         else
             hipLaunchKernelGGL(attn_fwd_kernel<DK>, grid, dim3(256), 0, (hipStream_t)stream, q, k, v, ld_q, ld_k,
                                ld_v, out, ld_out, lse, key_valid, (int)heads, (int)seq_len, causal, scale, p_drop,
