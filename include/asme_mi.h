@@ -130,8 +130,9 @@ int asme_gelu_dropout_bwd(const float* x, const float* dy, int64_t n, float p, u
  * stride ld_out; lse (batch*heads, seq_len, 2) = (row max, 1/row sum of exp) of the scaled, masked
  * scores (kept separate so a row with no admissible key keeps its exact 1/L weights).
  * head_dim in {16, 32, 64, 128}; seq_len <= 1024.  drop_mask (nullable; asme_attention_dropout_mask_bytes()
- * bytes): the forward records the dropout decisions (query-major nibbles + key-major 16-bit words) which
- * the backward then reads instead of regenerating them. */
+ * bytes): the forward records the dropout decisions (key-major 16-bit words, and query-major nibbles when the
+ * backward's dQ pass will read them -- not when the resident backward stores dS) which the backward then reads instead
+ * of regenerating them: an opaque record for the backward of the same shape and kernel family. */
 int asme_attention_fwd(const float* q, const float* k, const float* v, int64_t ld_q, int64_t ld_k, int64_t ld_v,
                        const uint8_t* key_valid, int64_t batch, int64_t heads, int64_t seq_len, int64_t head_dim,
                        int causal, float scale, float p_drop, uint64_t seed, float* out, int64_t ld_out, float* lse,
@@ -149,7 +150,8 @@ int asme_attention_bwd(const float* q, const float* k, const float* v, int64_t l
  * entry points above always run family 0): 0 = automatic (one workgroup per (batch, head) with the head's operands
  * resident in LDS whenever 2*ceil(L/16)*16*(dk+4)*4 B fits 160 KiB, else the 64-row streaming kernels; the resident
  * backward runs dK/dV first, storing dS, then dQ = dS K), 1 = streaming kernels only, 2 = resident kernels with a
- * dQ pass that recomputes S and dP.  No process-wide state. */
+ * dQ pass that recomputes S and dP.  No process-wide state.  A drop_mask is read only by the backward of the family
+ * whose forward wrote it. */
 int asme_attention_fwd_kernels(int kernels, const float* q, const float* k, const float* v, int64_t ld_q,
                                int64_t ld_k, int64_t ld_v, const uint8_t* key_valid, int64_t batch, int64_t heads,
                                int64_t seq_len, int64_t head_dim, int causal, float scale, float p_drop, uint64_t seed,
