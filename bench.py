@@ -205,6 +205,11 @@ def parse():
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--table-grad", choices=["sparse", "dense"], default="sparse")
+    ap.add_argument("--main-stream", choices=["default", "high"], default="default",
+                    help="run the training steps on a high-priority stream (producer side streams keep the default)")
+    ap.add_argument("--ids-ahead", choices=["on", "mid", "off"], default="on",
+                    help="SASRec (unsharded): produce the next batch and its table-id dedup / occurrence CSR on a "
+                         "side stream during the current step (off: inline, the A/B form)")
     ap.add_argument("--ids", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--kernel-events", choices=["on", "off"], default="on",
                     help="HIP events around the timed kernels (off: no per-kernel rooflines; for A/B of their cost)")
@@ -646,6 +651,34 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
 
         def run(j, i):
             step_fn(None, i, j)
+    elif args.producer == "gpu" and args.ids_ahead != "off":
+        # the next batch is produced on a side stream during this step -- the pos / neg sampler, then the id-only
+        # half of its table plan (dedup + occurrence CSR, module.prefetch -> ops.TableIdsAhead) -- the way the masked
+        # legs produce theirs; the step's training_step waits for it.  No prefetch across the warm-up / timed
+        # boundary or past the last timed step: the timed region produces and applies exactly K batches.
+        side = torch.cuda.Stream(dev)
+        ahead = {}
+        last = args.warmup + args.steps - 1
+
+        def produce_next(j):
+            if j < last and j != args.warmup - 1:
+                with torch.cuda.stream(side):
+                    nb = ahead[j + 1] = get_batch(j + 1)
+                    module.prefetch(nb)
+
+        def run(j, i):
+            b = ahead.pop(j, None)
+            if b is None:
+                b = get_batch(j)
+            if args.ids_ahead == "mid":  # (A/B form: the side work enqueued after this step's forward)
+                loss = module.training_step(b, i)["loss"]
+                produce_next(j)
+                asme.modules.backward(loss)
+                opt.step()
+                opt.zero_grad(set_to_none=True)
+                return
+            step_fn(b, i)
+            produce_next(j)
     else:
         def run(j, i):
             step_fn(get_batch(j), i)
@@ -803,12 +836,14 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
                    "batch_per_gpu": B, "seq_len": L, "items": args.items, "dim": d, "heads": args.heads,
                    "layers": args.layers, "dropout": args.dropout, "table_grad": args.table_grad,
                    "ids": ids_kind, "producer": args.producer,
+                   "ids_ahead": (args.ids_ahead if args.producer == "gpu" and not sharded else "off"),
                    "parallelism": f"dp{world}+rowshard{world}" if sharded else "single"},
         "roofline": roof,
         "rooflines": rooflines,
         "flush_ms": round(flush_ms, 3),
         # diagnostic: median host time to issue one step's launches (the GPU runs behind the host when it is smaller)
         "host_issue_ms": round(1000 * sorted(host_s)[len(host_s) // 2], 3),
+        "ids_ahead_hits": getattr(module, "ids_ahead_hits", 0),
         "cpu_baseline": None,
     }
     if eval_leg is not None:
@@ -918,6 +953,8 @@ def main():
         else:
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
+    if args.main_stream == "high":
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
     asme = __graft_entry__.load_package()
     V = args.items + 3
     B, L, d = args.batch, args.seq_len, args.dim

@@ -105,6 +105,9 @@ class _TableGradMixin:
                              "use table_grad='dense'")
         self.table_grad = mode
         self._slot_map = None
+        self._spare_map = None   # the second slot map of the ids-ahead path (prefetch_table_ids)
+        self._ids_ahead = None   # ops.TableIdsAhead of the next training step's ids
+        self.ids_ahead_hits = 0  # training steps that took a dedup made ahead (tests assert the overlap ran)
         # the catalogue's bf16 planes for fused evaluation, split once per validation pass (ops.CatalogPlanes)
         self._catalog_planes = ops.CatalogPlanes()
 
@@ -117,7 +120,15 @@ class _TableGradMixin:
         if table is None or not table.requires_grad:
             return
         if self._slot_map is None or self._slot_map.device != table.device:
-            self._slot_map = torch.full((table.shape[0],), -1, dtype=torch.int32, device=table.device)
+            self._slot_map = ops.new_slot_map(table.shape[0], table.device)
+            self._spare_map = None
+        ahead, self._ids_ahead = self._ids_ahead, None
+        if ahead is not None and not ahead.matches(id_sets):
+            ahead.discard()  # prefetched for other tensors: its map entries reset, the dedup runs inline below
+            ahead = None
+        if ahead is not None:  # its dedup used the spare map: that becomes this plan's map
+            self._slot_map, self._spare_map = self._spare_map, self._slot_map
+            self.ids_ahead_hits += 1
         tg = table._asme_table_grad
         if tg.plan is not None and not tg.plan.consumed:
             if tg.plan.has_gradient():
@@ -130,7 +141,27 @@ class _TableGradMixin:
                                    "dropped by optimizer.zero_grad()); use table_grad='dense' for gradient "
                                    "accumulation")
             tg.plan.release()  # a forward without a backward: nothing to lose
-        tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map)
+        tg.plan = ops.SparseTablePlan(table, id_sets, self._slot_map, ahead=ahead)
+
+    def _prefetch_table_ids(self, id_sets):
+        """the next training step's table-id dedup + occurrence CSR, enqueued now on the CURRENT stream (a producer's
+        side stream) over the spare slot map -- see ops.TableIdsAhead.  The next training_step must receive the
+        very same id tensors (else the prefetch is discarded and the dedup runs inline); it makes the training
+        stream wait for this stream's work itself."""
+        if self.table_grad != "sparse" or not self.training:
+            return
+        table = self.model.item_table()
+        if table is None or not table.requires_grad or not table.is_cuda:
+            return
+        if self._ids_ahead is not None:
+            self._ids_ahead.discard()
+            self._ids_ahead = None
+        if self._slot_map is None or self._slot_map.device != table.device:
+            self._slot_map = ops.new_slot_map(table.shape[0], table.device)
+            self._spare_map = None
+        if self._spare_map is None:
+            self._spare_map = ops.new_slot_map(table.shape[0], table.device)
+        self._ids_ahead = ops.TableIdsAhead(table.shape[0], table.shape[1], id_sets, self._spare_map)
 
     @staticmethod
     def _ids_i64(batch, keys):
@@ -180,6 +211,18 @@ class SequenceNextItemPredictionTrainingModule(_TableGradMixin, _Base):
         loss = self.loss_function(pos_logits, neg_logits, mask=item_mask)
         self.log(LOG_KEY_TRAINING_LOSS, loss)
         return {"loss": loss}
+
+    _ID_KEYS = (ITEM_SEQ_ENTRY_NAME, POSITIVE_SAMPLES_ENTRY_NAME, NEGATIVE_SAMPLES_ENTRY_NAME)
+
+    def prefetch(self, batch):
+        """Dedup the NEXT training step's table ids (sequence, positives, negatives) and build their occurrence CSR
+        now, on the current stream -- the stream that produced `batch`, one step ahead (the reference's DataLoader
+        workers run a batch ahead the same way).  The next training_step must receive this batch's very id
+        tensors (int64, contiguous: as the GPU producer writes them); it waits for this stream's work itself."""
+        ids = [batch[k] for k in self._ID_KEYS]
+        if any(t.dtype != torch.int64 or not t.is_contiguous() for t in ids):
+            return  # (training_step would normalise them into other tensors: nothing to match)
+        self._prefetch_table_ids(ids)
 
     def predict_step(self, batch, batch_idx, dataloader_idx: Optional[int] = None) -> torch.Tensor:
         self._flush_table()

@@ -1,8 +1,8 @@
 """Autograd wrappers over the gfx950 HIP kernels (libasme_mi.so).
 
 Each Function here replaces a chain of stock PyTorch ops of the reference (cited per Function) with
-one or two hand-written kernels.  Plain library GEMMs (the Linear projections) stay on PyTorch's
-hipBLASLt path; everything around them is fused here.
+one or two hand-written kernels; the Linear projections run on the package's own weight-stationary GEMM
+(csrc/wsgemm.hip) and split-T weight-gradient GEMM (csrc/gemm.hip), no library GEMM.
 
 Dropout: every call with p > 0 draws a fresh 64-bit seed from torch's default CPU generator; the
 kernels derive the mask from (seed, element index) with Philox, so the backward regenerates it.
@@ -163,35 +163,109 @@ class LazyTableState:
         self.catch_up(None)
 
 
+_MAP_FREE = {}  # slot map data_ptr -> the event after which its entries are all -1 again (TableIdsAhead waits on it)
+
+
+def _note_map_free(slot_map: torch.Tensor):
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(slot_map.device))
+    _MAP_FREE[slot_map.data_ptr()] = ev
+
+
+def new_slot_map(rows: int, device) -> torch.Tensor:
+    """a (rows,) int32 dedup slot map, -1 at rest; its fill is recorded as the point from which another stream's
+    dedup (TableIdsAhead) may use it"""
+    m = torch.full((rows,), -1, dtype=torch.int32, device=device)
+    if m.is_cuda:
+        _note_map_free(m)
+    return m
+
+
+class TableIdsAhead:
+    """The id-only half of a step's SparseTablePlan -- the dedup of its table ids (asme_dedup_ids_segments) and the
+    occurrence CSR of the table gradient (asme_occurrence_csr) -- enqueued on the CURRENT stream (a producer's side
+    stream) a step ahead.  Neither depends on the table's values, only on the ids, so they run beside the previous
+    step's kernels instead of in front of the next step's; the table-dependent half (staging the rows through the
+    lazy Adam) stays with SparseTablePlan on the training stream.  `slot_map` must not be the map of a plan that
+    is still live (the module alternates two); the dedup waits for the event of that map's last release
+    (_note_map_free), so it never sees a previous plan's entries."""
+
+    def __init__(self, vocab: int, dim: int, id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor):
+        cur = torch.cuda.current_stream(slot_map.device)
+        ev = _MAP_FREE.get(slot_map.data_ptr())
+        if ev is not None:
+            cur.wait_event(ev)
+        self.id_sets = list(id_sets)
+        self.keys = [(x.data_ptr(), tuple(x.shape)) for x in id_sets]
+        self.plan = SparseTablePlan(None, id_sets, slot_map, vocab=vocab, dim=dim)
+        self.plan._csr = self.plan._occurrence_csr() if self.plan.capacity > 0 else None
+        self.ready = torch.cuda.Event()
+        self.ready.record(cur)
+
+    def matches(self, id_sets: Sequence[torch.Tensor]) -> bool:
+        return [(x.data_ptr(), tuple(x.shape)) for x in id_sets] == self.keys
+
+    def tensors(self):
+        p = self.plan
+        out = [p.unique, p.count, p._flat_inverse] + list(self.id_sets)
+        if p._csr is not None:
+            out += [t for t in p._csr[:4]]
+        return out
+
+    def adopt(self):
+        """make the current stream wait for the work of the ahead stream and keep its tensors alive for this stream
+        (the caching allocator returns them to the side stream's pool only after this stream's reads)"""
+        cur = torch.cuda.current_stream(self.plan.unique.device)
+        cur.wait_event(self.ready)
+        for t in self.tensors():
+            t.record_stream(cur)
+
+    def discard(self):
+        """an ahead plan that no step will take: its slot map entries reset (on the current stream, after it)"""
+        self.adopt()
+        self.plan.release()
+
+
 class SparseTablePlan:
     """Per-step dedup of every id that touches the table: slot map, unique rows, compact grad."""
 
     def __init__(self, table: Optional[torch.Tensor], id_sets: Sequence[torch.Tensor], slot_map: torch.Tensor,
-                 vocab: Optional[int] = None, dim: int = 0):
+                 vocab: Optional[int] = None, dim: int = 0, ahead: Optional[TableIdsAhead] = None):
+        """ahead: the dedup and occurrence CSR of exactly these id tensors, computed a step ahead on another stream
+        (TableIdsAhead, over `slot_map`): taken over instead of running them here"""
         dev = slot_map.device
         tg = getattr(table, "_asme_table_grad", None) if table is not None else None
         if tg is not None:
             tg.drop_applied()  # the previous step's plan still marks the shared slot map
-        # the id sets are read in place as segments of one occurrence list (no concatenated copy)
-        segs = [_i64(x).reshape(-1) for x in id_sets]
-        segs = [x if x.is_contiguous() else x.contiguous() for x in segs]
-        if len(segs) > 4:
-            segs = [torch.cat(segs)]
-        n = sum(x.numel() for x in segs)
         self.vocab, self.dim = table.shape if table is not None else (vocab, dim)
         self.slot_map = slot_map
-        self.unique = torch.empty(n, device=dev, dtype=torch.int64)
-        inverse = torch.empty(n, device=dev, dtype=torch.int64)
-        # (asme_dedup_ids always writes the count)
-        self.count = torch.empty(1, device=dev, dtype=torch.int32) if n > 0 else torch.zeros(1, device=dev,
-                                                                                          dtype=torch.int32)
-        if n > 0:
-            ws_bytes = int(_lib.load().asme_dedup_workspace_bytes(n))
-            ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
-            k = len(segs)
-            call("asme_dedup_ids_segments", k, (ctypes_vp * k)(*[x.data_ptr() for x in segs]),
-                 (ctypes_i64 * k)(*[x.numel() for x in segs]), self.vocab, ptr(slot_map), ptr(ws), ws_bytes,
-                 ptr(self.unique), ptr(inverse), ptr(self.count), stream())
+        self._csr = None
+        if ahead is not None:
+            if ahead.plan.slot_map is not slot_map or not ahead.matches(id_sets):
+                raise ValueError("SparseTablePlan: the ahead dedup is of other ids or another slot map")
+            ahead.adopt()
+            n = ahead.plan.capacity
+            self.unique, inverse, self.count = ahead.plan.unique, ahead.plan._flat_inverse, ahead.plan.count
+            self._csr = ahead.plan._csr
+        else:
+            # the id sets are read in place as segments of one occurrence list (no concatenated copy)
+            segs = [_i64(x).reshape(-1) for x in id_sets]
+            segs = [x if x.is_contiguous() else x.contiguous() for x in segs]
+            if len(segs) > 4:
+                segs = [torch.cat(segs)]
+            n = sum(x.numel() for x in segs)
+            self.unique = torch.empty(n, device=dev, dtype=torch.int64)
+            inverse = torch.empty(n, device=dev, dtype=torch.int64)
+            # (asme_dedup_ids always writes the count)
+            self.count = torch.empty(1, device=dev, dtype=torch.int32) if n > 0 else torch.zeros(1, device=dev,
+                                                                                              dtype=torch.int32)
+            if n > 0:
+                ws_bytes = int(_lib.load().asme_dedup_workspace_bytes(n))
+                ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+                k = len(segs)
+                call("asme_dedup_ids_segments", k, (ctypes_vp * k)(*[x.data_ptr() for x in segs]),
+                     (ctypes_i64 * k)(*[x.numel() for x in segs]), self.vocab, ptr(slot_map), ptr(ws), ws_bytes,
+                     ptr(self.unique), ptr(inverse), ptr(self.count), stream())
         self.capacity = n
         self._slots_mapped = False
         self.grad_scale = 1.0  # factor on every reduced gradient row (the sharded owner: 1/W, DDP averaging)
@@ -230,6 +304,7 @@ class SparseTablePlan:
 
     _distinct = False
     accumulate = False
+    _csr = None  # (order, slot, seg_off, parts, part_bytes) once built (ahead, or by the first reduction)
 
     def has(self, ids: torch.Tensor) -> bool:
         return (ids.data_ptr(), tuple(ids.shape)) in (self._offset if self._distinct else self._inverse)
@@ -313,6 +388,7 @@ class SparseTablePlan:
         if not self._distinct or other.capacity == 0 or other._grad_rows is not None:
             raise RuntimeError("adopt_contributions: a distinct plan taking an unreduced plan over its slots")
         self._flat_inverse = other._flat_inverse
+        self._csr = None  # (over the adopted occurrences)
         self.capacity = other.capacity  # occurrences (>= slots): the CSR's length; count stays the slot count
         self._contrib = other._contrib
         other._contrib = []
@@ -339,6 +415,8 @@ class SparseTablePlan:
         self._contrib.append((self._offset[key], ids.numel(), rows, scale))
 
     def _occurrence_csr(self):
+        if self._csr is not None:
+            return self._csr
         n = self.capacity
         dev = self.unique.device
         lib = _lib.load()
@@ -353,7 +431,8 @@ class SparseTablePlan:
              ptr(seg_off), stream())
         part_bytes = int(lib.asme_table_grad_workspace(n, self.dim))
         parts = torch.empty(max(part_bytes, 4) // 4, device=dev, dtype=torch.float32)
-        return order, slot, seg_off, parts, part_bytes
+        self._csr = (order, slot, seg_off, parts, part_bytes)
+        return self._csr
 
     @staticmethod
     def _contrib_arrays(part):
@@ -449,6 +528,8 @@ class SparseTablePlan:
         # (a distinct plan's map holds entries only once row_slot_map() wrote them)
         if self.slot_map is not None and (self._slots_mapped or not self._distinct):
             call("asme_dedup_reset", ptr(self.unique), ptr(self.count), self.capacity, ptr(self.slot_map), stream())
+            if self.slot_map.data_ptr() in _MAP_FREE:  # a map another stream's dedup may use next (TableIdsAhead)
+                _note_map_free(self.slot_map)
         self.consumed = True
 
 
