@@ -343,6 +343,7 @@ int64_t super_tiles(int64_t N, int64_t K) {
 }
 
 Plan make_plan(int64_t T, int64_t N, int64_t K) {
+    if (T <= 0 || N <= 0 || K <= 0) return {0, kTT};  // (no chunk; the entry points reject the shape)
     const int64_t tiles = super_tiles(N, K);
     // one workgroup per CU (96 or 144 KiB of LDS each): chunks a multiple of 8 (one per XCD lane), tiles x chunks
     // <= 256
@@ -373,6 +374,8 @@ hipError_t launch_weight_grad(dim3 grid, hipStream_t s, const float* dy, int64_t
 }  // namespace
 
 ASME_API int64_t asme_linear_weight_grad_workspace(int64_t n_tokens, int64_t out_features, int64_t in_features) {
+    if (n_tokens < 0 || out_features <= 0 || in_features <= 0 || out_features > (1 << 20) || in_features > (1 << 20))
+        return 0;
     const Plan p = make_plan(n_tokens, out_features, in_features);
     return p.nchunks * (out_features * in_features + out_features) * (int64_t)sizeof(float);
 }
@@ -382,6 +385,9 @@ ASME_API int asme_linear_weight_grad(const float* dy, int64_t ld_dy, const float
                                      int64_t out_features, int64_t in_features, float* workspace,
                                      int64_t workspace_bytes, float* dw, float* db, int accumulate, void* stream) {
     ASME_CHECK_ARG(dy && x && workspace && dw, "asme_linear_weight_grad: null pointer");
+    ASME_CHECK_ARG(n_tokens >= 0 && out_features > 0 && in_features > 0 && out_features <= (1 << 20) &&
+                       in_features <= (1 << 20) && ld_dy >= out_features && ld_x >= in_features,
+                   "asme_linear_weight_grad: bad sizes");
     ASME_CHECK_ARG(out_features % 4 == 0 && in_features % 4 == 0 && ld_dy % 4 == 0 && ld_x % 4 == 0 &&
                        ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0,
                    "asme_linear_weight_grad: features / strides must be multiples of 4 floats, 16-B aligned");
