@@ -80,8 +80,23 @@ __device__ __forceinline__ float4 bits_keep(uint8_t m, float p) {
 // [4*ceil(L/4) keys], bit i of word (j, key) = query 16j+i kept.  It follows the nibble image, 256-B aligned.
 __host__ __device__ inline int64_t mask_nibble_bytes(int64_t bh, int L) { return bh * L * ((L + 3) / 4); }
 __host__ __device__ inline int mask_key_stride(int L) { return 4 * ((L + 3) / 4); }
-__host__ __device__ inline int64_t mask_total_bytes(int64_t bh, int L) {
-    return ((mask_nibble_bytes(bh, L) + 255) & ~(int64_t)255) + bh * ((L + 15) / 16) * mask_key_stride(L) * 2;
+__host__ __device__ inline int64_t mask_tag_offset(int64_t bh, int L) {
+    return (((mask_nibble_bytes(bh, L) + 255) & ~(int64_t)255) + bh * ((L + 15) / 16) * mask_key_stride(L) * 2 + 255) &
+           ~(int64_t)255;
+}
+// + a 16-B tag after the key-major words: the forward records whether it stored the query-major nibbles
+// (kMaskTagNib) or skipped them because the family-0 backward reads only the key words and the stored dS
+// (kMaskTagNoNib); the nibble-reading dQ passes check it and write NaN instead of a dQ from unwritten bits
+__host__ __device__ inline int64_t mask_total_bytes(int64_t bh, int L) { return mask_tag_offset(bh, L) + 16; }
+constexpr uint32_t kMaskTagNib = 0x3142494Eu, kMaskTagNoNib = 0x3042494Eu;
+__device__ __forceinline__ void mask_tag_write(uint8_t* m, int64_t bh_total, int L, bool with_nib) {
+    *reinterpret_cast<uint32_t*>(m + mask_tag_offset(bh_total, L)) = with_nib ? kMaskTagNib : kMaskTagNoNib;
+}
+// the factor a nibble-reading dQ pass scales its output by: `scale`, or NaN when the forward skipped the nibbles
+__device__ __forceinline__ float dq_out_scale(const uint8_t* m, int64_t bh_total, int L, float p_drop, float scale) {
+    if (!m || !(p_drop > 0.f)) return scale;
+    const uint32_t tag = *reinterpret_cast<const uint32_t*>(m + mask_tag_offset(bh_total, L));
+    return tag == kMaskTagNib ? scale : __builtin_nanf("");
 }
 __device__ __forceinline__ uint16_t* mask_keys(uint8_t* m, int64_t bh_total, int L) {
     return reinterpret_cast<uint16_t*>(m + ((mask_nibble_bytes(bh_total, L) + 255) & ~(int64_t)255));
@@ -245,6 +260,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
     const int qblk = blockIdx.x * kQB;
     const int qi = qblk + wave * 16 + c16;  // this lane's query row (C/D column)
     const int64_t tok0 = (int64_t)b * L;
+    if (drop_mask && p_drop > 0.f && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        mask_tag_write(drop_mask, gridDim.y, L, true);
 
     bool any_valid;
     int last_valid;
@@ -462,11 +479,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
         cols_times_weights<DK>(Ks, g, c16, ds, acc);  // dQ^T += K^T dS^T
     }
     if (qok) {
+        const float os = dq_out_scale(drop_mask, gridDim.y, L, p_drop, scale);
         float* row = dq + (tok0 + qi) * lddq + h * DK;
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct)
             *reinterpret_cast<float4*>(row + ct * 16 + 4 * g) =
-                make_float4(acc[ct][0] * scale, acc[ct][1] * scale, acc[ct][2] * scale, acc[ct][3] * scale);
+                make_float4(acc[ct][0] * os, acc[ct][1] * os, acc[ct][2] * os, acc[ct][3] * os);
     }
 }
 
@@ -691,6 +709,8 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
     const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
     const int64_t tok0 = (int64_t)b * L;
     const float* qh = q + tok0 * ldq + h * DK;
+    if (drop_mask && p_drop > 0.f && blockIdx.x == 0 && threadIdx.x == 0)
+        mask_tag_write(drop_mask, gridDim.x, L, with_nib != 0);
 
     stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
     if (ASME_ATTN_DIAG != 1)
@@ -899,11 +919,12 @@ __global__ __launch_bounds__(kResThreads) void attn_bwd_dq_res_kernel(
         for (; c0 + kNS <= nsub; c0 += kNS) chunk(std::integral_constant<int, kNS>{}, c0 * 16);
         for (; c0 < nsub; ++c0) chunk(std::integral_constant<int, 1>{}, c0 * 16);
         if (qok) {
+            const float os = dq_out_scale(drop_mask, gridDim.x, L, p_drop, scale);
             float* row = dq + (tok0 + qi) * lddq + h * DK;
 #pragma unroll
             for (int ct = 0; ct < NCT; ++ct)
                 *reinterpret_cast<float4*>(row + ct * 16 + 4 * g) =
-                    make_float4(acc[ct][0] * scale, acc[ct][1] * scale, acc[ct][2] * scale, acc[ct][3] * scale);
+                    make_float4(acc[ct][0] * os, acc[ct][1] * os, acc[ct][2] * os, acc[ct][3] * os);
         }
     }
 }

@@ -141,6 +141,7 @@ struct LogitsArgs {
     const float* tscore;     // rank: the target's score per query (from the tscore pass: the same products)
     int32_t* counts;         // rank: per query, items ranked above the target (atomically summed over chunks)
     int64_t id_stride, id_offset;
+    int64_t tclamp;          // rank: > 0: a target outside [0, tclamp) counts as item 0 (as gather_targets_kernel reads it)
     int64_t sblocks, per_xcd;  // set by launch_engine: the grid's work items and work items per XCD slot group
 };
 
@@ -261,9 +262,14 @@ __global__ __launch_bounds__(W * 64) void logits_engine_kernel(LogitsArgs a) {
     int r_jeq = -1, r_jlt = 0, r_cnt = 0;
     if (MODE == M_RANK && srow < a.n_stat) {
         r_ts = a.tscore[srow];
-        const int64_t rel = a.targets[srow] - a.id_offset;
-        r_jeq = (rel >= 0 && rel % a.id_stride == 0) ? (int)(rel / a.id_stride) : -1;
-        r_jlt = rel > 0 ? (int)((rel + a.id_stride - 1) / a.id_stride) : 0;
+        int64_t tg = a.targets[srow];
+        if (a.tclamp > 0 && (tg < 0 || tg >= a.tclamp)) tg = 0;  // the id whose score tscore holds
+        // (64-bit until clamped to this shard's rows: any target id, valid or not, gives 32-bit row numbers)
+        const int64_t rel = tg - a.id_offset;
+        const int64_t jq = rel >= 0 ? rel / a.id_stride : -1;
+        r_jeq = (rel >= 0 && rel % a.id_stride == 0 && jq < a.n_strm) ? (int)jq : -1;
+        const int64_t jl = rel > 0 ? (rel + a.id_stride - 1) / a.id_stride : 0;
+        r_jlt = (int)(jl < a.n_strm ? jl : a.n_strm);
     }
     floatx16 y[NFT];  // gradient product: Y^T[feature 32 ft + acc_row(i, h)][stationary row r32]
 #pragma unroll
@@ -1689,7 +1695,7 @@ int target_scores_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, cons
 
 int count_above_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const void* E_planes, int64_t V,
                    const float* bias, const int64_t* targets, const float* tscore, int64_t id_stride,
-                   int64_t id_offset, int32_t* counts, char* w, hipStream_t s) {
+                   int64_t id_offset, int64_t tclamp, int32_t* counts, char* w, hipStream_t s) {
     __bf16* hp = reinterpret_cast<__bf16*>(w);
     int rc = split(H, ld_h, nq, (int)dim, hp, s);
     if (rc != 0) return rc;
@@ -1712,6 +1718,7 @@ int count_above_x6(const float* H, int64_t ld_h, int64_t nq, int64_t dim, const 
     a.counts = counts;
     a.id_stride = id_stride;
     a.id_offset = id_offset;
+    a.tclamp = tclamp;
     return launch_kb<M_RANK>(a, p.sblocks, s);
 }
 }  // namespace
@@ -1743,7 +1750,7 @@ ASME_API int asme_catalog_count_above_x6(const float* H, int64_t ld_h, int64_t n
                    "asme_catalog_count_above_x6: bad shape");
     ASME_CHECK_ARG(ws_bytes >= asme_catalog_x6_workspace(nq, dim), "asme_catalog_count_above_x6: workspace too small");
     if (nq == 0) return 0;
-    const int rc = count_above_x6(H, ld_h, nq, dim, E_planes, V, bias, targets, tscore, id_stride, id_offset, counts,
+    const int rc = count_above_x6(H, ld_h, nq, dim, E_planes, V, bias, targets, tscore, id_stride, id_offset, 0, counts,
                                   reinterpret_cast<char*>(workspace), (hipStream_t)stream);
     if (rc != 0) return rc;
     ASME_LAUNCH_CHECK("asme_catalog_count_above_x6");
@@ -1770,7 +1777,7 @@ ASME_API int asme_catalog_rank_x6(const float* H, int64_t ld_h, int64_t nq, int6
                        targets, nq, (int)dim, rows, tbias);
     int rc = target_scores_x6(H, ld_h, nq, dim, rows, dim, bias ? tbias : nullptr, tscore, w, s);
     if (rc == 0)
-        rc = count_above_x6(H, ld_h, nq, dim, E_planes, V, bias, targets, tscore, 1, 0, counts_ws, w, s);
+        rc = count_above_x6(H, ld_h, nq, dim, E_planes, V, bias, targets, tscore, 1, 0, V, counts_ws, w, s);
     if (rc != 0) return rc;
     hipLaunchKernelGGL(rank_from_counts_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, counts_ws, nq,
                        ranks);

@@ -102,11 +102,9 @@ class GradientAllReduce:
             yield
         finally:
             self._sync = prev
-            # a row-sparse table gradient of these passes cannot be merged with the next one: mark its plan, so the
-            # next training_step raises instead of dropping it (modules._TableGradMixin._plan_table)
-            tg = getattr(self.table, "_asme_table_grad", None) if self.table is not None else None
-            if tg is not None and tg.plan is not None and tg.plan.has_gradient():
-                tg.plan.accumulate = True
+            # (a row-sparse table gradient of these passes cannot be merged with the next one: the next
+            # training_step finds its plan holding a gradient -- SparseTablePlan.has_gradient() -- and raises
+            # instead of dropping it, modules._TableGradMixin._plan_table)
 
     def _ready(self, p: torch.nn.Parameter):
         if not self._sync:

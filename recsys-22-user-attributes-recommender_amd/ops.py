@@ -92,6 +92,7 @@ class LazyTableState:
         self.hist = torch.zeros(1024, 8, dtype=torch.float32, device=param.device)
         self.step = 0
         self.rest = False  # some rows may be at rest (last_step == REST_STEP)
+        self._current_at = None  # the step every row is known to be current at (a full catch-up), else None
 
     def start(self, step: int, fresh: bool, wd: float, rest_rows: bool = True):
         """every row is current up to `step`; `fresh` (moments just created, all +0) without weight decay: every row
@@ -101,6 +102,7 @@ class LazyTableState:
         self.step = step
         self.rest = bool(rest_rows and fresh and wd == 0.0)
         self.last_step.fill_(REST_STEP if self.rest else step)
+        self._current_at = step
 
     def record(self, step: int, lr, b1, b2, eps, wd):
         if wd != 0.0 and self.rest:  # rows at rest are current up to the previous step; from now on they decay
@@ -121,7 +123,11 @@ class LazyTableState:
             return
         V, D = self.param.shape
         if rows is None:
+            if self._current_at == self.step:
+                return  # every row is current already (a second flush, an evaluation after one): nothing to replay
+            self._current_at = self.step
             cap = V
+        note_param_write()  # (writes table rows behind torch's version counter: cached catalogue planes are stale)
         call("asme_lazy_adam_catch_up", ptr(rows), ptr(count), cap, ptr(self.last_step), ptr(self.param),
              ptr(self.exp_avg), ptr(self.exp_avg_sq), D, ptr(self.hist), self.hist.shape[0], self.step, stream())
 
@@ -282,7 +288,6 @@ class SparseTablePlan:
             self._offset[key] = off
             off += k
         self.consumed = False
-        self.accumulate = False  # set when a backward into this plan ran for gradient accumulation (no_sync)
         # (3, capacity, d) param / moments of unique[s] brought up to date, or None: the step's readers take
         # `rows` + `gather_ids(ids)` instead of the table (see LazyTableState.stage)
         self.staged: Optional[torch.Tensor] = None
@@ -303,7 +308,6 @@ class SparseTablePlan:
         return table, ids
 
     _distinct = False
-    accumulate = False
     _csr = None  # (order, slot, seg_off, parts, part_bytes) once built (ahead, or by the first reduction)
 
     def has(self, ids: torch.Tensor) -> bool:

@@ -170,6 +170,59 @@ def test_catalog_rank_equals_rank_of_materialised_scores(asme, dev, nq, V, d, wi
     assert torch.equal(r2, want2)
 
 
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_catalog_rank_far_ties_and_invalid_targets(asme, dev, with_bias):
+    """Exact ties on the branch-free clean path (logits.hip M_RANK: a 32-row sub-tile holding neither the target's
+    row nor its lower-id boundary compares with s_t, or with the float just below s_t): every target's row is copied
+    5,000 rows above it and 6,000 rows below it -- other sub-tiles and chunks, one tie of a higher and one of a lower
+    id -- for positive and negative target scores (queries h and -h).  The ranks equal those read off the
+    materialised scores, unsharded (asme_catalog_rank_x6) and through the sharded count (asme_catalog_count_above_x6
+    over W = 3 cyclic shards, id_stride 3, id_offset r).  Targets -1 and V rank as item 0 (the score gather clamps
+    them to item 0, and so does the rank test)."""
+    torch.manual_seed(17 + with_bias)
+    V, d, nq = 27003, 128, 512
+    H = torch.randn(nq // 2, d, device=dev)
+    H = torch.cat([H, -H])
+    E = torch.randn(V, d, device=dev) / d ** 0.5
+    b = torch.randn(V, device=dev) if with_bias else None
+    targets = torch.randint(10000, 12000, (nq,), device=dev)
+    E2, b2 = E.clone(), (b.clone() if b is not None else None)
+    for off in (5000, -6000):
+        E2[targets + off] = E[targets]
+        if b2 is not None:
+            b2[targets + off] = b[targets]
+    S = asme.ops.logits(H, E2, b2)
+    ids = torch.arange(V, device=dev)[None, :]
+
+    def want_of(tg):
+        st = S.gather(1, tg[:, None])
+        return 1 + ((S > st) | ((S == st) & (ids < tg[:, None]))).sum(1)
+
+    want = want_of(targets)
+    st = S.gather(1, targets[:, None])[:, 0]
+    assert bool((st > 0).any()) and bool((st < 0).any())
+    ties = ((S == st[:, None]).sum(1) - 1)
+    assert int((ties >= 2).sum()) >= nq * 0.9  # the copies really tie (up and down)
+    assert torch.equal(asme.ops.catalog_rank(H, E2, targets, b2), want)
+    # sharded: W = 3 cyclic shards (row g on rank g % 3), counts summed, target scores from the target rows
+    tscore = asme.ops.catalog_target_scores(H, E2.index_select(0, targets),
+                                             b2.index_select(0, targets) if b2 is not None else None)
+    total = torch.zeros(nq, dtype=torch.int64, device=dev)
+    for r in range(3):
+        shard = E2[r::3].contiguous()
+        bs = b2[r::3].contiguous() if b2 is not None else None
+        total += asme.ops.catalog_count_above(H, shard, targets, tscore, 3, r, bs).to(torch.int64)
+    assert torch.equal(total + 1, want)
+    # invalid targets: ranked as item 0
+    bad = targets.clone()
+    bad[:16] = -1
+    bad[16:32] = V
+    got = asme.ops.catalog_rank(H, E2, bad, b2)
+    fix = bad.clone()
+    fix[:32] = 0
+    assert torch.equal(got, want_of(fix))
+
+
 def test_catalog_planes_cache_follows_every_table_write(asme, dev):
     """ops.CatalogPlanes reuses the split while the catalogue is unchanged and re-splits after any write: a torch
     in-place op (version counter), a FusedAdam step (kernels writing behind the counter); the module's validation
@@ -223,3 +276,11 @@ def test_catalog_planes_cache_follows_every_table_write(asme, dev):
         fresh = ops.catalog_rank(h, table, eval_batch["item.target"], bias)
     assert module._catalog_planes._planes is not planes
     assert torch.equal(r1, fresh)
+    # a flush with nothing deferred writes nothing and keeps the split; a catch-up that replays rows drops it
+    kept = module._catalog_planes.get(table)
+    opt.flush()
+    assert module._catalog_planes.get(table) is kept
+    lazy = table._asme_table_grad.lazy
+    lazy.record(lazy.step + 1, 1e-3, 0.9, 0.998, 1e-8, 1e-3)  # a zero-gradient step, replayed by the next flush
+    opt.flush()  # (LazyTableState.catch_up writes every row behind torch's version counter)
+    assert module._catalog_planes.get(table) is not kept

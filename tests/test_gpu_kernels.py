@@ -101,6 +101,44 @@ def test_attention_dropout_mask_matches_regeneration(asme, dev, causal, attn_mod
     assert torch.equal(grads[0], grads[1])
 
 
+def test_attention_mask_tag_guards_skipped_nibbles(asme, dev):
+    """The family-0 forward skips the query-major keep nibbles when its dS-storing backward will run, and records
+    that in the mask's tag: a backward of another family (which would read the nibbles) then writes NaN into dQ --
+    loud -- instead of a dQ from unwritten bits; with the family-0 backward, or a forward that stored the nibbles,
+    every gradient is finite (attention.hip family-0 nibble skip)."""
+    torch.manual_seed(2)
+    B, L, H, dk = 2, 67, 2, 64
+    D = H * dk
+    qkv = torch.randn(B, L, 3 * D, device=dev)
+    valid = torch.ones(B, L, dtype=torch.uint8, device=dev)
+    dout = torch.randn(B, L, D, device=dev)
+    call, ptr, st = asme._lib.call, asme._lib.ptr, asme._lib.stream
+    b, scale, seed = qkv.data_ptr(), dk ** -0.5, 99
+
+    def run(fwd_family, bwd_family):
+        out = torch.empty(B, L, D, device=dev)
+        stats = torch.empty(B * H, L, 2, device=dev)
+        mask = torch.full((asme.ops._mask_bytes(B, H, L),), 0xAB, device=dev, dtype=torch.uint8)
+        call("asme_attention_fwd_kernels", fwd_family, b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(valid), B, H,
+             L, dk, 1, scale, 0.25, seed, ptr(out), D, ptr(stats), ptr(mask), st())
+        g = torch.zeros_like(qkv)
+        ws = torch.empty(asme.ops._attn_bwd_ws_bytes(B, H, L, dk) // 4 + 1, device=dev)
+        gb = g.data_ptr()
+        call("asme_attention_bwd_kernels", bwd_family, b, b + 4 * D, b + 8 * D, 3 * D, 3 * D, 3 * D, ptr(out), D,
+             ptr(dout), D, ptr(stats), ptr(valid), B, H, L, dk, 1, scale, 0.25, seed, ptr(mask), ptr(ws), gb,
+             3 * D, gb + 4 * D, 3 * D, gb + 8 * D, 3 * D, st())
+        torch.cuda.synchronize()
+        return g[..., :D], g[..., D:]
+
+    dq, dkv = run(0, 2)
+    assert bool(torch.isnan(dq).all()) and bool(torch.isfinite(dkv).all())
+    dq, dkv = run(0, 0)
+    assert bool(torch.isfinite(dq).all()) and bool(torch.isfinite(dkv).all())
+    dq2, _ = run(2, 2)
+    assert bool(torch.isfinite(dq2).all())
+    assert _rel(dq2, dq) < 1e-4  # (the same dropout decisions either way)
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_attention_resident_matches_streaming_with_dropout(asme, dev, causal):
     """Both kernel families draw the same dropout masks (keyed by row and key), so they agree."""

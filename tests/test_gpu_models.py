@@ -109,38 +109,52 @@ def test_model_train_step_matches_reference(asme, dev, name, fused_xent, monkeyp
         assert close(got, g, TOL), (k, rel_err(got, g))
 
     opt, sched = asme.modules.split_optimizers(module.configure_optimizers())
+    lrs = [float(opt.param_groups[0]["lr"])]
     opt.step()
     opt.flush()  # a row-sparse table defers the zero-gradient rows' update (exact lazy Adam)
     if sched is not None:
         sched.step()
+    widened = [0, 0, 0]  # elements compared under the widened Adam bound, those that needed it, all elements
     for k, v in prefixed(z, "adam1").items():
         if _analytically_zero_grad(k):
             continue
-        got = _well_conditioned(named[k].detach().cpu().numpy(), v, grads[k])
-        assert close(got, v, TOL), (k, "adam step 1")
+        assert _adam_close(named[k].detach().cpu().numpy(), v, grads[k], lrs, widened), (k, "adam step 1")
     if "adam2/" + next(iter(grads)) in z.files:
+        lrs.append(float(opt.param_groups[0]["lr"]))
         opt.step()
         opt.flush()
         for k, v in prefixed(z, "adam2").items():
             if _analytically_zero_grad(k):
                 continue
-            got = _well_conditioned(named[k].detach().cpu().numpy(), v, grads[k])
-            assert close(got, v, TOL), (k, "adam step 2")
+            assert _adam_close(named[k].detach().cpu().numpy(), v, grads[k], lrs, widened), (k, "adam step 2")
+    print(f"{name}: Adam elements under the widened bound {widened[0]} of {widened[2]}, needing it {widened[1]} "
+          f"({widened[1] / max(widened[2], 1):.3%})")
+    assert widened[1] <= 0.01 * widened[2], widened
 
 
 ADAM_EPS = 1e-8
 
 
-def _well_conditioned(got, ref, grad_ref):
-    """Adam's first update of an element is lr * g / (|g| + eps); its derivative in g is
-    eps / (|g| + eps)^2, ~1/eps near |g| ~ eps: an fp32-rounding difference in a gradient of ~1e-8 (both
-    implementations' gradients agree to the tolerance checked above) moves the parameter by a visible fraction of
-    lr -- not determined by the reference.  Elements with 0 < |g| < 10 eps (0.3-1% of a d=128 fixture) take the
-    reference's value; exact zeros (rows with no gradient) and every other element are
-    compared as computed."""
-    g = np.abs(np.asarray(grad_ref))
-    ill = (g > 0) & (g < 10 * ADAM_EPS)
-    return np.where(ill, ref, got)
+def _adam_close(got, ref, grad_ref, lrs, widened):
+    """The parameters after Adam, compared as close() does (max-relative TOL), with one principled widening.  Adam's
+    first update of an element is lr * g / (|g| + eps), whose derivative in g, lr * eps / (|g| + eps)^2, is ~lr / eps
+    near |g| ~ eps: the gradient's own tolerance (TOL * max|g| + 1e-7, checked above) then moves the update by up to
+    its whole range -- the result is not determined by the reference there.  Each element's bound therefore adds
+    min(2 lr, lr * eps / (|g| + eps)^2 * (TOL * max|g| + 1e-7)) per step taken (lrs: each step's learning rate; the
+    step-1 gradient conditions both steps: a well-conditioned first step leaves v large).  `widened` counts the
+    elements whose bound grew by more than the base tolerance, how many of them actually differ by more than the
+    base tolerance, and all elements (the caller asserts the second stays <= 1 %)."""
+    got, ref, g = (np.asarray(x, np.float64) for x in (got, ref, grad_ref))
+    base = TOL * float(np.abs(ref).max()) + 1e-7
+    ag = np.abs(g)
+    dg = TOL * float(ag.max()) + 1e-7
+    extra = sum(np.minimum(2.0 * lr, lr * ADAM_EPS / (ag + ADAM_EPS) ** 2 * dg) for lr in lrs)
+    err = np.abs(got - ref)
+    wide = extra > base
+    widened[0] += int(wide.sum())
+    widened[1] += int((wide & (err > base)).sum())
+    widened[2] += err.size
+    return bool((err <= base + extra).all())
 
 
 def _sparse_table_grad(model):
