@@ -188,7 +188,11 @@ def emit(result, args):
     print(json.dumps(compact(result)), flush=True)
 
 
-def parse():
+def parse(argv=None):
+    return build_parser().parse_args(argv)
+
+
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--workload", choices=["sasrec-neg", "bert4rec", "kebert4rec"], default="sasrec-neg",
@@ -217,7 +221,7 @@ def parse():
                     help="gpu (default): every step samples a fresh batch from sessions in HBM with the GPU pos/neg "
                          "sampler (asme_posneg_sample) inside the timed step; resident: two pre-built device batches "
                          "alternating (rows touched one or two steps earlier: less lazy catch-up per step)")
-    ap.add_argument("--legs", default="bert4rec:27000,kebert4rec:13000,sasrec_zipf",
+    ap.add_argument("--legs", default="bert4rec:27000,kebert4rec:13000,sasrec_zipf,sasrec_overlap",
                     help="with the sasrec-neg headline: the other BASELINE workloads run in the same invocation and "
                          "reported under \"workloads\" of the one JSON line (name:items, comma-separated; "
                          "C3 BERT4Rec |I| = 27,000, C5 KeBERT4Rec |I| = 13,000, sasrec_zipf: the headline step on "
@@ -241,7 +245,7 @@ def parse():
     ap.add_argument("--cpu-batch-masked", type=int, default=64,
                     help="sequences per CPU-baseline step of the BERT4Rec / KeBERT4Rec workloads")
     ap.add_argument("--sampler-sessions", type=int, default=16, help="sessions for the CPU sampler rate")
-    return ap.parse_args()
+    return ap
 
 
 def parse_legs(spec: str):
@@ -250,9 +254,10 @@ def parse_legs(spec: str):
     out = []
     for part in spec.split(","):
         name, _, items = part.partition(":")
-        if name not in ("bert4rec", "kebert4rec", "sasrec_zipf"):
+        if name not in ("bert4rec", "kebert4rec", "sasrec_zipf", "sasrec_overlap"):
             raise SystemExit(f"--legs: unknown workload {name!r}")
-        out.append((name, int(items) if items else {"bert4rec": 27000, "kebert4rec": 13000, "sasrec_zipf": 0}[name]))
+        out.append((name, int(items) if items else {"bert4rec": 27000, "kebert4rec": 13000, "sasrec_zipf": 0,
+                                                    "sasrec_overlap": 0}[name]))
     return out
 
 
@@ -586,7 +591,7 @@ def bench_eval(args, asme, dev, world, rank, module, get_batch, ids_kind):
             "roofline": rooflines[0] if rooflines else None, "rooflines": rooflines}
 
 
-def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
+def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True, overlap=False):
     """The SASRec-neg training step (BASELINE C2 / C4): B sequences per GPU, |I| = args.items, the GPU pos/neg
     producer inside the timed step; ids_kind "uniform" (the headline) or "zipf" (Zipf(1.07) over item rank, seed
     1234: SURVEY §8d's secondary, hot keys for the dedup / occurrence CSR / ordered reduce-apply).  Returns the result
@@ -605,7 +610,8 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
     tok = asme.tokenization.Tokenizer(args.items)
     if sharded:
         module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok,
-                                                                              metrics=None, vocab=V)
+                                                                              metrics=None, vocab=V,
+                                                                              overlap_negatives=overlap)
         module.broadcast_dense_parameters()
         step_fn = None  # set below: each step also starts the next batch's id routing (module.prefetch)
     else:
@@ -837,6 +843,7 @@ def bench_sasrec(args, asme, dev, world, rank, ids_kind, with_eval=True):
                    "layers": args.layers, "dropout": args.dropout, "table_grad": args.table_grad,
                    "ids": ids_kind, "producer": args.producer,
                    "ids_ahead": (args.ids_ahead if args.producer == "gpu" and not sharded else "off"),
+                   "overlap_negatives": bool(overlap and sharded and world > 1),
                    "parallelism": f"dp{world}+rowshard{world}" if sharded else "single"},
         "roofline": roof,
         "rooflines": rooflines,
@@ -979,6 +986,13 @@ def main():
                 if args.ids == "zipf":
                     continue  # the headline already is the Zipf run
                 result["workloads"][leg] = bench_sasrec(args, asme, dev, world, rank, "zipf", with_eval=False)
+            elif leg == "sasrec_overlap":
+                # the headline step with the negative-only rows in a second, overlapped exchange (sharded.py
+                # overlap_negatives): only where rows cross the fabric (N > 1)
+                if world == 1:
+                    continue
+                result["workloads"][leg] = bench_sasrec(args, asme, dev, world, rank, args.ids, with_eval=False,
+                                                        overlap=True)
             else:
                 result["workloads"][leg] = bench_bert4rec(args, asme, dev, world, rank, leg, items)
             torch.cuda.empty_cache()

@@ -336,6 +336,14 @@ int64_t asme_bucket_by_owner_workspace(int64_t n, int world);
 int asme_bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, void* workspace,
                          int64_t ws_bytes, int64_t* order, int32_t* send_local, int64_t* counts, int64_t* pos,
                          void* stream);
+/* the same with two classes of ids (world <= 32): ids[i] with i < *split (a device int32: the requester's sequence /
+ * positive rows, first in the dedup's slot order) grouped by owner, then the rest (negative-only rows) by owner --
+ * counts has 2 * world entries, class-major, and the workspace is asme_bucket_by_owner_workspace(n, 2 * world).  The
+ * row-sharded SASRec step sends the two classes in two exchanges, the second overlapping the transformer
+ * (replaces the reference's replicated nn.Embedding lookup under DDP, sasrec_config.jsonnet:77-79). */
+int asme_bucket_by_owner_split(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, const int32_t* split,
+                               void* workspace, int64_t ws_bytes, int64_t* order, int32_t* send_local,
+                               int64_t* counts, int64_t* pos, void* stream);
 /* out[r] = table[ids[r]] (zero row for ids outside [0, vocab)): the owner side of the sharded lookup */
 int asme_gather_rows(const int64_t* ids, int64_t n, const float* table, int64_t vocab, int64_t dim, float* out,
                      void* stream);

@@ -115,6 +115,7 @@ SIGNATURES = {
     "asme_owner_histogram": [p, p, i64, i32, p, p, p],
     "asme_bucket_by_owner_workspace": [i64, i32],
     "asme_bucket_by_owner": [p, i64, p, i32, p, i64, p, p, p, p, p],
+    "asme_bucket_by_owner_split": [p, i64, p, i32, p, p, i64, p, p, p, p, p],
     "asme_gather_rows": [p, i64, p, i64, i64, p, p],
     "asme_session_batch": [p, p, i64, p, i64, i64, i64, i64, p, p, p],
     "asme_position_batch": [p, p, i64, p, i64, i64, i64, p, p, p, p, p],

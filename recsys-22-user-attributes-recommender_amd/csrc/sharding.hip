@@ -218,18 +218,25 @@ constexpr int kBk = 1024, kBkThreads = 256, kMaxW = 64;
 
 // n_dev (nullable): the number of ids is *n_dev <= n (a dedup count that never visits the host)
 __device__ __forceinline__ int64_t live_n(int64_t n, const int32_t* n_dev) { return n_dev ? min(n, (int64_t)*n_dev) : n; }
+// bucket of id i: its owner id % Wo, or -- with a class split (split non-null: the slots >= *split, the requester's
+// negative-only rows, travel in a second exchange) -- owner + Wo for the second class: 2 Wo buckets, class-major
+__device__ __forceinline__ int bucket_key(int64_t id, int64_t i, int Wo, int32_t split) {
+    return (int)(id % Wo) + (i >= split ? Wo : 0);
+}
 
 __global__ __launch_bounds__(kBkThreads) void bucket_count_kernel(const int64_t* __restrict__ ids, int64_t n,
                                                                   const int32_t* __restrict__ n_dev, int W,
-                                                                  int32_t* __restrict__ bcount, int64_t nb) {
+                                                                  int32_t* __restrict__ bcount, int64_t nb, int Wo,
+                                                                  const int32_t* __restrict__ split) {
     __shared__ int32_t h[kMaxW];
     n = live_n(n, n_dev);
+    const int32_t sp = split ? *split : 0x7FFFFFFF;
     for (int w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
     __syncthreads();
     const int64_t b0 = (int64_t)blockIdx.x * kBk;
     for (int r = 0; r < kBk / kBkThreads; ++r) {
         const int64_t i = b0 + r * kBkThreads + threadIdx.x;
-        if (i < n) atomicAdd(h + (int)(ids[i] % W), 1);
+        if (i < n) atomicAdd(h + bucket_key(ids[i], i, Wo, sp), 1);
     }
     __syncthreads();
     for (int w = threadIdx.x; w < W; w += blockDim.x) bcount[(int64_t)w * nb + blockIdx.x] = h[w];
@@ -275,9 +282,11 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_
                                                                     const int32_t* __restrict__ n_dev, int W,
                                                                     const int32_t* __restrict__ boff, int64_t nb,
                                                                     int64_t* __restrict__ order,
-                                                                    int32_t* __restrict__ send_local) {
+                                                                    int32_t* __restrict__ send_local, int Wo,
+                                                                    const int32_t* __restrict__ split) {
     constexpr int kWv = kBkThreads / 64;
     n = live_n(n, n_dev);
+    const int32_t sp = split ? *split : 0x7FFFFFFF;
     __shared__ int32_t base[kMaxW];
     __shared__ int32_t wcnt[kWv][kMaxW];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -288,7 +297,7 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_
         const int64_t i = b0 + r * kBkThreads + threadIdx.x;
         const bool live = i < n;
         const int64_t id = live ? ids[i] : 0;
-        const int mine = live ? (int)(id % W) : -1;
+        const int mine = live ? bucket_key(id, i, Wo, sp) : -1;
         int rank = 0;
         for (int w = 0; w < W; ++w) {
             const uint64_t m = __ballot(mine == w);
@@ -301,7 +310,7 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(const int64_
             for (int v = 0; v < wave; ++v) pre += wcnt[v][mine];
             const int64_t pos = (int64_t)base[mine] + pre + rank;
             order[pos] = i;
-            send_local[pos] = (int32_t)(id / W);
+            send_local[pos] = (int32_t)(id / Wo);
         }
         __syncthreads();
         for (int w = threadIdx.x; w < W; w += blockDim.x) {
@@ -414,28 +423,48 @@ ASME_API int64_t asme_bucket_by_owner_workspace(int64_t n, int world) {
 // crosses the fabric; a shard holds < 2^31 rows);
 // counts[w] = ids sent to rank w (int64, world entries); pos[order[j]] = j (nullable: the inverse permutation).
 // n_dev (nullable): only the first *n_dev <= n ids are live (the dedup count on the device: no host sync).
-ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, void* workspace,
-                                  int64_t ws_bytes, int64_t* order, int32_t* send_local, int64_t* counts, int64_t* pos,
-                                  void* stream) {
+namespace {
+int bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, const int32_t* split,
+                    void* workspace, int64_t ws_bytes, int64_t* order, int32_t* send_local, int64_t* counts,
+                    int64_t* pos, void* stream) {
+    const int nbk = split ? 2 * world : world;  // buckets
     ASME_CHECK_ARG(ids && workspace && order && send_local && counts, "asme_bucket_by_owner: null pointer");
-    ASME_CHECK_ARG(world >= 1 && world <= kMaxW, "asme_bucket_by_owner: world must be in [1, 64]");
+    ASME_CHECK_ARG(world >= 1 && nbk <= kMaxW, "asme_bucket_by_owner: world must be in [1, 64] (split: [1, 32])");
     ASME_CHECK_ARG(n >= 0 && n < ((int64_t)1 << 31), "asme_bucket_by_owner: bad n");
-    ASME_CHECK_ARG(ws_bytes >= asme_bucket_by_owner_workspace(n, world), "asme_bucket_by_owner: workspace too small");
+    ASME_CHECK_ARG(ws_bytes >= asme_bucket_by_owner_workspace(n, nbk), "asme_bucket_by_owner: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) {
-        if (hipMemsetAsync(counts, 0, world * sizeof(int64_t), s) != hipSuccess)
+        if (hipMemsetAsync(counts, 0, nbk * sizeof(int64_t), s) != hipSuccess)
             return hip_status(hipGetLastError(), "asme_bucket_by_owner");
         return 0;
     }
     const int64_t nb = (n + kBk - 1) / kBk;
     int32_t* bcount = (int32_t*)workspace;
-    hipLaunchKernelGGL(bucket_count_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, n_dev, world, bcount,
-                       nb);
-    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, bcount, nb, world, n, n_dev, counts);
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, n_dev, world, bcount,
-                       nb, order, send_local);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, n_dev, nbk, bcount,
+                       nb, world, split);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, bcount, nb, nbk, n, n_dev, counts);
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)nb), dim3(kBkThreads), 0, s, ids, n, n_dev, nbk, bcount,
+                       nb, order, send_local, world, split);
     if (pos) hipLaunchKernelGGL(invert_perm_kernel, dim3(nblk(n)), dim3(256), 0, s, order, n, n_dev, pos);
     ASME_LAUNCH_CHECK("asme_bucket_by_owner");
+}
+}  // namespace
+
+ASME_API int asme_bucket_by_owner(const int64_t* ids, int64_t n, const int32_t* n_dev, int world, void* workspace,
+                                  int64_t ws_bytes, int64_t* order, int32_t* send_local, int64_t* counts, int64_t* pos,
+                                  void* stream) {
+    return bucket_by_owner(ids, n, n_dev, world, nullptr, workspace, ws_bytes, order, send_local, counts, pos, stream);
+}
+
+// asme_bucket_by_owner with the ids split in two classes at the device slot *split: ids[i] with i < *split first, by
+// owner, then the rest, by owner -- 2 * world buckets (counts: 2 * world entries, class-major; workspace:
+// asme_bucket_by_owner_workspace(n, 2 * world)).  The row-sharded step sends its sequence / positive rows and its
+// negative-only rows in two exchanges, the second overlapping the transformer (sharded.py overlap_negatives).
+ASME_API int asme_bucket_by_owner_split(const int64_t* ids, int64_t n, const int32_t* n_dev, int world,
+                                        const int32_t* split, void* workspace, int64_t ws_bytes, int64_t* order,
+                                        int32_t* send_local, int64_t* counts, int64_t* pos, void* stream) {
+    ASME_CHECK_ARG(split, "asme_bucket_by_owner_split: null split");
+    return bucket_by_owner(ids, n, n_dev, world, split, workspace, ws_bytes, order, send_local, counts, pos, stream);
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -850,20 +850,29 @@ def select_rows(x2: torch.Tensor, rows: torch.Tensor, inverse: Optional[torch.Te
     return _SelectRowsFn.apply(x2.contiguous(), _i64(rows).reshape(-1), inverse)
 
 
-def bucket_by_owner(unique: torch.Tensor, world: int, count: Optional[torch.Tensor] = None):
+def bucket_by_owner(unique: torch.Tensor, world: int, count: Optional[torch.Tensor] = None,
+                    split: Optional[torch.Tensor] = None):
     """stable grouping of unique ids by owner (id % world): (order, send_local, counts (int64, world), pos) with
     unique[order[j]] the j-th id sent, send_local[j] its owner-local row, pos[order[j]] = j.  count (int32 (1,) on
-    the device, optional): only unique[:count] take part, the outputs past it are unspecified (no host sync)"""
+    the device, optional): only unique[:count] take part, the outputs past it are unspecified (no host sync).
+    split (int32 (1,) on the device, optional): two classes -- unique[:split] by owner, then the rest by owner;
+    counts then has 2 * world entries, class-major (asme_bucket_by_owner_split)"""
     u = _i64(unique).reshape(-1)
     n = u.numel()
     dev = u.device
-    ws = torch.empty(max(8, int(_lib.load().asme_bucket_by_owner_workspace(n, world))), device=dev, dtype=torch.uint8)
+    nbk = 2 * world if split is not None else world
+    ws = torch.empty(max(8, int(_lib.load().asme_bucket_by_owner_workspace(n, nbk))), device=dev, dtype=torch.uint8)
     order = torch.empty(n, device=dev, dtype=torch.int64)
     send_local = torch.empty(n, device=dev, dtype=torch.int32)
-    counts = torch.empty(world, device=dev, dtype=torch.int64)
+    counts = torch.empty(nbk, device=dev, dtype=torch.int64)
     pos = torch.empty(n, device=dev, dtype=torch.int64)
-    call("asme_bucket_by_owner", ptr(u), n, ptr(count), world, ptr(ws), ws.numel(), ptr(order), ptr(send_local),
-         ptr(counts), ptr(pos), stream())
+    if split is None:
+        call("asme_bucket_by_owner", ptr(u), n, ptr(count), world, ptr(ws), ws.numel(), ptr(order), ptr(send_local),
+             ptr(counts), ptr(pos), stream())
+    else:
+        sp = split.to(torch.int32).reshape(1)
+        call("asme_bucket_by_owner_split", ptr(u), n, ptr(count), world, ptr(sp), ptr(ws), ws.numel(), ptr(order),
+             ptr(send_local), ptr(counts), ptr(pos), stream())
     return order, send_local, counts, pos
 
 

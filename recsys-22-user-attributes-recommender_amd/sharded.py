@@ -41,13 +41,20 @@ def _host_staged(group, t: torch.Tensor) -> bool:
     return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
-def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, group=None):
+def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, group=None,
+                async_op: bool = False):
+    """all_to_all_single; async_op (RCCL): returns the work handle whose wait() makes the CURRENT stream wait for the
+    exchange (the host does not block), None when the exchange is already complete (gloo / host-staged)"""
     if _host_staged(group, inp):
         o = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
         out.copy_(o)
-    else:
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+        return None
+    work = dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=async_op)
+    if async_op and not out.is_cuda:  # (CPU gloo: complete before the caller reads it)
+        work.wait()
+        return None
+    return work
 
 
 def _all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
@@ -90,6 +97,10 @@ class ExchangeState:
     recv_counts: List[int]       # ids received from each requester
     recv_local: torch.Tensor     # local row ids requested from this rank, grouped by requester
     pos: torch.Tensor            # inverse of order: unique[i] is sent at position pos[i]
+    # two-class exchange (request(..., split=...)): the (send, recv) counts of each class; the send order and
+    # recv_local are class-major -- [class 0 by owner | class 1 by owner], [class 0 by requester | class 1 by requester]
+    classes: Optional[tuple] = None
+    work: object = None          # the class-1 rows' reply in flight (reply_rows(..., async_second=True))
 
 
 class RowShardExchange:
@@ -100,32 +111,45 @@ class RowShardExchange:
         self.vocab = vocab
         self.local_rows = shard_rows(vocab, self.world, self.rank)
 
-    def request(self, unique: torch.Tensor, count: Optional[torch.Tensor] = None) -> ExchangeState:
+    def request(self, unique: torch.Tensor, count: Optional[torch.Tensor] = None,
+                split: Optional[torch.Tensor] = None) -> ExchangeState:
         """route the requester's unique global ids to their owners (count: int32 (1,) device tensor, only
         unique[:count] are live -- the dedup count, read on the device; the per-owner counts below are the step's
-        one host sync)"""
-        return self.request_end(self.request_begin(unique, count))
+        one host sync).  split (int32 (1,) device tensor): two classes, unique[:split] and the rest, each routed by
+        owner in its own exchange (the class-1 rows can then come back while the model already runs)"""
+        return self.request_end(self.request_begin(unique, count, split))
 
-    def request_begin(self, unique: torch.Tensor, count: Optional[torch.Tensor] = None):
+    def request_begin(self, unique: torch.Tensor, count: Optional[torch.Tensor] = None,
+                      split: Optional[torch.Tensor] = None):
         """first half of request(): owner bucketing and the exchange of the per-owner counts are enqueued and the
         counts are copied to pinned host memory without waiting; request_end() reads them.  Issued a step ahead
         (ShardedSequenceNextItemPredictionTrainingModule.prefetch), the host's read of the split sizes RCCL needs
         no longer drains the GPU's queue."""
         W = self.world
-        if unique.is_cuda:  # stable owner bucketing in one counting-sort pass (asme_bucket_by_owner)
-            order, send_local, send_counts_t, pos = ops.bucket_by_owner(unique, W, count)
+        nbk = 2 * W if split is not None else W
+        if unique.is_cuda:  # stable owner bucketing in one counting-sort pass (asme_bucket_by_owner[_split])
+            order, send_local, send_counts_t, pos = ops.bucket_by_owner(unique, W, count, split)
         else:
             if count is not None:
                 unique = unique[:int(count.item())]
-            owner = unique % W
-            order = torch.argsort(owner, stable=True)
-            send_counts_t = torch.bincount(owner, minlength=W).to(torch.int64)
+            key = unique % W
+            if split is not None:
+                key = key + W * (torch.arange(len(unique)) >= int(split.reshape(-1)[0])).to(key.dtype)
+            order = torch.argsort(key, stable=True)
+            send_counts_t = torch.bincount(key, minlength=nbk).to(torch.int64)
             send_local = (unique.index_select(0, order) // W).to(torch.int32)
             pos = torch.empty_like(order)
             pos[order] = torch.arange(len(order), dtype=order.dtype)
-        recv_counts_t = torch.empty_like(send_counts_t)
-        _all_to_all(recv_counts_t, send_counts_t, group=self.group)
-        counts = torch.stack([send_counts_t, recv_counts_t])
+        if split is not None:
+            # per destination rank the pair (class-0 count, class-1 count): one (W, 2) exchange
+            sendm = send_counts_t.view(2, W).t().contiguous()
+            recvm = torch.empty_like(sendm)
+            _all_to_all(recvm, sendm, group=self.group)
+            counts = torch.stack([send_counts_t, recvm.t().reshape(-1)])  # both class-major (2 W)
+        else:
+            recv_counts_t = torch.empty_like(send_counts_t)
+            _all_to_all(recv_counts_t, send_counts_t, group=self.group)
+            counts = torch.stack([send_counts_t, recv_counts_t])
         event = None
         if counts.is_cuda:
             host = torch.empty(counts.shape, dtype=counts.dtype, pin_memory=True)
@@ -134,27 +158,47 @@ class RowShardExchange:
             event.record()
         else:
             host = counts
-        return (order, send_local, pos, host, event, unique.device)
+        return (order, send_local, pos, host, event, unique.device, split is not None)
 
     def request_end(self, pending) -> ExchangeState:
-        order, send_local, pos, host, event, dev = pending
+        order, send_local, pos, host, event, dev, two = pending
         if event is not None:
             event.synchronize()  # the step's one host sync
-        sc, rc = host[0].tolist(), host[1].tolist()
+        W = self.world
         # owner-local rows cross the fabric as int32 (a shard holds < 2^31 rows); widened once on arrival for the
         # gather / dedup kernels, which take int64 row ids
-        recv32 = torch.empty(sum(rc), dtype=torch.int32, device=dev)
-        _all_to_all(recv32, send_local[:sum(sc)], rc, sc, group=self.group)
-        return ExchangeState(order[:sum(sc)], sc, rc, recv32.to(torch.int64), pos)
+        if not two:
+            sc, rc = host[0].tolist(), host[1].tolist()
+            recv32 = torch.empty(sum(rc), dtype=torch.int32, device=dev)
+            _all_to_all(recv32, send_local[:sum(sc)], rc, sc, group=self.group)
+            return ExchangeState(order[:sum(sc)], sc, rc, recv32.to(torch.int64), pos)
+        s_all, r_all = host[0].tolist(), host[1].tolist()
+        sc0, sc1, rc0, rc1 = s_all[:W], s_all[W:], r_all[:W], r_all[W:]
+        n0 = sum(sc0)
+        recv32 = torch.empty(sum(rc0) + sum(rc1), dtype=torch.int32, device=dev)
+        _all_to_all(recv32[:sum(rc0)], send_local[:n0], rc0, sc0, group=self.group)
+        _all_to_all(recv32[sum(rc0):], send_local[n0:n0 + sum(sc1)], rc1, sc1, group=self.group)
+        sc = [a + b for a, b in zip(sc0, sc1)]
+        rc = [a + b for a, b in zip(rc0, rc1)]
+        return ExchangeState(order[:n0 + sum(sc1)], sc, rc, recv32.to(torch.int64), pos, classes=(sc0, sc1, rc0, rc1))
 
-    def reply_rows(self, st: ExchangeState, rows: torch.Tensor) -> torch.Tensor:
+    def reply_rows(self, st: ExchangeState, rows: torch.Tensor, async_second: bool = False) -> torch.Tensor:
         """owners' rows (aligned with st.recv_local) -> the requester's rows in SEND order: row j belongs to
-        unique[st.order[j]] (unique id i is row st.pos[i]; callers remap ids instead of permuting rows)"""
+        unique[st.order[j]] (unique id i is row st.pos[i]; callers remap ids instead of permuting rows).
+        A two-class state sends the class-0 rows, then the class-1 rows -- with async_second in flight on RCCL's
+        stream when this returns (st.work: wait() on it before reading rows past the class-0 block)"""
         if self.world == 1:  # the rank's own rows in request order: no copy
             return rows.detach().contiguous()
         U = len(st.order)
         got = torch.empty(U, rows.shape[1], dtype=rows.dtype, device=rows.device)
-        _all_to_all(got, rows.contiguous(), st.send_counts, st.recv_counts, group=self.group)
+        rows = rows.contiguous()
+        if st.classes is None:
+            _all_to_all(got, rows, st.send_counts, st.recv_counts, group=self.group)
+            return got
+        sc0, sc1, rc0, rc1 = st.classes
+        n0, r0 = sum(sc0), sum(rc0)
+        _all_to_all(got[:n0], rows[:r0], sc0, rc0, group=self.group)
+        st.work = _all_to_all(got[n0:], rows[r0:], sc1, rc1, group=self.group, async_op=async_second)
         return got
 
     def push_grads(self, st: ExchangeState, grad_send: torch.Tensor) -> torch.Tensor:
@@ -162,7 +206,14 @@ class RowShardExchange:
         if self.world == 1:
             return grad_send.contiguous()
         recv = torch.empty(len(st.recv_local), grad_send.shape[1], dtype=grad_send.dtype, device=grad_send.device)
-        _all_to_all(recv, grad_send.contiguous(), st.recv_counts, st.send_counts, group=self.group)
+        grad_send = grad_send.contiguous()
+        if st.classes is None:
+            _all_to_all(recv, grad_send, st.recv_counts, st.send_counts, group=self.group)
+            return recv
+        sc0, sc1, rc0, rc1 = st.classes
+        n0, r0 = sum(sc0), sum(rc0)
+        _all_to_all(recv[:r0], grad_send[:n0], rc0, sc0, group=self.group)
+        _all_to_all(recv[r0:], grad_send[n0:], rc1, sc1, group=self.group)
         return recv
 
 
@@ -175,9 +226,15 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
 
     def __init__(self, model, item_tokenizer, metrics, vocab: int, learning_rate: float = 0.001,
                  beta_1: float = 0.99, beta_2: float = 0.998, weight_decay: float = 1e-3, loss_function=None,
-                 group=None):
+                 group=None, overlap_negatives: bool = False):
+        """overlap_negatives (W > 1): the rows only the sampled head reads -- ids that occur among the negatives but
+        not in the sequence or the positives, ~half the step's distinct rows -- come back in a second all-to-all
+        that runs on RCCL's stream while the embedding and the transformer compute; the head waits for it.  Their
+        gradients go back in a second all-to-all too.  Same owner plan (one dedup, one lazy-Adam staging, one
+        ordered reduction over every requester's rows), DDP semantics unchanged."""
         super().__init__(model, item_tokenizer, metrics, learning_rate, beta_1, beta_2, weight_decay,
                          loss_function, table_grad="sparse")
+        self.overlap_negatives = overlap_negatives
         self.exchange = RowShardExchange(vocab, group)
         self.vocab = vocab
         self.group = group
@@ -224,7 +281,19 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         id_sets = [batch[k] for k in self._ID_KEYS]
         self._maps(self.model.item_table().device)
         req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
-        self._prefetched = (originals, id_sets, req, self.exchange.request_begin(req.unique, req.count))
+        self._prefetched = (originals, id_sets, req,
+                            self.exchange.request_begin(req.unique, req.count, self._split(req, id_sets)))
+
+    def _split(self, req, id_sets) -> Optional[torch.Tensor]:
+        """overlap_negatives: the requester's class boundary (int32 (1,) on the device) -- the dedup numbers the unique
+        ids in first-occurrence order over [sequence, positives, negatives], so the ids the sequence or the positives
+        hold are exactly the slots below max(their slots) + 1 and every slot past it is a negative-only row"""
+        if not self.overlap_negatives or self.exchange.world == 1 or len(id_sets) != 3:
+            return None
+        n_a = id_sets[0].numel() + id_sets[1].numel()
+        if n_a == 0:
+            return torch.zeros(1, dtype=torch.int32, device=req.unique.device)
+        return (req._flat_inverse[:n_a].max() + 1).to(torch.int32).reshape(1)
 
     def cancel_prefetch(self):
         """drop a prefetched request that will not be used (its counts exchange is complete on every rank);
@@ -261,7 +330,7 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
             req = ops.SparseTablePlan.for_ids(self.vocab, id_sets, self._req_map)
             # 2. route ids to owners (the dedup count stays on the device); owners bring their rows up to date
             # (lazy Adam: staged in slot order, or caught up in the table) and gather them
-            st = self.exchange.request(req.unique, req.count)
+            st = self.exchange.request(req.unique, req.count, self._split(req, id_sets) if train else None)
         own = None
         src, src_ids = shard.detach(), st.recv_local
         if train:
@@ -277,8 +346,9 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
                 rows = src[:len(st.recv_local)]
             else:
                 rows = ops.gather_rows(src_ids, src) if len(st.recv_local) else shard.new_empty(0, shard.shape[1])
-        # the compact table stays in send order; the ids are remapped to it (no row permutation)
-        compact = self.exchange.reply_rows(st, rows)
+        # the compact table stays in send order; the ids are remapped to it (no row permutation).  Two classes: the
+        # negative-only rows' reply stays in flight (st.work), past the class-0 block the model reads first
+        compact = self.exchange.reply_rows(st, rows, async_second=True)
         inv = [st.pos.index_select(0, req.inverse_of(x).reshape(-1)).view(x.shape) for x in id_sets]
         req.release()
         return st, own, compact, inv
@@ -302,10 +372,19 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         meta["positive_samples"], meta["negative_samples"] = inv_pos, inv_neg
         padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
         emb._table_override = compact
+        wait = None
+        if st.work is not None:  # the negative-only rows are still arriving: the sampled head waits for them
+            work, st.work = st.work, None
+
+            def _wait(module, args):  # (returns None: the head's inputs unchanged)
+                work.wait()
+            wait = self.model._projection_layer.register_forward_pre_hook(_wait)
         try:
             pos_logits, neg_logits = self.model(InputSequence(inv_seq, padding_mask, meta))
         finally:
             emb._table_override = None
+            if wait is not None:
+                wait.remove()
         loss = self.loss_function(pos_logits, neg_logits, mask=padding_mask)
         self._pending = (st, own, compact, cplan)
         return {"loss": loss}

@@ -99,14 +99,23 @@ def test_compact_line_keeps_contract_and_every_workload(bench):
               "roofline": roofs[0], "rooflines": roofs, "cpu_baseline": None,
               "eval": {"metric": "e", "value": 9.0, "unit": "sequences/s", "ms_per_step": 3.0, "steps": 3,
                        "ndcg@10": 0.0, "roofline": roofs[0], "rooflines": roofs},
-              "workloads": {"bert4rec": leg, "kebert4rec": leg, "sasrec_zipf": leg}}
+              "workloads": {"bert4rec": leg, "kebert4rec": leg, "sasrec_zipf": leg, "sasrec_overlap": leg}}
     c = bench.compact(result)
     line = json.dumps(c)
     assert len(line) < 6000
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "config", "roofline", "cpu_baseline"):
         assert k in c
-    assert set(c["workloads"]) == {"bert4rec", "kebert4rec", "sasrec_zipf"}
+    assert set(c["workloads"]) == {"bert4rec", "kebert4rec", "sasrec_zipf", "sasrec_overlap"}
     assert all(len(w["rooflines_top"]) == 3 and w["value"] == 1.0 for w in c["workloads"].values())
     assert c["target_kernels"]["asme_embedding_ln_fwd"] == 0.61
     assert c["eval"]["value"] == 9.0
+
+
+def test_default_legs_include_the_overlapped_exchange(bench):
+    """the default invocation measures the overlapped row exchange beside the headline wherever rows cross the fabric
+    (the leg is skipped at N = 1); an unknown leg name is refused"""
+    legs = dict(bench.parse_legs(bench.build_parser().get_default("legs")))
+    assert {"bert4rec", "kebert4rec", "sasrec_zipf", "sasrec_overlap"} <= set(legs)
+    with pytest.raises(SystemExit):
+        bench.parse_legs("sasrec_overlapped")

@@ -20,7 +20,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, V, D, q):
+def _worker(rank, world, port, V, D, split, q):
     sys.path.insert(0, ROOT)
     import __graft_entry__
     asme = __graft_entry__.load_package()
@@ -34,11 +34,19 @@ def _worker(rank, world, port, V, D, q):
         assert shard.shape[0] == asme.sharded.shard_rows(V, world, rank)
         gr = torch.Generator().manual_seed(100 + rank)
         unique = torch.randperm(V, generator=gr)[: 17 + 5 * rank]     # this rank's distinct ids
-        st = ex.request(unique)
+        # split: two classes (overlap_negatives), the first 5 + rank unique ids and the rest, each routed by owner
+        sp = torch.tensor([5 + rank], dtype=torch.int32) if split else None
+        st = ex.request(unique, split=sp)
         assert int((st.recv_local >= shard.shape[0]).sum()) == 0
-        rows = ex.reply_rows(st, shard[st.recv_local])                # send order: row j <-> unique[order[j]]
+        rows = ex.reply_rows(st, shard[st.recv_local], async_second=split)  # send order: row j <-> unique[order[j]]
+        assert st.work is None  # (CPU gloo: complete on return)
         ok_rows = torch.equal(rows, table[unique[st.order]]) and torch.equal(rows[st.pos], table[unique])
-        ok_rows = ok_rows and bool((unique[st.order] % world == torch.sort(unique[st.order] % world).values).all())
+        key = unique[st.order] % world
+        if split:  # class-major: the first class's ids (slots < split) by owner, then the rest by owner
+            cls = (st.order >= 5 + rank).to(torch.int64)
+            key = key + world * cls
+            ok_rows = ok_rows and int(st.classes[0][0] + sum(st.classes[0][1:])) == 5 + rank
+        ok_rows = ok_rows and bool((key == torch.sort(key).values).all())
         # gradient push: owners receive every requester's rows, averaged over ranks
         grad = torch.randn(len(unique), D, generator=gr)
         recv = ex.push_grads(st, grad[st.order])
@@ -58,12 +66,12 @@ def _worker(rank, world, port, V, D, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_shard_exchange_gloo(world):
+@pytest.mark.parametrize("world,split", [(2, False), (3, False), (2, True), (3, True)])
+def test_row_shard_exchange_gloo(world, split):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 101, 8, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 101, 8, split, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -51,7 +51,7 @@ def _worker(rank, world, port, cfg, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     try:
-        B, L, V, d, h, N, steps, id_dtype = cfg
+        B, L, V, d, h, N, steps, id_dtype, overlap = cfg
         torch.manual_seed(0)
         full = _model(asme, V, L, d, h, N)                      # the logical model, identical on every rank
         sd = {k: v.clone() for k, v in full.state_dict().items()}
@@ -84,7 +84,8 @@ def _worker(rank, world, port, cfg, q):
         model.load_state_dict(ssd)
         model.to(dev)
         module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok,
-                                                                              metrics=None, vocab=V)
+                                                                              metrics=None, vocab=V,
+                                                                              overlap_negatives=overlap)
         module.broadcast_dense_parameters()
         opt = module.configure_optimizers()
         per = B // world
@@ -143,7 +144,7 @@ def _worker(rank, world, port, cfg, q):
         dist.destroy_process_group()
 
 
-def _ddp_worker(rank, world, port, q):
+def _ddp_worker(rank, world, port, overlap, q):
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -164,7 +165,8 @@ def _ddp_worker(rank, world, port, q):
         model.to(dev)
         tok = asme.tokenization.Tokenizer(V - 3)
         module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok,
-                                                                              metrics=None, vocab=V)
+                                                                              metrics=None, vocab=V,
+                                                                              overlap_negatives=overlap)
         opt = module.configure_optimizers()
         per = B // world
         part = {k: torch.from_numpy(z[s][rank * per:(rank + 1) * per]).to(dev)
@@ -201,13 +203,14 @@ def _spawn(target, world, extra=()):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_sharded_training_matches_reference_ddp(world):
+@pytest.mark.parametrize("world,overlap", [(2, False), (8, False), (2, True), (8, True)])
+def test_sharded_training_matches_reference_ddp(world, overlap):
     """BASELINE C4's semantics pinned to the reference: the row-sharded step on W ranks == the reference module's DDP
-    step (tests/golden/ddp_sasrec_neg.npz), element-wise"""
+    step (tests/golden/ddp_sasrec_neg.npz), element-wise; overlap: the negative-only rows in their own exchange
+    (overlap_negatives), same bounds"""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm GPU")
-    res = _spawn(_ddp_worker, world)
+    res = _spawn(_ddp_worker, world, (overlap,))
     for rank, errs in res.items():
         assert isinstance(errs, dict), f"rank {rank}: {errs}"
         bad = {k: e for k, e in errs.items() if not e <= 1.0}
@@ -313,13 +316,14 @@ def test_sharded_full_vocabulary_matches_unsharded():
 # (world, d): d = 32 runs every Linear on the general fp32-MFMA kernel, d = 128 (h = 2, d_ff = 512) on the
 # production composition -- the weight-stationary bf16x6 GEMMs, the fused FFN and the split-T weight gradients;
 # W = 8 is the node's shard map (8 ranks on the one GPU, the ids of every owner crossing the exchange)
-@pytest.mark.parametrize("world,d,id_dtype", [(2, 32, torch.int64), (3, 32, torch.int32), (2, 128, torch.int32),
-                                              (8, 128, torch.int64)])
-def test_sharded_training_multirank_matches_unsharded(world, d, id_dtype):
+@pytest.mark.parametrize("world,d,id_dtype,overlap", [(2, 32, torch.int64, False), (3, 32, torch.int32, False),
+                                                      (2, 128, torch.int32, False), (8, 128, torch.int64, False),
+                                                      (3, 32, torch.int64, True), (8, 128, torch.int32, True)])
+def test_sharded_training_multirank_matches_unsharded(world, d, id_dtype, overlap):
     if not torch.cuda.is_available():
         pytest.skip("no ROCm GPU")
     B = 6 * world
-    cfg = (B, 16, 301 if d == 32 else 1031, d, 2, 2, 4, id_dtype)
+    cfg = (B, 16, 301 if d == 32 else 1031, d, 2, 2, 4, id_dtype, overlap)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--seq", type=int, default=200)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--order", choices=["slot", "random"], default="slot")
+    ap.add_argument("--basic", action="store_true", help="only the p = 0.2 / 0 timings (no in-step probes)")
     a = ap.parse_args()
     asme = __graft_entry__.load_package()
     L_ = asme._lib
@@ -68,10 +69,13 @@ def main():
         b = timed(bwd, a.iters)
         print(f"p={p}: fwd {f:.1f} us ({fwd_bytes / f / 8e6:.3f} of 8 TB/s)  bwd {b:.1f} us "
               f"({bwd_bytes / b / 8e6:.3f})", flush=True)
+    if a.basic:
+        return
     # in-step conditions: the lazy-Adam stage writes ~0.9 GB of staged rows right before the forward (dirty lines
     # still draining from the L2 / MALL); each call bracketed by its own event pair, as bench.py's KernelTimer does
     big = torch.empty(3 * 3 * T * D, device=dev)
     import ctypes
+    # (build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/probe/stream_probe.hip -o tools/probe/libstream.so)
     probe = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "probe", "libstream.so"))
     probe.run_stream.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.c_void_p]
     nb4 = big.numel() // 4
