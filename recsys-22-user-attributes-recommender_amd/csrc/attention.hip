@@ -160,6 +160,11 @@ struct Stage {
     }
 };
 
+// the sliced image of a tile (rows_times_slice<..., SL = true>): element (r, c) at (c / DQ) * sl + r * (DQ + 4) + c % DQ,
+// sl = the slice stride (a multiple of 64 floats)
+__host__ __device__ inline int sliced_stride(int Lp, int DK) { return (Lp * (DK / 4 + 4) + 63) & ~63; }
+__device__ __forceinline__ int sliced_off(int r, int c, int DQ, int sl) { return (c / DQ) * sl + r * (DQ + 4) + c % DQ; }
+
 // this lane's contiguous DQ = DK/4 features of one row, from global memory
 template <int DK>
 __device__ __forceinline__ void load_row_slice(const float* __restrict__ rowp, bool ok, int g, float (&f)[DK / 4]) {
@@ -180,13 +185,18 @@ struct NoFill {
 // acc[sub] += Tile[sub*16 + c16][slice g] . f  (16 x 16 result per sub-tile, rows of the tile on C/D rows).
 // fill(s4) runs after step s4's MFMAs are issued, in the same scheduling region: independent vector work of the
 // caller that issues in the shadow of this wave's MFMAs.
-template <int DK, int NS = kNS, class F = NoFill>
+template <int DK, int NS = kNS, class F = NoFill, bool SL = false>
 __device__ __forceinline__ void rows_times_slice(const float* __restrict__ tile, int g, int c16,
-                                                 const float (&f)[DK / 4], floatx4 (&acc)[NS], F&& fill = F{}) {
-    constexpr int S = DK + 4, DQ = DK / 4;
+                                                 const float (&f)[DK / 4], floatx4 (&acc)[NS], F&& fill = F{},
+                                                 int sl = 0) {
+    // SL: the tile in the sliced layout (sliced_off): row stride DQ + 4 within each of the 4 column slices, slices
+    // sl floats apart (sl % 64 == 0) -- a lane's b128 read lands at bank chunk 5 r + const (DK = 64), so the 16 lanes
+    // of each b128 lane group hit 16 distinct chunks (the padded row-major image, stride DK + 4, puts two lanes on
+    // one chunk in half the groups: ~1 extra LDS cycle per read)
+    constexpr int S = SL ? DK / 4 + 4 : DK + 4, DQ = DK / 4;
     // the b128 row reads of step s4+1 are issued before step s4's MFMAs (LDS latency off the MFMA stream)
     float4 ab[2][NS];
-    const float* base = tile + c16 * S + g * DQ;
+    const float* base = tile + c16 * S + g * (SL ? sl : DQ);
 #pragma unroll
     for (int sub = 0; sub < NS; ++sub) ab[0][sub] = *reinterpret_cast<const float4*>(base + sub * 16 * S);
     __builtin_amdgcn_sched_barrier(0);
@@ -619,17 +629,22 @@ constexpr int kResThreads = ASME_RES_THREADS;  // forward and dQ passes
 constexpr int kResThreadsKV = 512;             // dK/dV pass: 168+ VGPRs, 12 waves would spill
 
 __host__ __device__ inline int res_rows(int L) { return (L + 15) & ~15; }
-inline size_t res_lds_bytes(int L, int DK, bool with_stats) {
+#ifndef ASME_ATTN_SLICED
+#define ASME_ATTN_SLICED 1  // the resident forward keeps K in the sliced image (conflict-free b128 row reads)
+#endif
+inline size_t res_lds_bytes(int L, int DK, bool with_stats, bool k_sliced = false) {
     const size_t Lp = (size_t)res_rows(L);
-    return 2 * Lp * (DK + 4) * sizeof(float) + (with_stats ? 3 * Lp * sizeof(float) : 0) + (Lp + 31) / 32 * 4 + 16;
+    const size_t kimg = k_sliced ? (size_t)4 * sliced_stride((int)Lp, DK) : Lp * (DK + 4);
+    return (kimg + Lp * (DK + 4)) * sizeof(float) + (with_stats ? 3 * Lp * sizeof(float) : 0) + (Lp + 31) / 32 * 4 + 16;
 }
 
 // rows [0, Lp) of two (L x DK) operands into padded LDS images (rows >= L zeroed); 8 float4 in flight
-template <int DK, int NT = kResThreads>
+template <int DK, int NT = kResThreads, bool A_SL = false>
 __device__ __forceinline__ void load_pair_resident(const float* __restrict__ a, int64_t lda,
                                                    const float* __restrict__ b, int64_t ldb, int L, int Lp,
                                                    float* __restrict__ As, float* __restrict__ Bs) {
     constexpr int C4 = DK / 4, S = DK + 4;
+    const int asl = A_SL ? sliced_stride(Lp, DK) : 0;
     const int n4 = Lp * C4;
     // all loads of a batch are issued before the first store: at L = 200, dk = 64 one batch covers the head
     for (int base = threadIdx.x; base < n4; base += NT * 8) {
@@ -645,7 +660,7 @@ __device__ __forceinline__ void load_pair_resident(const float* __restrict__ a, 
         for (int u = 0; u < 8; ++u) {
             const int idx = base + u * NT, row = idx / C4, c = (idx % C4) * 4;
             if (idx < n4) {
-                *reinterpret_cast<float4*>(As + row * S + c) = ra[u];
+                *reinterpret_cast<float4*>(As + (A_SL ? sliced_off(row, c, DK / 4, asl) : row * S + c)) = ra[u];
                 *reinterpret_cast<float4*>(Bs + row * S + c) = rb[u];
             }
         }
@@ -700,8 +715,10 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
     constexpr int DQ = DK / 4, NCT = DK / 16, S = DK + 4;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int Lp = res_rows(L);
+    constexpr bool KSL = ASME_ATTN_SLICED;  // K in the sliced image (rows_times_slice's conflict-free row reads)
+    const int ksl = KSL ? sliced_stride(Lp, DK) : 0;
     float* Ks = lds;
-    float* Vs = Ks + Lp * S;
+    float* Vs = Ks + (KSL ? 4 * ksl : Lp * S);
     uint32_t* kvw = reinterpret_cast<uint32_t*>(Vs + Lp * S);
     int* ctl = reinterpret_cast<int*>(kvw + (Lp + 31) / 32);
 
@@ -714,7 +731,8 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
 
     stage_valid_res(key_valid, b, L, Lp, kvw, ctl);
     if (ASME_ATTN_DIAG != 1)
-        load_pair_resident<DK>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks, Vs);
+        load_pair_resident<DK, kResThreads, KSL>(k + tok0 * ldk + h * DK, ldk, v + tok0 * ldv + h * DK, ldv, L, Lp, Ks,
+                                                 Vs);
     __syncthreads();
     const int last_valid = ctl[0];
     const bool any_valid = last_valid >= 0;
@@ -743,7 +761,7 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
             floatx4 st[NS];
 #pragma unroll
             for (int sub = 0; sub < NS; ++sub) st[sub] = floatx4{0.f, 0.f, 0.f, 0.f};
-            rows_times_slice<DK, NS>(Ks + k0 * S, g, c16, qf, st);
+            rows_times_slice<DK, NS, NoFill, KSL>(Ks + k0 * (KSL ? DQ + 4 : S), g, c16, qf, st, NoFill{}, ksl);
             float p[NS][4];
             float tmax = kInitMax;
             if (chunk_unmasked(kvw, k0, NS * 16, L, causal, q0)) {
@@ -1331,7 +1349,7 @@ ASME_API int asme_attention_fwd_kernels(int kernels, const float* q, const float
                    "asme_attention_fwd: operands must be 16-B aligned with ld % 4 == 0");
     if (batch == 0) return 0;
     const dim3 grid((unsigned)((seq_len + kQB - 1) / kQB), (unsigned)(batch * heads));
-    const size_t lds = res_lds_bytes((int)seq_len, (int)head_dim, false);
+    const size_t lds = res_lds_bytes((int)seq_len, (int)head_dim, false, ASME_ATTN_SLICED);
     ASME_DK_DISPATCH(head_dim,
         // the query-major keep nibbles are read only by the dQ passes that regenerate P (families 1 and 2, and family
         // 0 when its dS-storing backward does not fit); the family-0 backward's dK/dV pass reads the key-major words

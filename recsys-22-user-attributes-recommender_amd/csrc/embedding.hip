@@ -652,6 +652,213 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
     if (partials) write_row_partials<R, NACC, kWavesPerBlock>(acc, lane, wave, D, partials);
 }
 
+// D = 128 on 16 lanes x two float4 with the keep bytes given (or no dropout): the operations of
+// emb_bwd4_kernel<RowLayout<4, 16, 2>, 1, LN3, LN2> in the same order, as straight-line code -- the width a compile-time
+// constant (no column checks), no Philox regeneration path, and no per-lane live branches: every lane loads a real row
+// (the tail pass clamps its token to T - 1 and zeroes its gradient inputs), so each pass is one run of loads and one
+// run of arithmetic.  (emb_bwd4_kernel's ISA: ~830 VALU per pass, 170 of them register moves around the live / keep
+// branches, and one exec-masked branch per LayerNorm stage.)
+#ifndef ASME_EMB_BWD128_WPE
+#define ASME_EMB_BWD128_WPE 2  // (3: 168 VGPRs and 11 spilled, 116-120 vs 105-108 us at 2 waves per SIMD)
+#endif
+#ifndef ASME_EMB_BWD128_PF
+#define ASME_EMB_BWD128_PF 1
+#endif
+template <bool LN3, bool LN2, bool POS, bool DROP>  // POS: a position table; DROP: keep bytes given (some p > 0)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASME_EMB_BWD128_WPE, 8))) void emb_bwd128_kernel(
+    const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V,
+    const float* __restrict__ pos, const float* __restrict__ w1, const float* __restrict__ b1, float p1,
+    const float* __restrict__ extra, const float* __restrict__ w2, float p2, const uint8_t* __restrict__ keep,
+    const float* __restrict__ dout, const float* __restrict__ stats, float* __restrict__ d_rows,
+    float* __restrict__ d_extra, float* __restrict__ partials, EmbLn3 l3) {
+    using R = RowLayout<4, 16, 2>;
+    constexpr int D = 128;
+    constexpr int NACC = LN3 ? 6 : 4;
+    const int lane = threadIdx.x & 63, sub = lane & 15, wave = threadIdx.x >> 6;
+    float acc[NACC][R::NV][R::W];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) row_zero<R>(acc[k]);
+    const bool small = T < ((int64_t)1 << 31) && L < ((int64_t)1 << 31);
+    const float k1 = 1.f / (1.f - p1), k2 = 1.f / (1.f - p2);
+    __shared__ __attribute__((aligned(16))) float prm[5][D];
+    for (int e = threadIdx.x; e < D; e += blockDim.x) {
+        prm[0][e] = w1 ? w1[e] : 0.f;
+        prm[1][e] = w1 ? b1[e] : 0.f;
+        if constexpr (LN3) prm[2][e] = l3.w[e];
+        if constexpr (LN2) {
+            prm[3][e] = w2[e];
+            if constexpr (LN3) prm[4][e] = l3.b2[e];
+        }
+    }
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * R::RPW;
+    // software pipeline (ASME_EMB_BWD128_PF): the next pass's rows are requested before this pass's arithmetic, and the
+    // ids two passes ahead -- a row load depends on its id, so ids run one pass ahead of the rows.  At one pass in
+    // flight per wave the CU held ~32 KB of loads on average (8 waves, half of them computing), not enough to cover
+    // HBM latency; with the next pass in flight every wave keeps its loads outstanding while it computes.
+    struct PassIn {
+        RowVals<R> x, q, g, dl;
+        float4 st;
+        float2 st3;
+        uint32_t kv;
+    };
+    auto tok_of = [&](int64_t b) { const int64_t t = b + lane / R::LPR; return t < T ? t : T - 1; };
+    // (raw ids: clamped where a row address is formed -- a clamp right after the load made the wave wait for it, and
+    // with it for every load issued before, i.e. for the whole next pass, at the top of every pass)
+    auto load_id = [&](int64_t b) -> int64_t { return ids[tok_of(b)]; };
+    auto load_pass = [&](int64_t b, int64_t raw_id, PassIn& in) {
+        const int64_t tt = tok_of(b);
+        const int64_t id = (raw_id < 0 || raw_id >= V) ? 0 : raw_id;
+        row_load<R>(table + id * D, sub, D, in.x);
+        // (position t % L in 32-bit arithmetic where the token count allows: a 64-bit remainder is a ~40-instruction
+        // sequence per pass)
+        const int64_t pr = small ? (int64_t)((uint32_t)tt % (uint32_t)L) : tt % L;
+        if constexpr (POS) row_load<R>(pos + pr * D, sub, D, in.q);
+        row_load<R>(dout + tt * D, sub, D, in.g);
+        in.st = *reinterpret_cast<const float4*>(stats + tt * 4);
+        in.st3 = make_float2(0.f, 1.f);
+        if constexpr (LN3) {
+            row_load<R>(l3.dln + tt * D, sub, D, in.dl);
+            in.st3 = *reinterpret_cast<const float2*>(l3.stats + tt * 2);
+        }
+        // (the lane's two keep bytes: one 16-bit load, as emb_keep_load; a p = 0 half is all 1s)
+        in.kv = DROP ? (uint32_t)*reinterpret_cast<const uint16_t*>(keep + tt * (D >> 2) + sub * 2) : 0xFFFFu;
+    };
+    int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * R::RPW;
+    PassIn nin;
+    int64_t nid = 0;
+    if (ASME_EMB_BWD128_PF && base < T) {
+        load_pass(base, load_id(base), nin);
+        if (base + stride < T) nid = load_id(base + stride);
+    }
+    for (; base < T; base += stride) {
+        const int64_t t = base + lane / R::LPR;
+        const int64_t tt = t < T ? t : T - 1;
+        PassIn in;
+        if (ASME_EMB_BWD128_PF) {
+            in = nin;
+            if (base + stride < T) {  // (wave-uniform) the next pass's rows, and the ids of the one after it
+                load_pass(base + stride, nid, nin);
+                if (base + 2 * stride < T) nid = load_id(base + 2 * stride);
+            }
+        } else {
+            load_pass(base, load_id(base), in);
+        }
+        RowVals<R>& x = in.x;
+        RowVals<R>& q = in.q;
+        RowVals<R>& g = in.g;
+        RowVals<R>& dl = in.dl;
+        const float4 st = in.st;
+        const float2 st3 = in.st3;
+        uint32_t bits[R::NV] = {in.kv & 0xFFu, in.kv >> 8};
+        if (base + R::RPW > T && t >= T) {  // (tail pass only) a token past T: no gradient flows from it
+            row_zero<R>(g);
+            if constexpr (LN3) row_zero<R>(dl);
+        }
+        if constexpr (POS)
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[j][i] += q[j][i];
+        // recompute z = drop1(LN1(x)) + extra
+        RowVals<R> xh1, xh2;
+        if (w1) {
+            row_normalise<R>(x, sub, D, st.x, st.y, xh1);
+            row_affine<R>(xh1, sub, D, prm[0], prm[1], x);
+        } else {
+            row_zero<R>(xh1);
+        }
+        if constexpr (DROP)
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[j][i] *= keep_factor_bit(bits[j], i, k1);
+        if constexpr (LN2) {
+            if (extra) {
+                row_load<R>(extra + tt * D, sub, D, q);
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[j][i] += q[j][i];
+            }
+            row_normalise<R>(x, sub, D, st.z, st.w, xh2);
+        }
+        if constexpr (LN3) {
+            // the embedding output drop2(LN2(z)) (or drop2(z) without LN2), then g += LN3 backward of dln
+            RowVals<R> xo, xh3, gl;
+            if constexpr (LN2) {
+                row_affine<R>(xh2, sub, D, prm[3], prm[4], xo);
+            } else {
+                if (extra) row_load<R>(extra + tt * D, sub, D, q);
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xo[j][i] = x[j][i] + (extra ? q[j][i] : 0.f);
+            }
+            if constexpr (DROP)
+#pragma unroll
+                for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xo[j][i] *= keep_factor_bit(bits[j], 4 + i, k2);
+            row_normalise<R>(xo, sub, D, st3.x, st3.y, xh3);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    acc[4][j][i] += dl[j][i] * xh3[j][i];
+                    acc[5][j][i] += dl[j][i];
+                }
+            row_ln_bwd<R>(dl, xh3, prm[2], st3.y, sub, D, gl);
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) g[j][i] += gl[j][i];
+        }
+        if constexpr (DROP)
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) g[j][i] *= keep_factor_bit(bits[j], 4 + i, k2);
+        RowVals<R> gz;
+        if constexpr (LN2) {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    acc[2][j][i] += g[j][i] * xh2[j][i];
+                    acc[3][j][i] += g[j][i];
+                }
+            row_ln_bwd<R>(g, xh2, prm[3], st.w, sub, D, gz);
+        } else {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) gz[j][i] = g[j][i];
+        }
+        if (d_extra && t < T) row_store<R>(d_extra + t * D, sub, D, gz);
+        if constexpr (DROP)
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) gz[j][i] *= keep_factor_bit(bits[j], i, k1);
+        if (w1) {
+#pragma unroll
+            for (int j = 0; j < R::NV; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    acc[0][j][i] += gz[j][i] * xh1[j][i];
+                    acc[1][j][i] += gz[j][i];
+                }
+            RowVals<R> gx;
+            row_ln_bwd<R>(gz, xh1, prm[0], st.y, sub, D, gx);
+            if (t < T) row_store<R, ASME_EMB_NT>(d_rows + t * D, sub, D, gx);
+        } else if (t < T) {
+            row_store<R, ASME_EMB_NT>(d_rows + t * D, sub, D, gz);
+        }
+    }
+    if (partials) write_row_partials<R, NACC, kWavesPerBlock>(acc, lane, wave, D, partials);
+}
+
 template <int VPL>
 __global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float* __restrict__ rows,
                                                                const int64_t* __restrict__ ids, int64_t n, int D,
@@ -907,6 +1114,12 @@ inline int vpl_of(int64_t D) { return (int)((D + 63) / 64); }
 #ifndef ASME_EMB_K
 #define ASME_EMB_K 1
 #endif
+#ifndef ASME_EMB_BWD_PASS
+#define ASME_EMB_BWD_PASS 1
+#endif
+#ifndef ASME_EMB_BWD128
+#define ASME_EMB_BWD128 1  // 0: the D = 128 backward on the general emb_bwd4_kernel (A/B)
+#endif
 template <class F>
 int with_emb_layout(int64_t D, F&& f, bool lpr16 = ASME_EMB_LPR16) {
     if (lpr16 && D == 128) {
@@ -1011,14 +1224,35 @@ int embedding_bwd(const int64_t* ids, int64_t n_tokens, int64_t seq_len, const f
             // grid-stride with one partial row per block when the LN parameter grads are wanted
             const int64_t nb = partials ? n_partials : (n_tokens + rows - 1) / rows;
             if constexpr (R::W == 4) {
-                constexpr int kPass = 1;  // 2 tokens per pass: 160 VGPRs, 3 waves/SIMD, slower (169 vs 121 us)
+                constexpr int kPass = ASME_EMB_BWD_PASS;  // 2 tokens per pass at 16 lanes: 160 VGPRs, slower (169 vs 121 us)
                 const int64_t nb4 = partials ? n_partials : (n_tokens + rows - 1) / rows;
+                // D = 128 (16 lanes x two float4) with the keep bytes given or no dropout: the straight-line kernel
+                const bool fast = ASME_EMB_BWD128 && R::LPR == 16 && R::NV == 2 && dim == 128 &&
+                                  (keep_mask || (p1 == 0.f && p2 == 0.f));
                 auto launch = [&](auto ln3_tag, auto ln2_tag) {
                     constexpr bool LN3 = decltype(ln3_tag)::value, LN2 = decltype(ln2_tag)::value;
-                    hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass, LN3, LN2>), dim3((unsigned)nb4),
-                                       dim3(256), lds, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab,
-                                       (int)dim, pos_table, ln1_w, ln1_b, p1, extra, ln2_w, p2, emb_seed(seed1, seed2),
-                                       keep_mask, dout, stats, d_rows, d_extra, partials, l3 ? *l3 : EmbLn3{});
+                    auto go = [&](auto pos_tag, auto drop_tag) {
+                        constexpr bool POS = decltype(pos_tag)::value, DROP = decltype(drop_tag)::value;
+                        hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd128_kernel<LN3, LN2, POS, DROP>), dim3((unsigned)nb4),
+                                           dim3(256), lds, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab,
+                                           pos_table, ln1_w, ln1_b, p1, extra, ln2_w, p2, keep_mask, dout, stats, d_rows,
+                                           d_extra, partials, l3 ? *l3 : EmbLn3{});
+                    };
+                    const bool drop = keep_mask && (p1 > 0.f || p2 > 0.f);
+                    if (fast) {
+                        if (pos_table) {
+                            if (drop) go(std::true_type{}, std::true_type{});
+                            else go(std::true_type{}, std::false_type{});
+                        } else {
+                            if (drop) go(std::false_type{}, std::true_type{});
+                            else go(std::false_type{}, std::false_type{});
+                        }
+                    } else
+                        hipLaunchKernelGGL(HIP_KERNEL_NAME(emb_bwd4_kernel<R, kPass, LN3, LN2>), dim3((unsigned)nb4),
+                                           dim3(256), lds, (hipStream_t)stream, ids, n_tokens, seq_len, table, vocab,
+                                           (int)dim, pos_table, ln1_w, ln1_b, p1, extra, ln2_w, p2,
+                                           emb_seed(seed1, seed2), keep_mask, dout, stats, d_rows, d_extra, partials,
+                                           l3 ? *l3 : EmbLn3{});
                 };
                 if (l3) {
                     if (ln2_w) launch(std::true_type{}, std::true_type{});

@@ -81,7 +81,10 @@ __device__ __forceinline__ int wslot(int r, int s, int K4) { return r * K4 + (s 
 #endif
 constexpr int kNtMinN = ASME_WS_NT_MIN_N;
 #ifndef ASME_WS_DIAG
-#define ASME_WS_DIAG 0  // diagnostic builds (tools/ws_ab.py): 1 no MFMA, 2 no stores, 3 no W reads in the loop, 4 no X
+#define ASME_WS_DIAG 0  // diagnostic builds (tools/ws_ab.py): 1 no MFMA, 2 no stores, 3 no W reads in the loop, 4 no X,
+#endif                  // 5 no bf16 split of X (one plane reinterpreted: wrong products, timing only)
+#ifndef ASME_WS_PRIO_MFMA
+#define ASME_WS_PRIO_MFMA 0  // > 0: a wave raises its issue priority to this for each block's MFMA chain (experiment)
 #endif
 __device__ __forceinline__ void bstore(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
     if (ASME_WS_DIAG == 2) off = kDrop;
@@ -193,6 +196,13 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             return r;
         } else {
             (void)c;
+            if (ASME_WS_DIAG == 5) {
+                Bf3 r;
+                r.h = __builtin_bit_cast(bf16x8, a);
+                r.m = r.h;
+                r.l = __builtin_bit_cast(bf16x8, b);
+                return r;
+            }
             return split_bf3(a, b);
         }
     };
@@ -376,6 +386,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             const int kb = kq + d;
             const int kbn = kb + 1 == NKB ? 0 : kb + 1;
             // each feature tile's six MFMAs, then its next-block W read into the registers they consumed
+            if (ASME_WS_PRIO_MFMA) __builtin_amdgcn_s_setprio(ASME_WS_PRIO_MFMA);
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
 #if ASME_WS_DIAG != 1
@@ -389,6 +400,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
 #endif
                 __builtin_amdgcn_sched_barrier(0);
             }
+            if (ASME_WS_PRIO_MFMA) __builtin_amdgcn_s_setprio(0);
             // refill the slot just consumed: block kb + RD of this tile or of the next one (unconditional,
             // so the vmcnt bookkeeping stays exact; past the last tile it re-reads the last one)
             const float* src = kb + RD < NKB ? rc : rn;
