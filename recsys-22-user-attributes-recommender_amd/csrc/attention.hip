@@ -620,7 +620,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
 // fully-masked 16-key sub-tiles are skipped.  Used when 2 * ceil(L/16)*16 * (dk+4) * 4 B fits the
 // 160 KiB LDS (L <= 300 at dk = 64); the streaming kernels above cover the rest.
 #ifndef ASME_ATTN_DIAG
-#define ASME_ATTN_DIAG 0  // diagnostic builds only: 1 = the resident kernels skip their per-head operand loads
+#define ASME_ATTN_DIAG 0  // diagnostic builds only: 1 = the resident kernels skip their per-head operand loads,
+                          // 2 = the dK/dV pass skips its dS stores (the dQ pass reads stale dS: timing only)
 #endif
 #ifndef ASME_RES_THREADS
 #define ASME_RES_THREADS 768  // 12 waves: 3 per SIMD (512: 245/605 us fwd/bwd, 768: 231/588)
@@ -1083,7 +1084,7 @@ __global__ __launch_bounds__(kResThreadsKV) void attn_bwd_dkdv_res_kernel(
                     pd[r] = ok ? __fmul_rn(pr, f) : 0.f;
                     ds[r] = (ok && !masked) ? __fmul_rn(pr, __fmaf_rn(dpv[r], f, -pick(ds4, r))) : 0.f;
                 }
-                if (DS) {  // dS[query q4 + r][key kj]: 16 lanes of a group store 64 contiguous bytes per row
+                if (DS && ASME_ATTN_DIAG != 2) {  // dS[query q4 + r][key kj]: 16 lanes of a group store 64 contiguous bytes per row
 #pragma unroll
                     for (int r = 0; r < 4; ++r) ds_head[(int64_t)(q4 + r) * Lp + kj] = ds[r];
                 }
