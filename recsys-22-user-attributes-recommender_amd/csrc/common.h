@@ -131,29 +131,31 @@ __device__ __forceinline__ float dropout_factor(uint64_t seed, uint32_t salt, ui
 }
 
 // GELU(x) = x * Phi(x), Phi(x) = 0.5 * (1 + erf(x / sqrt 2)) (nn.GELU(), the exact-erf form the reference uses) and
-// its derivative Phi(x) + x * phi(x).  Phi from erfc: erfc(a) = t * exp(-a^2 + P(t)), t = 1 / (1 + a / 2) (the
-// Chebyshev fit of Numerical Recipes, fractional error < 1.2e-7 everywhere, so the negative tail keeps its
-// RELATIVE accuracy), 1 + erf(z) = 2 - erfc(z) for z >= 0 and erfc(-z) below: one reciprocal, two exponentials
-// and ten FMAs per element for both values -- the FFN epilogues evaluate it for all T x 4d activations and are
-// VALU-bound on libm's erff (56 instructions for the pair, 22 here).
+// its derivative Phi(x) + x * phi(x).  Phi from erfc: erfc(a) = t * exp(-a^2) * Q(t), t = 1 / (1 + a / 2), where Q
+// is a degree-10 weighted Chebyshev fit of erfcx(a) / t over t in (0, 1] (every a >= 0; relative error 4e-8, so the
+// negative tail keeps its RELATIVE accuracy), and 1 + erf(z) = 2 - erfc(z) for z >= 0, erfc(-z) below.  With
+// a^2 = x^2 / 2 the exponential is phi's own, so both values cost one reciprocal, ONE exponential and eleven FMAs
+// (the FFN epilogues evaluate them for all T x 4d activations and are VALU-bound on them; libm's erff alone is 56
+// instructions for the pair).  The coefficients carry Phi's 1/2.
 __device__ __forceinline__ void gelu_erf_and_grad(float x, float& gelu, float& grad) {
-    const float z = x * 0.70710678118654752f;
-    const float a = fabsf(z);
+    const float a = fabsf(x) * 0.70710678118654752f;
     const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * a);
-    float p = 0.17087277f;
-    p = fmaf(p, t, -0.82215223f);
-    p = fmaf(p, t, 1.48851587f);
-    p = fmaf(p, t, -1.13520398f);
-    p = fmaf(p, t, 0.27886807f);
-    p = fmaf(p, t, -0.18628806f);
-    p = fmaf(p, t, 0.09678418f);
-    p = fmaf(p, t, 0.37409196f);
-    p = fmaf(p, t, 1.00002368f);
-    p = fmaf(p, t, -1.26551223f);
-    const float erfc_a = t * __expf(fmaf(-a, a, p));
-    const float cdf = 0.5f * (z >= 0.f ? 2.0f - erfc_a : erfc_a);
+    float q = 0.022210972383618355f;
+    q = fmaf(q, t, -0.12038972973823547f);
+    q = fmaf(q, t, 0.2531980574131012f);
+    q = fmaf(q, t, -0.23490440845489502f);
+    q = fmaf(q, t, 0.07135776430368423f);
+    q = fmaf(q, t, -0.03194592893123627f);
+    q = fmaf(q, t, 0.04737446457147598f);
+    q = fmaf(q, t, 0.08755350857973099f);
+    q = fmaf(q, t, 0.12345138192176819f);
+    q = fmaf(q, t, 0.14104652404785156f);
+    q = fmaf(q, t, 0.141047403216362f);
+    const float e = __expf(-0.5f * x * x);  // exp(-a^2) = sqrt(2 pi) phi(x)
+    const float h = t * e * q;              // erfc(a) / 2
+    const float cdf = x >= 0.f ? 1.0f - h : h;
     gelu = x * cdf;
-    grad = fmaf(x * 0.3989422804014327f, __expf(-0.5f * x * x), cdf);
+    grad = fmaf(x * 0.3989422804014327f, e, cdf);
 }
 __device__ __forceinline__ float gelu_erf(float x) {
     float g, d;
