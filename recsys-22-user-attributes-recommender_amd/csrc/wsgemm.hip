@@ -106,14 +106,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
 // (the input gradient dX = dY W of a layer whose weight is N_out x N_in = K x N).
 // XP: X arrives already split into its three bf16 planes ([3][M][ldx] bf16, written by its producer): the ring holds
 // the planes and the loop issues no split VALU (an experiment: asme_ws_linear_planes)
-template <int K, int CT, bool TRANS, int EPI, bool XP = false>
-__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ws_gemm_kernel(
+#ifndef ASME_WS16
+#define ASME_WS16 0  // 1: the K = 128 store launches on 16-wave workgroups, four waves per SIMD (experiment)
+#endif
+#ifndef ASME_WS16_RD
+#define ASME_WS16_RD 2
+#endif
+#ifndef ASME_WS16_WR
+#define ASME_WS16_WR 2
+#endif
+template <int K, int CT, bool TRANS, int EPI, bool XP = false, int WV = kWaves>
+__global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4, WV / 4))) void ws_gemm_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W, int N, float* __restrict__ Y, WsEpi ep) {
+    constexpr int kWaves = WV;   // waves per workgroup (one workgroup per CU)
     constexpr int NB = 16 * CT;  // output features per workgroup
     // k32 blocks of X in flight: the whole 8-block tile for the first K = 256 half of the FFN-out forward (its waves
     // wait on X most; 256 VGPRs, no spill; tools/ws_ab.py same process 180 -> 173 us per product; the input-gradient
     // form and K = 384 measured flat or slower with a deeper ring)
-    constexpr int RD = (K == 256 && EPI == WS_STORE && !TRANS) ? 8 : kD;
+    constexpr int RD = WV == 16 ? ASME_WS16_RD : (K == 256 && EPI == WS_STORE && !TRANS) ? 8 : kD;
     constexpr int K8 = K / 8;    // 16-B slots (8 bf16) of a W image row
     constexpr int NKB = K / 32;
     constexpr int PL = NB * K8;  // slots of one bf16 plane
@@ -129,7 +139,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     constexpr bool kStage = CT >= 4 && NB * K * 6 + kWaves * 16 * SROW * 4 <= kLdsMax;  // (CT = 2: no gain)
     // W fragments in flight: one k32 block ahead for every feature tile (CT <= 6), or a ring of four tiles ahead
     // (CT = 8: 48 instead of 96 registers; still 24 MFMAs between a fragment's read and its use)
-    constexpr int WR = CT <= 6 ? CT : 4;
+    constexpr int WR = WV == 16 ? ASME_WS16_WR : CT <= 6 ? CT : 4;
     extern __shared__ __attribute__((aligned(16))) uint4 lds16[];
     const int nblk = N / NB;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
@@ -448,14 +458,15 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
     for (int ct = 0; ct < CT; ++ct) epilogue(ct);  // the last tile
 }
 
-template <int K, int CT, bool TRANS, int EPI, bool XP = false>
+template <int K, int CT, bool TRANS, int EPI, bool XP = false, int WV = kWaves>
 int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
+    constexpr int kWaves = WV;
     constexpr int NB = 16 * CT;
     const size_t planes = (size_t)NB * K * 6;  // three bf16 planes
     const size_t stage = (size_t)kWaves * 16 * (CT == 8 ? NB : NB + 4) * 4;  // (the kernel's SROW)
     const size_t lds = planes + (CT >= 4 && planes + stage <= (size_t)kLdsMax ? stage : 0);
     // opt in above 64 KiB of dynamic LDS once per instantiation (a function-local static: thread-safe initialisation)
-    static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI, XP>,
+    static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI, XP, WV>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return hip_status(attr, "asme_ws_linear: LDS opt-in");
     int dev = 0, cus = 256;
@@ -467,7 +478,7 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
         set_error("asme_ws_linear: more feature blocks than workgroups per XCD for this epilogue");
         return -1;
     }
-    hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI, XP>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M,
+    hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI, XP, WV>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M,
                        W, N, Y, ep);
     return hip_status(hipGetLastError(), "asme_ws_linear");
 }
@@ -492,6 +503,8 @@ int pick_ct(int N, int K) {
 
 template <int K, bool TRANS, int EPI>
 int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
+    if constexpr (ASME_WS16 && K == 128 && EPI == WS_STORE)
+        if (N % 64 == 0 && N / 64 <= 32) return launch_ws<K, 4, TRANS, EPI, false, 16>(X, M, W, N, Y, ep, s);
     if constexpr (64 * K * 6 <= kLdsMax)
         if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
     if constexpr (K == 128)
