@@ -668,11 +668,13 @@ def test_sasrec_sparse_lazy_matches_dense_training(asme, dev):
         assert _rel(results[1][k], results[0][k]) < 1e-5, k
 
 
-@pytest.mark.parametrize("lazy_table", [True, False])
-def test_sharded_module_single_rank_matches_unsharded(asme, dev, lazy_table):
+@pytest.mark.parametrize("lazy_table,overlap", [(True, False), (False, False), (True, True)])
+def test_sharded_module_single_rank_matches_unsharded(asme, dev, lazy_table, overlap):
     """The row-sharded training path (dedup -> all_to_all routing -> owner catch-up/gather -> compact
     table -> grad push -> lazy Adam on the shard) on a 1-rank RCCL group equals plain training.  lazy_table=False:
-    the owner's distinct-id plan hands the non-lazy row Adam (asme_adam_rows_step) its row -> slot map."""
+    the owner's distinct-id plan hands the non-lazy row Adam (asme_adam_rows_step) its row -> slot map.
+    overlap=True: the negatives' rows in the second, asynchronous RCCL all-to-all the sampled head waits for
+    (overlap_negatives), with the next batch's routing prefetched as bench.py does."""
     import os
     import torch.distributed as dist
     from helpers import build_model, load, state_dict
@@ -695,12 +697,12 @@ def test_sharded_module_single_rank_matches_unsharded(asme, dev, lazy_table):
             model.to(dev)
             if sharded:
                 module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(
-                    model=model, item_tokenizer=tok, metrics=None, vocab=V)
+                    model=model, item_tokenizer=tok, metrics=None, vocab=V, overlap_negatives=overlap)
                 opt = asme.optim.FusedAdam(module.parameters(), lr=module.learning_rate,
                                            betas=(module.beta_1, module.beta_2), weight_decay=module.weight_decay,
                                            lazy_table=lazy_table)
                 for i in range(3):
-                    asme.sharded.train_step(module, opt, batch, i)
+                    asme.sharded.train_step(module, opt, batch, i, next_batch=batch if overlap and i < 2 else None)
             else:
                 module = asme.SequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok, metrics=None,
                                                                        table_grad="sparse")

@@ -15,7 +15,9 @@ Reference: DDP semantics (Lightning, per-rank mean loss, gradients averaged over
     evaluation) against an unsharded run on the same GPU -- full-length sequences, so W ranks on batch slices ==
     one process on the whole batch;
   * test_sharded_full_vocabulary_matches_unsharded: BASELINE C4's table (|V| = 10,000,003, d = 128, L = 200) row-sharded
-    over 2 ranks against the unsharded path, every row of both shards compared."""
+    over 2 ranks against the unsharded path, every row of both shards compared;
+  * test_sharded_zipf_load_matches_unsharded: Zipf(1.07) ids (hot owners, uneven all-to-all splits) at W = 4,
+    L = 200, plain and overlapped exchange, against the same DDP-serial unsharded run."""
 import os
 import socket
 import sys
@@ -217,7 +219,16 @@ def test_sharded_training_matches_reference_ddp(world, overlap):
         assert not bad, (rank, bad)
 
 
-def _full_worker(rank, world, port, q):
+def _zipf_ids(n, V, g, s=1.07):
+    """Zipf(s) item ids over 3 .. V-1 by the inverse CDF of the continuous power law (bench.session_ids' form): id 3
+    the hottest, a few ids on a large share of the batch"""
+    u = torch.rand(n, generator=g, dtype=torch.float64)
+    m = V - 3
+    k = (1.0 + u * (m ** (1.0 - s) - 1.0)) ** (1.0 / (1.0 - s))
+    return (k.floor().long().clamp(1, m) + 2)
+
+
+def _full_worker(rank, world, port, cfg, q):
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
     import __graft_entry__
@@ -226,11 +237,15 @@ def _full_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     try:
-        V, L, d, h, N, B, steps = 10_000_003, 200, 128, 2, 2, 4 * world, 2
+        V, per_rank, ids, overlap = cfg
+        L, d, h, N, B, steps = 200, 128, 2, 2, per_rank * world, 2
         g = torch.Generator().manual_seed(77)
         batches = []
         for _ in range(steps):
-            seq = torch.randint(3, V, (B, L + 1), generator=g)
+            if ids == "zipf":
+                seq = _zipf_ids(B * (L + 1), V, g).view(B, L + 1)
+            else:
+                seq = torch.randint(3, V, (B, L + 1), generator=g)
             seq[1, 150:] = 0  # ragged: per-rank token counts differ
             neg = torch.randint(3, V, (B, L), generator=g)
             neg[seq[:, :L] == 0] = 0
@@ -276,12 +291,14 @@ def _full_worker(rank, world, port, q):
         with torch.no_grad():
             model.item_table().copy_(init_shard)
         module = asme.sharded.ShardedSequenceNextItemPredictionTrainingModule(model=model, item_tokenizer=tok,
-                                                                              metrics=None, vocab=V)
+                                                                              metrics=None, vocab=V,
+                                                                              overlap_negatives=overlap)
         opt = module.configure_optimizers()
         losses = []
-        for s, b in enumerate(batches):
-            part = {k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()}
-            losses.append(float(asme.sharded.train_step(module, opt, part, s)))
+        parts = [{k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()} for b in batches]
+        for s, part in enumerate(parts):
+            losses.append(float(asme.sharded.train_step(module, opt, part, s,
+                                                        next_batch=parts[s + 1] if s + 1 < len(parts) else None)))
         opt.flush()
         errs = {"loss": max(abs(a - b) / abs(b) for a, b in zip(losses, ref_losses))}
         shard = model.item_table().detach()
@@ -304,7 +321,24 @@ def test_sharded_full_vocabulary_matches_unsharded():
     ragged batches, against the unsharded path with DDP semantics; the whole shard (5 million rows) compared"""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm GPU")
-    res = _spawn(_full_worker, 2)
+    res = _spawn(_full_worker, 2, ((10_000_003, 4, "uniform", False),))
+    for rank, errs in res.items():
+        assert isinstance(errs, dict), f"rank {rank}: {errs}"
+        for k, e in errs.items():
+            if k.endswith("attention.linear_layers.1.bias"):
+                continue
+            assert e == 0 if k == "table_rows_unchanged" else e < 1e-4, (rank, k, e)
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_sharded_zipf_load_matches_unsharded(overlap):
+    """Load shape at scale: Zipf(1.07) sequence ids (the hottest item on several percent of the tokens, so a few owners
+    receive far more requests than the rest and the all-to-all splits are uneven) over |V| = 400,003 rows, W = 4
+    ranks x 16 sessions x L = 200, two steps with the next batch's routing prefetched, against the unsharded path
+    with DDP semantics -- the whole shard compared; overlap: the negatives' rows in the second exchange"""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm GPU")
+    res = _spawn(_full_worker, 4, ((400_003, 16, "zipf", overlap),))
     for rank, errs in res.items():
         assert isinstance(errs, dict), f"rank {rank}: {errs}"
         for k, e in errs.items():
