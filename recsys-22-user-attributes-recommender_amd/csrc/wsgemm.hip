@@ -115,6 +115,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
 #ifndef ASME_WS16_WR
 #define ASME_WS16_WR 2
 #endif
+#ifndef ASME_WSREG
+#define ASME_WSREG 0  // 1: K = 128 launches at one wave per SIMD with the whole W block in registers (experiment)
+#endif
 template <int K, int CT, bool TRANS, int EPI, bool XP = false, int WV = kWaves>
 __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4, WV / 4))) void ws_gemm_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W, int N, float* __restrict__ Y, WsEpi ep) {
@@ -123,7 +126,9 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
     // k32 blocks of X in flight: the whole 8-block tile for the first K = 256 half of the FFN-out forward (its waves
     // wait on X most; 256 VGPRs, no spill; tools/ws_ab.py same process 180 -> 173 us per product; the input-gradient
     // form and K = 384 measured flat or slower with a deeper ring)
-    constexpr int RD = WV == 16 ? ASME_WS16_RD : (K == 256 && EPI == WS_STORE && !TRANS) ? 8 : kD;
+    // WV = 4: one wave per SIMD, 512 registers: every W fragment of the block held in registers (no W reads in the loop)
+    constexpr bool kRegW = WV == 4;
+    constexpr int RD = kRegW ? K / 32 : WV == 16 ? ASME_WS16_RD : (K == 256 && EPI == WS_STORE && !TRANS) ? 8 : kD;
     constexpr int K8 = K / 8;    // 16-B slots (8 bf16) of a W image row
     constexpr int NKB = K / 32;
     constexpr int PL = NB * K8;  // slots of one bf16 plane
@@ -279,8 +284,17 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
         return w;
     };
     Bf3 wc[WR];  // wc[ct % WR] holds tile ct's fragment of the current block when its MFMAs run
+    Bf3 wall[kRegW ? CT : 1][kRegW ? NKB : 1];  // kRegW: the whole block
+    static_assert(!kRegW || NKB == RD, "register-resident W: one trip of RD blocks per tile");
+    if constexpr (kRegW) {
 #pragma unroll
-    for (int ct = 0; ct < WR; ++ct) wc[ct] = wload(ct, 0);
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) wall[ct][kb] = wload(ct, kb);
+    } else {
+#pragma unroll
+        for (int ct = 0; ct < WR; ++ct) wc[ct] = wload(ct, 0);
+    }
     Bf3 xs = xsplit(ring[0], ring[1], ring3[0]);
     // the stashed tile's epilogue for one 16-feature tile
     auto epilogue = [&](int ct) {
@@ -399,6 +413,11 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
             if (ASME_WS_PRIO_MFMA) __builtin_amdgcn_s_setprio(ASME_WS_PRIO_MFMA);
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
+                if constexpr (kRegW) {
+                    acc[ct] = mfma_bf3(wall[ct][kRegW ? kb : 0], xs, acc[ct]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    continue;
+                }
 #if ASME_WS_DIAG != 1
                 acc[ct] = mfma_bf3(wc[ct % WR], xs, acc[ct]);
 #else
@@ -505,6 +524,8 @@ template <int K, bool TRANS, int EPI>
 int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
     if constexpr (ASME_WS16 && K == 128 && EPI == WS_STORE)
         if (N % 64 == 0 && N / 64 <= 32) return launch_ws<K, 4, TRANS, EPI, false, 16>(X, M, W, N, Y, ep, s);
+    if constexpr (ASME_WSREG && K == 128 && (EPI == WS_STORE || EPI == WS_GELU_DROP || EPI == WS_GELU_BWD))
+        if (N % 64 == 0 && N / 64 <= 32) return launch_ws<K, 4, TRANS, EPI, false, 4>(X, M, W, N, Y, ep, s);
     if constexpr (64 * K * 6 <= kLdsMax)
         if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
     if constexpr (K == 128)
