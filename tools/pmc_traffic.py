@@ -23,8 +23,11 @@ MAP = [
     (r"attn_bwd_dkdv(_res)?_kernel", "asme_attention_bwd", False),
     (r"weight_grad_kernel", "asme_linear_weight_grad", True),
     (r"sum_slabs(_cols)?_kernel", "asme_linear_weight_grad", False),
-    (r"emb_fwd4_kernel<.*, true>", "asme_embedding_ln_fwd", True),  # + block 0's input LayerNorm
-    (r"emb_bwd4_kernel<.*, true>", "asme_embedding_ln_bwd", True),
+    # <RowLayout, k, LN3, LN2>: LN3 (block 0's input LayerNorm fused) makes the call the _ln form
+    (r"emb_fwd4_kernel<asme::RowLayout<[^>]*>, \d+, true", "asme_embedding_ln_fwd", True),
+    (r"emb_bwd4_kernel<asme::RowLayout<[^>]*>, \d+, true", "asme_embedding_ln_bwd", True),
+    (r"emb_bwd128_kernel<true", "asme_embedding_ln_bwd", True),  # (LN3: the fused next LayerNorm)
+    (r"emb_bwd128_kernel", "asme_embedding_bwd", True),
     (r"emb_fwd4?_kernel", "asme_embedding_fwd", True),
     (r"emb_bwd4?_kernel", "asme_embedding_bwd", True),
     (r"lazy_catch_up(_v4)?_kernel", "asme_lazy_adam_catch_up", True),
