@@ -86,6 +86,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
 }
 
 // ------------------------------------------------------------ residual + dropout(s) + LayerNorm
+#ifndef ASME_RLN_NT
+#define ASME_RLN_NT 3  // non-temporal stores in residual_ln_fwd (bit 0: s, bit 1: LN(s)) / _bwd (bit 2: d_res, bit 3: d_y)
+#endif
 template <class R>
 __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(
     const float* __restrict__ res, const float* __restrict__ y, int64_t T, int D, float pa, uint64_t sa, float pb,
@@ -109,13 +112,13 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(
         row_keep<R>(sb, 4u, (uint64_t)t * D, sub, pb, f);
         row_mul<R>(h, f);
     }
-    row_store<R>(s_out + t * D, sub, D, h);
+    row_store<R, (ASME_RLN_NT & 1) != 0>(s_out + t * D, sub, D, h);
     if (w) {
         float m, r;
         row_ln_stats<R>(h, sub, D, eps, m, r);
         row_normalise<R>(h, sub, D, m, r, a);
         row_affine<R>(a, sub, D, w, b, f);
-        row_store<R>(ln_out + t * D, sub, D, f);
+        row_store<R, (ASME_RLN_NT & 2) != 0>(ln_out + t * D, sub, D, f);
         if (sub == 0) {
             stats[t * 2] = m;
             stats[t * 2 + 1] = r;
@@ -172,13 +175,13 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
             row_keep<R>(sb, 4u, (uint64_t)t * D, sub, pb, f);
             row_mul<R>(g, f);
         }
-        row_store<R>(d_res + t * D, sub, D, g);
+        row_store<R, (ASME_RLN_NT & 4) != 0>(d_res + t * D, sub, D, g);
         if (d_y) {
             if (pa > 0.f) {
                 row_keep<R>(sa, 3u, (uint64_t)t * D, sub, pa, f);
                 row_mul<R>(g, f);
             }
-            row_store<R>(d_y + t * D, sub, D, g);
+            row_store<R, (ASME_RLN_NT & 8) != 0>(d_y + t * D, sub, D, g);
         }
     }
     if (partials) write_row_partials<R, 2, kWaves>(acc, lane, wave, D, partials);
