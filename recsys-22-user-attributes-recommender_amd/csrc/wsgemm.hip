@@ -115,6 +115,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
 #ifndef ASME_WS16_WR
 #define ASME_WS16_WR 2
 #endif
+#ifndef ASME_WS_KSPLIT
+#define ASME_WS_KSPLIT 1  // K = 512 plain products as two K = 256 launches (0: one launch, 32-feature blocks; A/B)
+#endif
+#ifndef ASME_WS512_WV16
+#define ASME_WS512_WV16 0  // with ASME_WS_KSPLIT=0: the one-launch K = 512 product at four waves per SIMD (A/B)
+#endif
 #ifndef ASME_WSREG
 #define ASME_WSREG 0  // 1: K = 128 launches at one wave per SIMD with the whole W block in registers (experiment)
 #endif
@@ -524,6 +530,8 @@ template <int K, bool TRANS, int EPI>
 int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
     if constexpr (ASME_WS16 && K == 128 && EPI == WS_STORE)
         if (N % 64 == 0 && N / 64 <= 32) return launch_ws<K, 4, TRANS, EPI, false, 16>(X, M, W, N, Y, ep, s);
+    if constexpr (ASME_WS512_WV16 && K == 512 && EPI == WS_STORE)
+        if (ct == 2) return launch_ws<K, 2, TRANS, EPI, false, 16>(X, M, W, N, Y, ep, s);
     if constexpr (ASME_WSREG && K == 128 && (EPI == WS_STORE || EPI == WS_GELU_DROP || EPI == WS_GELU_BWD))
         if (N % 64 == 0 && N / 64 <= 32) return launch_ws<K, 4, TRANS, EPI, false, 4>(X, M, W, N, Y, ep, s);
     if constexpr (64 * K * 6 <= kLdsMax)
@@ -582,7 +590,7 @@ ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W
     hipStream_t s = (hipStream_t)stream;
     // K = 512 plain stores: two K = 256 halves with 64-feature blocks (the 512-deep split W block only fits 32
     // features, which splits and re-reads X four times); the second half accumulates into Y
-    if (K == 512 && epi == 0 && pick_ct((int)N, 256) == 4) {
+    if (ASME_WS_KSPLIT && K == 512 && epi == 0 && pick_ct((int)N, 256) == 4) {
         const WsEpi e1{bias, nullptr, nullptr, 0.f, 0, 512, 512, 0};
         const WsEpi e2{nullptr, nullptr, nullptr, 0.f, 0, 512, 512, 256};
         const int rc = trans ? launch_ws<256, 4, true, WS_STORE>(X, M, W, (int)N, Y, e1, s)
