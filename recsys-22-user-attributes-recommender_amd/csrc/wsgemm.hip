@@ -83,9 +83,6 @@ constexpr int kNtMinN = ASME_WS_NT_MIN_N;
 #ifndef ASME_WS_DIAG
 #define ASME_WS_DIAG 0  // diagnostic builds (tools/ws_ab.py): 1 no MFMA, 2 no stores, 3 no W reads in the loop, 4 no X,
 #endif                  // 5 no bf16 split of X (one plane reinterpreted: wrong products, timing only)
-#ifndef ASME_WS_PRIO_MFMA
-#define ASME_WS_PRIO_MFMA 0  // > 0: a wave raises its issue priority to this for each block's MFMA chain (experiment)
-#endif
 __device__ __forceinline__ void bstore(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
     if (ASME_WS_DIAG == 2) off = kDrop;
     const u32v4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
@@ -106,35 +103,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
 // (the input gradient dX = dY W of a layer whose weight is N_out x N_in = K x N).
 // XP: X arrives already split into its three bf16 planes ([3][M][ldx] bf16, written by its producer): the ring holds
 // the planes and the loop issues no split VALU (an experiment: asme_ws_linear_planes)
-#ifndef ASME_WS16
-#define ASME_WS16 0  // 1: the K = 128 store launches on 16-wave workgroups, four waves per SIMD (experiment)
-#endif
-#ifndef ASME_WS16_RD
-#define ASME_WS16_RD 2
-#endif
-#ifndef ASME_WS16_WR
-#define ASME_WS16_WR 2
-#endif
-#ifndef ASME_WS_KSPLIT
-#define ASME_WS_KSPLIT 1  // K = 512 plain products as two K = 256 launches (0: one launch, 32-feature blocks; A/B)
-#endif
-#ifndef ASME_WS512_WV16
-#define ASME_WS512_WV16 0  // with ASME_WS_KSPLIT=0: the one-launch K = 512 product at four waves per SIMD (A/B)
-#endif
-#ifndef ASME_WSREG
-#define ASME_WSREG 0  // 1: K = 128 launches at one wave per SIMD with the whole W block in registers (experiment)
-#endif
-template <int K, int CT, bool TRANS, int EPI, bool XP = false, int WV = kWaves>
-__global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4, WV / 4))) void ws_gemm_kernel(
+// (round 6, measured and removed -- git history before the commit that dropped them: four waves per SIMD on 16-wave
+// workgroups, the W block register-resident at one wave per SIMD, K = 512 in one launch on 32-feature blocks, issue
+// priority around the MFMA chains; all slower)
+template <int K, int CT, bool TRANS, int EPI, bool XP = false>
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void ws_gemm_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W, int N, float* __restrict__ Y, WsEpi ep) {
-    constexpr int kWaves = WV;   // waves per workgroup (one workgroup per CU)
     constexpr int NB = 16 * CT;  // output features per workgroup
     // k32 blocks of X in flight: the whole 8-block tile for the first K = 256 half of the FFN-out forward (its waves
     // wait on X most; 256 VGPRs, no spill; tools/ws_ab.py same process 180 -> 173 us per product; the input-gradient
     // form and K = 384 measured flat or slower with a deeper ring)
-    // WV = 4: one wave per SIMD, 512 registers: every W fragment of the block held in registers (no W reads in the loop)
-    constexpr bool kRegW = WV == 4;
-    constexpr int RD = kRegW ? K / 32 : WV == 16 ? ASME_WS16_RD : (K == 256 && EPI == WS_STORE && !TRANS) ? 8 : kD;
+    constexpr int RD = (K == 256 && EPI == WS_STORE && !TRANS) ? 8 : kD;
     constexpr int K8 = K / 8;    // 16-B slots (8 bf16) of a W image row
     constexpr int NKB = K / 32;
     constexpr int PL = NB * K8;  // slots of one bf16 plane
@@ -150,7 +129,7 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
     constexpr bool kStage = CT >= 4 && NB * K * 6 + kWaves * 16 * SROW * 4 <= kLdsMax;  // (CT = 2: no gain)
     // W fragments in flight: one k32 block ahead for every feature tile (CT <= 6), or a ring of four tiles ahead
     // (CT = 8: 48 instead of 96 registers; still 24 MFMAs between a fragment's read and its use)
-    constexpr int WR = WV == 16 ? ASME_WS16_WR : CT <= 6 ? CT : 4;
+    constexpr int WR = CT <= 6 ? CT : 4;
     extern __shared__ __attribute__((aligned(16))) uint4 lds16[];
     const int nblk = N / NB;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
@@ -290,17 +269,8 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
         return w;
     };
     Bf3 wc[WR];  // wc[ct % WR] holds tile ct's fragment of the current block when its MFMAs run
-    Bf3 wall[kRegW ? CT : 1][kRegW ? NKB : 1];  // kRegW: the whole block
-    static_assert(!kRegW || NKB == RD, "register-resident W: one trip of RD blocks per tile");
-    if constexpr (kRegW) {
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) wall[ct][kb] = wload(ct, kb);
-    } else {
-#pragma unroll
-        for (int ct = 0; ct < WR; ++ct) wc[ct] = wload(ct, 0);
-    }
+    for (int ct = 0; ct < WR; ++ct) wc[ct] = wload(ct, 0);
     Bf3 xs = xsplit(ring[0], ring[1], ring3[0]);
     // the stashed tile's epilogue for one 16-feature tile
     auto epilogue = [&](int ct) {
@@ -416,14 +386,8 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
             const int kb = kq + d;
             const int kbn = kb + 1 == NKB ? 0 : kb + 1;
             // each feature tile's six MFMAs, then its next-block W read into the registers they consumed
-            if (ASME_WS_PRIO_MFMA) __builtin_amdgcn_s_setprio(ASME_WS_PRIO_MFMA);
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
-                if constexpr (kRegW) {
-                    acc[ct] = mfma_bf3(wall[ct][kRegW ? kb : 0], xs, acc[ct]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    continue;
-                }
 #if ASME_WS_DIAG != 1
                 acc[ct] = mfma_bf3(wc[ct % WR], xs, acc[ct]);
 #else
@@ -435,7 +399,6 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
 #endif
                 __builtin_amdgcn_sched_barrier(0);
             }
-            if (ASME_WS_PRIO_MFMA) __builtin_amdgcn_s_setprio(0);
             // refill the slot just consumed: block kb + RD of this tile or of the next one (unconditional,
             // so the vmcnt bookkeeping stays exact; past the last tile it re-reads the last one)
             const float* src = kb + RD < NKB ? rc : rn;
@@ -483,15 +446,14 @@ __global__ __launch_bounds__(WV * 64) __attribute__((amdgpu_waves_per_eu(WV / 4,
     for (int ct = 0; ct < CT; ++ct) epilogue(ct);  // the last tile
 }
 
-template <int K, int CT, bool TRANS, int EPI, bool XP = false, int WV = kWaves>
+template <int K, int CT, bool TRANS, int EPI, bool XP = false>
 int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
-    constexpr int kWaves = WV;
     constexpr int NB = 16 * CT;
     const size_t planes = (size_t)NB * K * 6;  // three bf16 planes
     const size_t stage = (size_t)kWaves * 16 * (CT == 8 ? NB : NB + 4) * 4;  // (the kernel's SROW)
     const size_t lds = planes + (CT >= 4 && planes + stage <= (size_t)kLdsMax ? stage : 0);
     // opt in above 64 KiB of dynamic LDS once per instantiation (a function-local static: thread-safe initialisation)
-    static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI, XP, WV>,
+    static const hipError_t attr = hipFuncSetAttribute((const void*)ws_gemm_kernel<K, CT, TRANS, EPI, XP>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return hip_status(attr, "asme_ws_linear: LDS opt-in");
     int dev = 0, cus = 256;
@@ -503,7 +465,7 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
         set_error("asme_ws_linear: more feature blocks than workgroups per XCD for this epilogue");
         return -1;
     }
-    hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI, XP, WV>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M,
+    hipLaunchKernelGGL((ws_gemm_kernel<K, CT, TRANS, EPI, XP>), dim3((cus / 8) * 8), dim3(kWaves * 64), lds, s, X, M,
                        W, N, Y, ep);
     return hip_status(hipGetLastError(), "asme_ws_linear");
 }
@@ -528,12 +490,6 @@ int pick_ct(int N, int K) {
 
 template <int K, bool TRANS, int EPI>
 int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float* Y, const WsEpi& ep, hipStream_t s) {
-    if constexpr (ASME_WS16 && K == 128 && EPI == WS_STORE)
-        if (N % 64 == 0 && N / 64 <= 32) return launch_ws<K, 4, TRANS, EPI, false, 16>(X, M, W, N, Y, ep, s);
-    if constexpr (ASME_WS512_WV16 && K == 512 && EPI == WS_STORE)
-        if (ct == 2) return launch_ws<K, 2, TRANS, EPI, false, 16>(X, M, W, N, Y, ep, s);
-    if constexpr (ASME_WSREG && K == 128 && (EPI == WS_STORE || EPI == WS_GELU_DROP || EPI == WS_GELU_BWD))
-        if (N % 64 == 0 && N / 64 <= 32) return launch_ws<K, 4, TRANS, EPI, false, 4>(X, M, W, N, Y, ep, s);
     if constexpr (64 * K * 6 <= kLdsMax)
         if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
     if constexpr (K == 128)
@@ -590,7 +546,7 @@ ASME_API int asme_ws_linear(const float* X, int64_t M, int64_t K, const float* W
     hipStream_t s = (hipStream_t)stream;
     // K = 512 plain stores: two K = 256 halves with 64-feature blocks (the 512-deep split W block only fits 32
     // features, which splits and re-reads X four times); the second half accumulates into Y
-    if (ASME_WS_KSPLIT && K == 512 && epi == 0 && pick_ct((int)N, 256) == 4) {
+    if (K == 512 && epi == 0 && pick_ct((int)N, 256) == 4) {
         const WsEpi e1{bias, nullptr, nullptr, 0.f, 0, 512, 512, 0};
         const WsEpi e2{nullptr, nullptr, nullptr, 0.f, 0, 512, 512, 256};
         const int rc = trans ? launch_ws<256, 4, true, WS_STORE>(X, M, W, (int)N, Y, e1, s)
