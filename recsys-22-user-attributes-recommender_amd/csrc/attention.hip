@@ -707,9 +707,6 @@ __device__ __forceinline__ int claim_group(int* ctl, int lane) {
     return __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
 }
 
-#ifndef ASME_ATTN_O_NT
-#define ASME_ATTN_O_NT 0  // A/B: non-temporal stores of the resident forward's output rows
-#endif
 template <int DK>
 __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, int64_t ldq, int64_t ldk,
@@ -836,14 +833,9 @@ __global__ __launch_bounds__(kResThreads) void attn_fwd_res_kernel(
             const float inv = 1.f / l;
             float* orow = o + (tok0 + qi) * ldo + h * DK;
 #pragma unroll
-            for (int ct = 0; ct < NCT; ++ct) {
-                const float4 ov = make_float4(acc[ct][0] * inv, acc[ct][1] * inv, acc[ct][2] * inv, acc[ct][3] * inv);
-                typedef float f4v __attribute__((ext_vector_type(4)));
-                if (ASME_ATTN_O_NT)
-                    __builtin_nontemporal_store(f4v{ov.x, ov.y, ov.z, ov.w}, reinterpret_cast<f4v*>(orow + ct * 16 + 4 * g));
-                else
-                    *reinterpret_cast<float4*>(orow + ct * 16 + 4 * g) = ov;
-            }
+            for (int ct = 0; ct < NCT; ++ct)
+                *reinterpret_cast<float4*>(orow + ct * 16 + 4 * g) =
+                    make_float4(acc[ct][0] * inv, acc[ct][1] * inv, acc[ct][2] * inv, acc[ct][3] * inv);
             if (g == 0) {
                 stats[((int64_t)bh * L + qi) * 2] = m;
                 stats[((int64_t)bh * L + qi) * 2 + 1] = inv;
