@@ -245,7 +245,11 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         xload(rc, d, ring[2 * d], ring[2 * d + 1], ring3[XP ? d : 0]);
         __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop's vmcnt waits assume it
     }
-    float4 stash[CT], pre[CT];
+    // GELU backward on 128-feature blocks: the activation factor of the stashed tile is read four feature tiles ahead
+    // of its epilogue (a 4-slot ring) instead of all CT at the tile boundary, which would need CT x 4 more registers
+    constexpr bool kLateA = EPI == WS_GELU_BWD && CT == 8;
+    constexpr int NPRE = kLateA ? 4 : CT;
+    float4 stash[CT], pre[NPRE];
     uint32_t soff = kDrop;  // byte offset of (row, n0 + 4g) of the stashed tile in Y
     int64_t srow0 = M;      // staged: first token of the stashed tile (M: none yet, every store dropped)
     float* stg = reinterpret_cast<float*>(lds16 + 3 * PL) + (threadIdx.x >> 6) * 16 * SROW;
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
         return stg + row * SROW + 4 * (kSwz ? (c4 ^ row) : c4);
     };
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) stash[ct] = pre[ct] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ct = 0; ct < CT; ++ct) stash[ct] = pre[ct % NPRE] = make_float4(0.f, 0.f, 0.f, 0.f);
     // W operand of feature tile ct, k32 block kb: row ct*16 + c16, k 8g..8g+7 of the three planes
     auto wload = [&](int ct, int kb) -> Bf3 {
         const int sl = wslot(ct * 16 + c16, kb * 4 + g, K8);
@@ -341,8 +345,10 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                     if (sub == 0 && t < M) *reinterpret_cast<float2*>(ep.stats + 2 * t) = make_float2(m, r);
                 }
             } else {
-                const float4 f = pre[ct];
+                const float4 f = pre[ct % NPRE];
                 bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off, nt_out);
+                if constexpr (kLateA)
+                    if (ct + NPRE < CT) pre[ct % NPRE] = bload(pr, staged_off(ct + NPRE, srow0));
             }
             return;
         }
@@ -370,7 +376,7 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
             bstore(make_float4(u[0] * gd[0], u[1] * gd[1], u[2] * gd[2], u[3] * gd[3]), pr, off, nt_out);
             bstore(make_float4(gl[0] * u[0], gl[1] * u[1], gl[2] * u[2], gl[3] * u[3]), yr, off, nt_out);
         } else {
-            const float4 f = pre[ct];
+            const float4 f = pre[ct % NPRE];
             bstore(make_float4(v.x * f.x, v.y * f.y, v.z * f.z, v.w * f.w), yr, off, nt_out);
         }
     };
@@ -429,14 +435,14 @@ __global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2, 
                              : make_float4(acc[ct][0] + breg[ct].x, acc[ct][1] + breg[ct].y, acc[ct][2] + breg[ct].z,
                                            acc[ct][3] + breg[ct].w);
                 if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM || EPI == WS_RESID_LN)
-                    pre[ct] = bload(pr, staged_off(ct, srow0));
+                    if (ct < NPRE) pre[ct] = bload(pr, staged_off(ct, srow0));
             }
         } else {
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 stash[ct] = make_float4(acc[ct][0] + breg[kBiasEpi ? 0 : ct].x, acc[ct][1] + breg[kBiasEpi ? 0 : ct].y,
                                         acc[ct][2] + breg[kBiasEpi ? 0 : ct].z, acc[ct][3] + breg[kBiasEpi ? 0 : ct].w);
-                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM || EPI == WS_RESID_LN) pre[ct] = bload(pr, soff + ct * 64);
+                if constexpr (EPI == WS_GELU_BWD || EPI == WS_ACCUM || EPI == WS_RESID_LN) pre[ct % NPRE] = bload(pr, soff + ct * 64);
             }
         }
         rc = rn;
@@ -473,6 +479,9 @@ int launch_ws(const float* X, int64_t M, const float* W, int N, float* Y, const 
 // features per workgroup: 64; 96 when N / 64 does not divide the 32 workgroups of an XCD (N = 384, K = 128:
 // wider tiles at larger K run out of registers); 32 when a 64-feature block of the three bf16 planes would
 // not fit the LDS (K = 512); else 64 with the XCD's leftover workgroups idle
+#ifndef ASME_WS_GBWD_CT8
+#define ASME_WS_GBWD_CT8 1  // the GELU backward on 128-feature blocks, its factor read four tiles ahead (0: 64-feature
+#endif                      // blocks, the whole tile's factor at the boundary; tools/ws_ab.py 211.3 -> 183.7 us)
 #ifndef ASME_WS_CT8
 #define ASME_WS_CT8 1
 #endif
@@ -494,8 +503,9 @@ int dispatch_ct(int ct, const float* X, int64_t M, const float* W, int N, float*
         if (ct == 4) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);
     if constexpr (K == 128)
         if (ct == 6) return launch_ws<K, 6, TRANS, EPI>(X, M, W, N, Y, ep, s);
-    // (the activation-factor epilogue keeps 64-feature blocks: its CT factor registers would spill at CT = 8)
-    if constexpr (K == 128 && EPI != WS_GELU_BWD)
+    // (the activation-factor epilogue on 128-feature blocks reads its factor through a 4-slot ring, kLateA: CT = 8
+    // factor registers at the tile boundary would spill)
+    if constexpr (K == 128 && (EPI != WS_GELU_BWD || ASME_WS_GBWD_CT8))
         if (ct == 8) return launch_ws<K, 8, TRANS, EPI>(X, M, W, N, Y, ep, s);
     if constexpr (K == 128 && EPI == WS_GELU_BWD)
         if (ct == 8) return launch_ws<K, 4, TRANS, EPI>(X, M, W, N, Y, ep, s);

@@ -69,8 +69,8 @@ def test_ws_linear_rejects_unsupported(asme):
 
 
 def test_ws_gelu_bwd_wide_feature_blocks(asme, dev):
-    """the activation-factor epilogue at K = 128, N = 2048 (a CT = 8 shape that runs on 64-feature blocks): every
-    output element written, equal to (dY W2) * factor"""
+    """the activation-factor epilogue at K = 128, N = 2048 (a CT = 8 shape: 128-feature blocks, the factor read through
+    the 4-slot ring): every output element written, equal to (dY W2) * factor"""
     torch.manual_seed(9)
     M, D, Fd = 3000, 128, 2048
     w2 = torch.randn(D, Fd, device=dev) / Fd ** 0.5
