@@ -532,7 +532,8 @@ ASME_API int asme_ws_linear_supported(int64_t M, int64_t K, int64_t N) {
     if (N > 4096 || pick_ct((int)N, (int)K) == 0) return 0;
     // the activation-factor epilogue runs CT = 8 shapes on 64-feature blocks (dispatch_ct): those must fit an XCD's
     // 32 workgroups too, so the shape is supported for every epilogue (K = 128, N = 4096)
-    if (pick_ct((int)N, (int)K) == 8 && !(N % 64 == 0 && 32 % (N / 64) == 0)) return 0;
+    // (with ASME_WS_GBWD_CT8 every epilogue runs CT = 8 shapes on 128-feature blocks: nothing to add)
+    if (!ASME_WS_GBWD_CT8 && pick_ct((int)N, (int)K) == 8 && !(N % 64 == 0 && 32 % (N / 64) == 0)) return 0;
     if (M * N * 4 >= (int64_t)kDrop || M * K * 4 >= ((int64_t)1 << 40)) return 0;
     return 1;
 }

@@ -62,17 +62,20 @@ def test_ws_linear_rejects_unsupported(asme):
     assert lib.asme_ws_linear_supported(100, 128, 100) == 0      # N not a multiple of 64 / 96
     assert lib.asme_ws_linear_supported(100, 512, 384) == 0      # split W block over 160 KiB of LDS
     assert lib.asme_ws_linear_supported(1 << 22, 128, 512) == 0  # Y over 2 GiB
-    # K = 128, N = 4096: 128-feature blocks fit an XCD's 32 workgroups, but the activation-factor epilogue's
-    # 64-feature blocks would not -- refused for every epilogue rather than leaving Y unwritten
-    assert lib.asme_ws_linear_supported(100, 128, 4096) == 0
+    # K = 128, N = 4096: 32 128-feature blocks fill an XCD's 32 workgroups -- every epilogue runs on 128-feature
+    # blocks (the activation-factor one since round 6), so it is taken; 4224 (33 blocks) is not
+    assert lib.asme_ws_linear_supported(100, 128, 4096) == 1
     assert lib.asme_ws_linear_supported(100, 128, 2048) == 1
+    assert lib.asme_ws_linear_supported(100, 128, 4224) == 0
 
 
-def test_ws_gelu_bwd_wide_feature_blocks(asme, dev):
-    """the activation-factor epilogue at K = 128, N = 2048 (a CT = 8 shape: 128-feature blocks, the factor read through
-    the 4-slot ring): every output element written, equal to (dY W2) * factor"""
+@pytest.mark.parametrize("Fd", [2048, 4096])
+def test_ws_gelu_bwd_wide_feature_blocks(asme, dev, Fd):
+    """the activation-factor epilogue at K = 128, N = 2048 / 4096 (CT = 8 shapes: 128-feature blocks, the factor read
+    through the 4-slot ring; 4096 = one block per workgroup of an XCD): every output element written, equal to
+    (dY W2) * factor"""
     torch.manual_seed(9)
-    M, D, Fd = 3000, 128, 2048
+    M, D = 3000, 128
     w2 = torch.randn(D, Fd, device=dev) / Fd ** 0.5
     dy = torch.randn(M, D, device=dev)
     fac = torch.rand(M, Fd, device=dev)
