@@ -132,7 +132,9 @@ def adam_excess(got, want, g, lr, rtol=1e-3, floor=1e-3):
     ag = np.abs(g)
     tol = rtol * (np.abs(want) + floor * np.abs(want).max()) + \
         lr * ADAM_EPS / (ag + ADAM_EPS) ** 2 * rtol * (ag + floor * ag.max())
-    return float((np.abs(got - want) / tol).max())
+    err = np.abs(got - want)
+    with np.errstate(divide="ignore", invalid="ignore"):  # (a zero bound passes only an exact match)
+        return float(np.where(err == 0, 0.0, err / tol).max())
 
 
 def ddp_errors(z, world, rank, loss, grads, params, tables=(), rows=None):

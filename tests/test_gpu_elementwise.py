@@ -5,6 +5,8 @@ test_gpu_models.py bounds every tensor by 1e-3 of its largest magnitude.  Here e
 than three decades below the tensor's scale, where fp32 summation order alone decides the low bits (a logit or
 gradient that is a near-cancelling sum): there the bound is an absolute 1e-6 of the tensor's max (~16 ulp of it).
 Measured (MI355X, every fixture): worst element 0.15 of the bound on the logits, 0.50 on the gradients.
+The parameters after the first Adam step are held element-wise too (helpers.adam_excess: the parameter's own bound
+plus what the gradient's element-wise bound moves lr * g / (|g| + eps) by -- the DDP tests' criterion).
 """
 import numpy as np
 import pytest
@@ -86,3 +88,37 @@ def test_train_grads_elementwise(asme, dev, name):
         worst = max(worst, (e, k))
         assert e <= 1.0, (k, e)
     print(f"{name}: worst gradient element-wise excess {worst[0]:.3f} ({worst[1]})")
+
+
+@pytest.mark.parametrize("name", MODEL_FIXTURES + D128_FIXTURES)
+def test_adam_step_elementwise(asme, dev, name):
+    """The parameters after the first optimizer step (the reference's torch Adam, L2-coupled weight decay; here
+    FusedAdam, the item table's lazy rows flushed), element by element: each within 1e-3 of its own magnitude plus what
+    the gradient's own element-wise bound moves Adam's first update lr * g / (|g| + eps) by (helpers.adam_excess, the
+    bound of the DDP tests) -- no max-relative comparison, no substituted or counted elements."""
+    from helpers import adam_excess
+    z = load(name)
+    model = build_model(asme, name, z)
+    model.load_state_dict(state_dict(z), strict=True)
+    model.to(dev)
+    V = int(z["cfg"][5] if name != "narm" else z["cfg"][4])
+    module = _module(asme, name, model, V)
+    module.training_step(_batch(name, z, dev), 0)["loss"].backward()
+    opt, sched = asme.modules.split_optimizers(module.configure_optimizers())
+    group_of = {id(p): g for g in opt.param_groups for p in g["params"]}
+    lr = float(opt.param_groups[0]["lr"])
+    opt.step()
+    opt.flush()
+    named = dict(model.named_parameters())
+    p0 = state_dict(z)
+    grads = prefixed(z, "grad")
+    worst = (0.0, "")
+    for k, want in prefixed(z, "adam1").items():
+        if _analytically_zero_grad(k):
+            continue
+        wd = float(group_of[id(named[k])]["weight_decay"])
+        g_total = grads[k] + wd * p0[k].numpy()
+        e = adam_excess(named[k].detach().cpu().numpy(), want, g_total, lr)
+        worst = max(worst, (e, k))
+        assert e <= 1.0, (k, e)
+    print(f"{name}: worst Adam-step element-wise excess {worst[0]:.3f} ({worst[1]})")
