@@ -988,8 +988,8 @@ def main():
                 result["workloads"][leg] = bench_sasrec(args, asme, dev, world, rank, "zipf", with_eval=False)
             elif leg == "sasrec_overlap":
                 # the headline step with the negative-only rows in a second, overlapped exchange (sharded.py
-                # overlap_negatives): only where rows cross the fabric (N > 1)
-                if world == 1:
+                # overlap_negatives): where rows cross the fabric (N > 1), or on a 1-rank RCCL group with --sharded
+                if world == 1 and not args.sharded:
                     continue
                 result["workloads"][leg] = bench_sasrec(args, asme, dev, world, rank, args.ids, with_eval=False,
                                                         overlap=True)
