@@ -372,12 +372,14 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
         meta["positive_samples"], meta["negative_samples"] = inv_pos, inv_neg
         padding_mask = get_padding_mask(input_seq, self.item_tokenizer)
         emb._table_override = compact
-        wait = None
+        wait, pending = None, []
         if st.work is not None:  # the negative-only rows are still arriving: the sampled head waits for them
-            work, st.work = st.work, None
+            pending.append(st.work)
+            st.work = None
 
             def _wait(module, args):  # (returns None: the head's inputs unchanged)
-                work.wait()
+                while pending:
+                    pending.pop().wait()
             wait = self.model._projection_layer.register_forward_pre_hook(_wait)
         try:
             pos_logits, neg_logits = self.model(InputSequence(inv_seq, padding_mask, meta))
@@ -385,6 +387,8 @@ class ShardedSequenceNextItemPredictionTrainingModule(SequenceNextItemPrediction
             emb._table_override = None
             if wait is not None:
                 wait.remove()
+            while pending:  # a forward that never reached the head (or raised): the exchange still completes here
+                pending.pop().wait()
         loss = self.loss_function(pos_logits, neg_logits, mask=padding_mask)
         self._pending = (st, own, compact, cplan)
         return {"loss": loss}
