@@ -41,6 +41,9 @@ __device__ __forceinline__ int tslot(int c, int s) {
 }
 
 typedef unsigned u32v2 __attribute__((ext_vector_type(2)));
+#ifndef ASME_WG_LOAD_AUX
+#define ASME_WG_LOAD_AUX 2  // operand loads non-temporal (each dY / X row is read once: weight gradient 1.5 % faster)
+#endif
 constexpr uint32_t kDrop = 0x80000000u;  // >= every chunk's record count: the load returns 0
 
 // rows 8 rg .. + 7 of a token block of this thread's column pair, by buffer loads against the chunk's record range:
@@ -52,7 +55,7 @@ __device__ __forceinline__ void load_cols(__amdgpu_buffer_rsrc_t rs, const uint3
                                           float2 (&r)[8]) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        const u32v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[q], soff, 0);
+        const u32v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[q], soff, ASME_WG_LOAD_AUX);
         r[q] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
     }
 }
