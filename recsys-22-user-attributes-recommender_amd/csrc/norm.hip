@@ -86,6 +86,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
 }
 
 // ------------------------------------------------------------ residual + dropout(s) + LayerNorm
+#ifndef ASME_RLNB_LOAD_NT
+#define ASME_RLNB_LOAD_NT 3  // residual_ln_bwd loads non-temporal (bit 0 the gradients, bit 1 the saved s): -4 % per call
+#endif
 #ifndef ASME_RLN_NT
 #define ASME_RLN_NT 3  // non-temporal stores in residual_ln_fwd (bit 0: s, bit 1: LN(s)) / _bwd (bit 2: d_res, bit 3: d_y)
 #endif
@@ -142,15 +145,15 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
         const bool live = t < T;
         RowVals<R> g;
         if (live && d_s)
-            row_load<R>(d_s + t * D, sub, D, g);
+            row_load_p<R, (ASME_RLNB_LOAD_NT & 1) != 0>(d_s + t * D, sub, D, g);
         else
             row_zero<R>(g);
         if (w && d_ln) {
             const float m = live ? stats[t * 2] : 0.f, r = live ? stats[t * 2 + 1] : 0.f;
             RowVals<R> v, xh, gl, gx;
             if (live) {
-                row_load<R>(s + t * D, sub, D, v);
-                row_load<R>(d_ln + t * D, sub, D, gl);
+                row_load_p<R, (ASME_RLNB_LOAD_NT & 2) != 0>(s + t * D, sub, D, v);
+                row_load_p<R, (ASME_RLNB_LOAD_NT & 1) != 0>(d_ln + t * D, sub, D, gl);
             } else {
                 row_zero<R>(v);
                 row_zero<R>(gl);

@@ -71,12 +71,20 @@ __device__ __forceinline__ void row_zero(RowVals<R>& x) {
         for (int i = 0; i < R::W; ++i) x[j][i] = 0.f;
 }
 
-template <class R>
-__device__ __forceinline__ void row_load(const float* __restrict__ p, int sub, int D, RowVals<R>& x) {
+// NT: non-temporal loads (rows read once)
+template <class R, bool NT>
+__device__ __forceinline__ void row_load_p(const float* __restrict__ p, int sub, int D, RowVals<R>& x) {
 #pragma unroll
     for (int j = 0; j < R::NV; ++j) {
         const int c = R::col(sub, j);
-        if constexpr (R::W == 4) {
+        if constexpr (R::W == 4 && NT) {
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v v = c < D ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p + c)) : f4v{0.f, 0.f, 0.f, 0.f};
+            x[j][0] = v.x;
+            x[j][1] = v.y;
+            x[j][2] = v.z;
+            x[j][3] = v.w;
+        } else if constexpr (R::W == 4) {
             const float4 v = c < D ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
             x[j][0] = v.x;
             x[j][1] = v.y;
@@ -86,6 +94,10 @@ __device__ __forceinline__ void row_load(const float* __restrict__ p, int sub, i
             x[j][0] = c < D ? p[c] : 0.f;
         }
     }
+}
+template <class R>
+__device__ __forceinline__ void row_load(const float* __restrict__ p, int sub, int D, RowVals<R>& x) {
+    row_load_p<R, false>(p, sub, D, x);
 }
 
 // NT: non-temporal (streaming) stores -- rows the next kernels read back from HBM anyway; a 1-read / 2-write row
