@@ -664,6 +664,9 @@ __global__ __launch_bounds__(256) ASME_EMB_BWD_ATTR void emb_bwd4_kernel(
 #ifndef ASME_EMB_BWD128_PF
 #define ASME_EMB_BWD128_PF 1
 #endif
+#ifndef ASME_EMB_BWD128_NT
+#define ASME_EMB_BWD128_NT 0  // (A/B) non-temporal loads: bit 0 the incoming gradients, bit 1 the gathered table rows
+#endif
 template <bool LN3, bool LN2, bool POS, bool DROP>  // POS: a position table; DROP: keep bytes given (some p > 0)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASME_EMB_BWD128_WPE, 8))) void emb_bwd128_kernel(
     const int64_t* __restrict__ ids, int64_t T, int64_t L, const float* __restrict__ table, int64_t V,
@@ -709,16 +712,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASME_EMB_BW
     auto load_pass = [&](int64_t b, int64_t raw_id, PassIn& in) {
         const int64_t tt = tok_of(b);
         const int64_t id = (raw_id < 0 || raw_id >= V) ? 0 : raw_id;
-        row_load<R>(table + id * D, sub, D, in.x);
+        row_load_p<R, (ASME_EMB_BWD128_NT & 2) != 0>(table + id * D, sub, D, in.x);
         // (position t % L in 32-bit arithmetic where the token count allows: a 64-bit remainder is a ~40-instruction
         // sequence per pass)
         const int64_t pr = small ? (int64_t)((uint32_t)tt % (uint32_t)L) : tt % L;
         if constexpr (POS) row_load<R>(pos + pr * D, sub, D, in.q);
-        row_load<R>(dout + tt * D, sub, D, in.g);
+        row_load_p<R, (ASME_EMB_BWD128_NT & 1) != 0>(dout + tt * D, sub, D, in.g);
         in.st = *reinterpret_cast<const float4*>(stats + tt * 4);
         in.st3 = make_float2(0.f, 1.f);
         if constexpr (LN3) {
-            row_load<R>(l3.dln + tt * D, sub, D, in.dl);
+            row_load_p<R, (ASME_EMB_BWD128_NT & 1) != 0>(l3.dln + tt * D, sub, D, in.dl);
             in.st3 = *reinterpret_cast<const float2*>(l3.stats + tt * 2);
         }
         // (the lane's two keep bytes: one 16-bit load, as emb_keep_load; a p = 0 half is all 1s)
